@@ -1,0 +1,250 @@
+#!/usr/bin/env python3
+"""Benchmark: batched full sBayes log-likelihood evaluations on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[4], the roofline run, per GPU): synthetic 2000 sites x
+500 features x 10 states, 8 zones, 4 families (inheritance, C = 3), 256 chains per GPU
+(2048 over 8 GPUs), mixture likelihood = Likelihood.__call__(sample, caching=False)
+(sbayes/model.py:145-171) per chain.  One step = one batched evaluation of all 256
+resident chains (one likelihood launch + its 256-thread reduce launch).  Chains are
+sharded by rank (weak scaling, no collective in the timed loop); the timed region is
+bracketed by a barrier + device synchronize, and the max over ranks is reported.
+
+Inputs are resident in HBM before timing.  To keep the measurement an HBM one (the
+256 chains' parameters are 137 MB and would otherwise sit in the 256 MiB Infinity
+Cache), each step evaluates the next of --pool disjoint chain batches (default 4,
+548 MB in total), so every launch streams parameters that were evicted since their
+last use.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "likelihood-evals/sec + ESS/sec, 2000 sites×500 feat, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--chains", type=int, default=256, help="chains per GPU")
+    p.add_argument("--pool", type=int, default=4, help="disjoint chain batches cycled per step")
+    p.add_argument("--sites", type=int, default=2000)
+    p.add_argument("--features", type=int, default=500)
+    p.add_argument("--states", type=int, default=10)
+    p.add_argument("--zones", type=int, default=8)
+    p.add_argument("--families", type=int, default=4)
+    p.add_argument("--mode", choices=["mixture", "source"], default="mixture")
+    p.add_argument("--cpu-seconds", type=float, default=12.0,
+                   help="bounded CPU-baseline sample (0 disables)")
+    p.add_argument("--seed", type=int, default=5)
+    return p.parse_args()
+
+
+def make_shared(args, rng):
+    import numpy as np
+    N, F, S, Fam = args.sites, args.features, args.states, args.families
+    obs = rng.integers(0, S, size=(N, F)).astype(np.int8)
+    obs[rng.random((N, F)) < 0.02] = -1
+    fam = rng.integers(0, Fam, size=N).astype(np.uint8)
+    fam[rng.random(N) < 0.2] = 255
+    return obs, fam
+
+
+def make_chains_torch(args, n_chains, gen, dev):
+    """Chain states on the device: disjoint zones of N/(4Z) sites, Dirichlet(1) parameters."""
+    import torch
+    N, F, S, Z, Fam = args.sites, args.features, args.states, args.zones, args.families
+    C = 3
+
+    zone_size = max(1, N // (4 * max(Z, 1)))
+    perm = torch.argsort(torch.rand(n_chains, N, generator=gen, device=dev), dim=1)
+    zos = torch.full((n_chains, N), 255, dtype=torch.uint8, device=dev)
+    for z in range(Z):
+        idx = perm[:, z * zone_size:(z + 1) * zone_size]
+        zos.scatter_(1, idx, torch.full_like(idx, z, dtype=torch.uint8))
+    w = -torch.log(torch.rand(n_chains, F, C, generator=gen, device=dev, dtype=torch.float64))
+    w = w / w.sum(-1, keepdim=True)
+
+    def probs(*shape):
+        x = -torch.log(torch.rand(*shape, S, generator=gen, device=dev, dtype=torch.float64))
+        return x / x.sum(-1, keepdim=True)
+
+    pg = probs(n_chains, F)
+    pz = probs(n_chains, Z, F)
+    pf = probs(n_chains, Fam, F)
+    src = None
+    if args.mode == "source":  # allowed components only: global, zone where zoned, family where present
+        r = torch.rand(n_chains, N, F, generator=gen, device=dev)
+        src = torch.zeros(n_chains, N, F, dtype=torch.uint8, device=dev)
+        src[(zos[:, :, None] != 255) & (r > 0.5)] = 1
+        fam_t = torch.as_tensor(args._fam, device=dev)
+        src[(fam_t[None, :, None] != 255) & (r < 0.25)] = 2
+    return dict(zos=zos.contiguous(), w=w.contiguous(), pg=pg.contiguous(), pz=pz.contiguous(),
+                pf=pf.contiguous(), src=src)
+
+
+def algorithmic_bytes(args, B, source=False):
+    """bytes/eval = P + D/B; a launch of B chains moves B*P + D bytes."""
+    N, F, S, Z, Fam = args.sites, args.features, args.states, args.zones, args.families
+    C = 3
+    P = 8 * F * S * (1 + Z + Fam) + 8 * F * C + N + (N * F if source else 0)
+    D = N * F + N
+    return P, D, B * P + D
+
+
+def cpu_baseline(args, seconds):
+    """Time the numpy restatement of Likelihood.__call__ (oracle, kind 'port') on 1 core."""
+    import numpy as np
+    from oracle import lik_numpy
+    rng = np.random.default_rng(args.seed)
+    obs, fam = make_shared(args, rng)
+    N, F, S, Z, Fam = args.sites, args.features, args.states, args.zones, args.families
+    zos = np.full(N, 255, np.uint8)
+    perm = rng.permutation(N)
+    zs = max(1, N // (4 * max(Z, 1)))
+    for z in range(Z):
+        zos[perm[z * zs:(z + 1) * zs]] = z
+    w = rng.dirichlet(np.ones(3), size=F)
+    pg = rng.dirichlet(np.ones(S), size=F)
+    pz = rng.dirichlet(np.ones(S), size=(Z, F))
+    pf = rng.dirichlet(np.ones(S), size=(Fam, F))
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        lik_numpy.loglik(obs, fam, zos, w, pg, pz, pf, inheritance=True)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": n / el, "unit": "likelihood-evals/s", "cores": 1, "kind": "port",
+            "sample": f"numpy restatement of Likelihood.__call__(caching=False) (oracle/lik_numpy.py), "
+                      f"1 chain at {N}x{F}x{S}, Z={Z}, Fam={Fam}: {n} evals in {el:.1f} s, 1 thread"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus > 1 must be launched with torch.distributed.run")
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from contact_zones_amd.likelihood import LikelihoodEngine
+
+    rng = np.random.default_rng(args.seed)
+    obs, fam = make_shared(args, rng)  # replicated on every rank (1 MB)
+    args._fam = fam
+    eng = LikelihoodEngine(obs, fam, args.states, args.zones, args.families, True, device=local_rank)
+    stream = torch.cuda.current_stream()
+    eng.set_stream(stream.cuda_stream)
+
+    B = args.chains
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(args.seed * 1000003 + rank)  # chains differ per rank (global chain ids)
+    pool = [make_chains_torch(args, B, gen, dev) for _ in range(args.pool)]
+    out = torch.empty(args.pool, B, dtype=torch.float64, device=dev)
+    src_mode = args.mode == "source"
+
+    def step(i):
+        c = pool[i % args.pool]
+        eng.loglik_device(B, c["zos"].data_ptr(), c["w"].data_ptr(), c["pg"].data_ptr(),
+                          c["pz"].data_ptr(), c["pf"].data_ptr(),
+                          c["src"].data_ptr() if src_mode else 0, out[i % args.pool].data_ptr())
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for i in range(args.steps):
+        step(i)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ev_ms = ev0.elapsed_time(ev1)
+    if not torch.isfinite(out).all():
+        raise SystemExit("non-finite log-likelihood in bench")
+
+    t = torch.tensor([wall, ev_ms / 1e3], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall_max, ev_max = float(t[0]), float(t[1])
+
+    total_evals = B * args.steps * world
+    value = total_evals / wall_max
+    P, D, per_launch = algorithmic_bytes(args, B, src_mode)
+    launch_s = ev_ms / 1e3 / args.steps  # this rank's device time per step (lik + reduce launch)
+    achieved = per_launch / launch_s / 1e9
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "likelihood-evals/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": wall_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {
+                "workload": f"cfg5 roofline run: {args.sites} sites x {args.features} features x "
+                            f"{args.states} states, {args.zones} zones, {args.families} families, "
+                            f"{B} chains/GPU, {args.mode} log-likelihood, full evaluation per chain",
+                "chains_per_gpu": B,
+                "global_chains": B * world,
+                "mode": args.mode,
+                "pool_batches": args.pool,
+                "parallelism": f"chains sharded over {world} GPU(s)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": None,
+                "bytes_per_eval": P + D / B,
+                "bytes_per_launch": per_launch,
+                "launch_us": launch_s * 1e6,
+            },
+            "device_time_s": ev_max,
+        }
+        if world == 1 and args.cpu_seconds > 0:
+            line["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
+            line["speedup_vs_cpu"] = value / line["cpu_baseline"]["value"]
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

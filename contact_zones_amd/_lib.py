@@ -1,0 +1,72 @@
+"""ctypes binding of the in-tree HIP library contact_zones_amd/libsbz.so (include/sbz.h).
+
+There is no CPU fallback: if the library is missing or fails to load, importing the
+product path raises.  Build it with ``python -c "import __graft_entry__ as g; g.build()"``
+(or ``make -C contact_zones_amd/csrc``).
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsbz.so")
+
+SBZ_OK = 0
+SBZ_INHERITANCE = 1
+ERRORS = {-1: "SBZ_EINVAL", -2: "SBZ_EHIP", -3: "SBZ_ENOMEM", -4: "SBZ_ESTATE"}
+
+
+class SbzError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class sbz_dims(ctypes.Structure):
+    _fields_ = [("n_sites", ctypes.c_int32), ("n_features", ctypes.c_int32),
+                ("n_states", ctypes.c_int32), ("n_zones", ctypes.c_int32),
+                ("n_families", ctypes.c_int32), ("flags", ctypes.c_int32)]
+
+
+# name -> (restype, argtypes); every symbol declared in include/sbz.h
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+SIGNATURES = {
+    "sbz_version": (ctypes.c_char_p, []),
+    "sbz_device_count": (_I, []),
+    "sbz_open": (_I, [_I, ctypes.POINTER(sbz_dims), _P, _P, ctypes.POINTER(_P)]),
+    "sbz_close": (None, [_P]),
+    "sbz_last_error": (ctypes.c_char_p, [_P]),
+    "sbz_set_stream": (_I, [_P, _P]),
+    "sbz_synchronize": (_I, [_P]),
+    "sbz_loglik_batch": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "sbz_loglik_batch_device": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "sbz_device_alloc": (_I, [_P, ctypes.c_uint64, ctypes.POINTER(_P)]),
+    "sbz_device_free": (_I, [_P, _P]),
+    "sbz_memcpy_h2d": (_I, [_P, _P, _P, ctypes.c_uint64]),
+    "sbz_memcpy_d2h": (_I, [_P, _P, _P, ctypes.c_uint64]),
+    "sbz_lik_lds_bytes": (ctypes.c_uint64, [ctypes.POINTER(sbz_dims), _I]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libsbz.so once (raises if it is missing: there is no fallback path)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} not built: run `make -C contact_zones_amd/csrc` "
+                              "(or __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc, ctx=None):
+    if rc != SBZ_OK:
+        msg = lib().sbz_last_error(ctx).decode() if ctx else ""
+        raise SbzError(rc, msg)

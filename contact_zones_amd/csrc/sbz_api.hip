@@ -1,0 +1,274 @@
+// sbz_api.hip — C-ABI entry points of include/sbz.h (context, memory, likelihood).
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "sbz_internal.h"
+
+#define SBZ_VERSION "sbz 0.1.0 (gfx950)"
+
+namespace sbz {
+
+int fail(sbz_ctx *ctx, int code, const std::string &msg) {
+    if (ctx) ctx->err = msg;
+    return code;
+}
+
+int hip_fail(sbz_ctx *ctx, hipError_t e, const char *what) {
+    return fail(ctx, SBZ_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+int ensure(sbz_ctx *ctx, DevBuf &buf, size_t bytes) {
+    if (buf.bytes >= bytes && buf.ptr) return SBZ_OK;
+    if (buf.ptr) {
+        hipStreamSynchronize(ctx->stream);
+        hipFree(buf.ptr);
+        buf.ptr = nullptr;
+        buf.bytes = 0;
+    }
+    const size_t want = std::max<size_t>(bytes, 256);
+    hipError_t e = hipMalloc(&buf.ptr, want);
+    if (e != hipSuccess) {
+        buf.ptr = nullptr;
+        return fail(ctx, SBZ_ENOMEM, std::string("hipMalloc(") + std::to_string(want) +
+                                         "): " + hipGetErrorString(e));
+    }
+    buf.bytes = want;
+    return SBZ_OK;
+}
+
+static void free_buf(DevBuf &b) {
+    if (b.ptr) hipFree(b.ptr);
+    b.ptr = nullptr;
+    b.bytes = 0;
+}
+
+static int check_dims(sbz_ctx *ctx, const sbz_dims *d) {
+    if (!d) return fail(ctx, SBZ_EINVAL, "dims is NULL");
+    if (d->n_sites <= 0 || d->n_features <= 0)
+        return fail(ctx, SBZ_EINVAL, "n_sites and n_features must be positive");
+    if (d->n_states < 1 || d->n_states > 127)
+        return fail(ctx, SBZ_EINVAL, "n_states must be in 1..127");
+    if (d->n_zones < 0 || d->n_zones > 254) return fail(ctx, SBZ_EINVAL, "n_zones must be in 0..254");
+    if (d->n_families < 0 || d->n_families > 254)
+        return fail(ctx, SBZ_EINVAL, "n_families must be in 0..254");
+    return SBZ_OK;
+}
+
+}  // namespace sbz
+
+using namespace sbz;
+
+extern "C" {
+
+const char *sbz_version(void) { return SBZ_VERSION; }
+
+int sbz_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char *sbz_last_error(const sbz_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int sbz_open(int device, const sbz_dims *dims, const int8_t *obs, const uint8_t *fam_of_site,
+             sbz_ctx **out) {
+    if (!out) return SBZ_EINVAL;
+    *out = nullptr;
+    sbz_ctx *ctx = new (std::nothrow) sbz_ctx();
+    if (!ctx) return SBZ_ENOMEM;
+    int rc = check_dims(ctx, dims);
+    if (rc) {
+        delete ctx;
+        return rc;
+    }
+    if (!obs) {
+        delete ctx;
+        return SBZ_EINVAL;
+    }
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) {
+        delete ctx;
+        return SBZ_EHIP;
+    }
+    ctx->device = device;
+    ctx->d = *dims;
+    const bool inh = (dims->flags & SBZ_INHERITANCE) != 0;
+    ctx->C = inh ? 3 : 2;
+    ctx->FamC = inh ? dims->n_families + 1 : 1;
+    ctx->T = (dims->n_features + FT - 1) / FT;
+    e = hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete ctx;
+        return SBZ_EHIP;
+    }
+    ctx->stream = ctx->own_stream;
+
+    const int N = dims->n_sites, F = dims->n_features, S = dims->n_states, T = ctx->T;
+    // obs -> tiled [T][N][FT], x in 0..S (S = NA), padded features 0; validate states.
+    std::vector<uint8_t> obs_t((size_t)T * N * FT, 0);
+    for (int s = 0; s < N; s++)
+        for (int f = 0; f < F; f++) {
+            const int x = obs[(size_t)s * F + f];
+            if (x >= S) {
+                sbz_close(ctx);
+                return SBZ_EINVAL;
+            }
+            obs_t[((size_t)(f / FT) * N + s) * FT + (f % FT)] = (uint8_t)(x < 0 ? S : x);
+        }
+    std::vector<uint8_t> famc(N, 0);
+    if (inh && fam_of_site) {
+        for (int s = 0; s < N; s++) {
+            const int fam = fam_of_site[s];
+            if (fam != SBZ_NONE && fam >= dims->n_families) {
+                sbz_close(ctx);
+                return SBZ_EINVAL;
+            }
+            famc[s] = fam == SBZ_NONE ? 0 : (uint8_t)(fam + 1);
+        }
+    }
+    if (hipMalloc(&ctx->d_obs_t, obs_t.size()) != hipSuccess ||
+        hipMalloc(&ctx->d_famc, famc.size()) != hipSuccess) {
+        sbz_close(ctx);
+        return SBZ_ENOMEM;
+    }
+    if (hipMemcpy(ctx->d_obs_t, obs_t.data(), obs_t.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(ctx->d_famc, famc.data(), famc.size(), hipMemcpyHostToDevice) != hipSuccess) {
+        sbz_close(ctx);
+        return SBZ_EHIP;
+    }
+    // Allow the likelihood kernels their full dynamic LDS table.
+    rc = lik_configure(ctx);
+    if (rc) {
+        sbz_close(ctx);
+        return rc;
+    }
+    *out = ctx;
+    return SBZ_OK;
+}
+
+void sbz_close(sbz_ctx *ctx) {
+    if (!ctx) return;
+    if (ctx->own_stream) hipStreamSynchronize(ctx->own_stream);
+    if (ctx->stream && ctx->stream != ctx->own_stream) hipStreamSynchronize(ctx->stream);
+    if (ctx->d_obs_t) hipFree(ctx->d_obs_t);
+    if (ctx->d_famc) hipFree(ctx->d_famc);
+    free_buf(ctx->partial);
+    free_buf(ctx->src_t);
+    free_buf(ctx->stage);
+    free_buf(ctx->out);
+    if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
+    delete ctx;
+}
+
+int sbz_set_stream(sbz_ctx *ctx, void *hip_stream) {
+    if (!ctx) return SBZ_EINVAL;
+    ctx->stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->own_stream;
+    return SBZ_OK;
+}
+
+int sbz_synchronize(sbz_ctx *ctx) {
+    if (!ctx) return SBZ_EINVAL;
+    hipError_t e = hipStreamSynchronize(ctx->stream);
+    return e == hipSuccess ? SBZ_OK : hip_fail(ctx, e, "hipStreamSynchronize");
+}
+
+uint64_t sbz_lik_lds_bytes(const sbz_dims *dims, int source_mode) {
+    if (!dims) return 0;
+    const size_t b = lik_lds_bytes(*dims, source_mode != 0);
+    return b > 160 * 1024 ? 0 : b;
+}
+
+int sbz_loglik_batch_device(sbz_ctx *ctx, int B, const uint8_t *zone_of_site, const double *w,
+                            const double *p_global, const double *p_zones, const double *p_fam,
+                            const uint8_t *source, double *out_ll) {
+    if (!ctx) return SBZ_EINVAL;
+    if (B < 0 || !zone_of_site || !w || !p_global || !out_ll ||
+        (ctx->d.n_zones > 0 && !p_zones))
+        return fail(ctx, SBZ_EINVAL, "null argument or negative B");
+    hipSetDevice(ctx->device);
+    return launch_loglik(ctx, B, zone_of_site, w, p_global, p_zones, p_fam, source, out_ll);
+}
+
+int sbz_loglik_batch(sbz_ctx *ctx, int B, const uint8_t *zone_of_site, const double *w,
+                     const double *p_global, const double *p_zones, const double *p_fam,
+                     const uint8_t *source, double *out_ll) {
+    if (!ctx) return SBZ_EINVAL;
+    if (B < 0 || !zone_of_site || !w || !p_global || !out_ll ||
+        (ctx->d.n_zones > 0 && !p_zones))
+        return fail(ctx, SBZ_EINVAL, "null argument or negative B");
+    if (B == 0) return SBZ_OK;
+    hipSetDevice(ctx->device);
+    const sbz_dims &d = ctx->d;
+    const size_t N = d.n_sites, F = d.n_features, S = d.n_states, Z = d.n_zones,
+                 Fam = d.n_families, C = ctx->C;
+    const bool inh = C == 3;
+    if (inh && Fam > 0 && !p_fam) return fail(ctx, SBZ_EINVAL, "p_fam is required with inheritance");
+    // host-side validation of the indices the kernels trust
+    for (size_t i = 0; i < (size_t)B * N; i++)
+        if (zone_of_site[i] != SBZ_NONE && zone_of_site[i] >= Z)
+            return fail(ctx, SBZ_EINVAL, "zone_of_site holds an index >= n_zones");
+    if (source)
+        for (size_t i = 0; i < (size_t)B * N * F; i++)
+            if (source[i] >= C) return fail(ctx, SBZ_EINVAL, "source holds a component index >= C");
+
+    const size_t bz = B * N, bw = B * F * C * 8, bg = B * F * S * 8, bpz = B * Z * F * S * 8,
+                 bpf = inh ? B * Fam * F * S * 8 : 0, bs = source ? B * N * F : 0;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t o_w = 0, o_g = o_w + al(bw), o_z = o_g + al(bg), o_f = o_z + al(bpz),
+                 o_zone = o_f + al(bpf), o_src = o_zone + al(bz), total = o_src + al(bs);
+    int rc = ensure(ctx, ctx->stage, total);
+    if (rc) return rc;
+    rc = ensure(ctx, ctx->out, (size_t)B * 8);
+    if (rc) return rc;
+    char *base = static_cast<char *>(ctx->stage.ptr);
+    hipStream_t st = ctx->stream;
+    hipError_t e = hipMemcpyAsync(base + o_w, w, bw, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(base + o_g, p_global, bg, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess && bpz) e = hipMemcpyAsync(base + o_z, p_zones, bpz, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess && bpf) e = hipMemcpyAsync(base + o_f, p_fam, bpf, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(base + o_zone, zone_of_site, bz, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess && bs) e = hipMemcpyAsync(base + o_src, source, bs, hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipMemcpyAsync H2D");
+    rc = launch_loglik(ctx, B, reinterpret_cast<uint8_t *>(base + o_zone),
+                       reinterpret_cast<double *>(base + o_w), reinterpret_cast<double *>(base + o_g),
+                       reinterpret_cast<double *>(base + o_z),
+                       inh ? reinterpret_cast<double *>(base + o_f) : nullptr,
+                       source ? reinterpret_cast<uint8_t *>(base + o_src) : nullptr,
+                       static_cast<double *>(ctx->out.ptr));
+    if (rc) return rc;
+    e = hipMemcpyAsync(out_ll, ctx->out.ptr, (size_t)B * 8, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return hip_fail(ctx, e, "likelihood D2H");
+    return SBZ_OK;
+}
+
+int sbz_device_alloc(sbz_ctx *ctx, uint64_t bytes, void **out) {
+    if (!ctx || !out) return SBZ_EINVAL;
+    hipSetDevice(ctx->device);
+    hipError_t e = hipMalloc(out, std::max<uint64_t>(bytes, 1));
+    return e == hipSuccess ? SBZ_OK : fail(ctx, SBZ_ENOMEM, hipGetErrorString(e));
+}
+
+int sbz_device_free(sbz_ctx *ctx, void *ptr) {
+    if (!ctx) return SBZ_EINVAL;
+    hipError_t e = hipFree(ptr);
+    return e == hipSuccess ? SBZ_OK : hip_fail(ctx, e, "hipFree");
+}
+
+int sbz_memcpy_h2d(sbz_ctx *ctx, void *dst, const void *src, uint64_t bytes) {
+    if (!ctx) return SBZ_EINVAL;
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    return e == hipSuccess ? SBZ_OK : hip_fail(ctx, e, "h2d");
+}
+
+int sbz_memcpy_d2h(sbz_ctx *ctx, void *dst, const void *src, uint64_t bytes) {
+    if (!ctx) return SBZ_EINVAL;
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    return e == hipSuccess ? SBZ_OK : hip_fail(ctx, e, "d2h");
+}
+
+}  // extern "C"

@@ -1,0 +1,176 @@
+"""GPU likelihood: batched engine + drop-in for ``sbayes.model.Likelihood``.
+
+``LikelihoodEngine`` owns one sbz context (one GPU) holding the shared data
+(observations, family membership) and evaluates the full log-likelihood of B
+chains per call (``sbz_loglik_batch`` / ``sbz_loglik_batch_device``).
+
+``GpuLikelihood(data, inheritance)`` mirrors the reference interface
+``Likelihood(data, inheritance)`` / ``__call__(sample, caching=True) -> float``
+(sbayes/model.py:69-171): same constructor arguments, same attributes the
+operators read (``na_features``, ``has_family``, ``n_sites`` ...), same call
+semantics.  The reference caches component likelihoods behind the sample's
+``what_changed`` flags; every GPU evaluation is a full, stateless evaluation
+(equal to the cached one by construction), after which the ``lh`` flags are
+cleared exactly as ``Likelihood.everything_updated`` does (model.py:186-192).
+"""
+import ctypes
+
+import numpy as np
+
+from . import packing
+from ._lib import SBZ_INHERITANCE, check, lib, sbz_dims
+
+
+def _ptr(a):
+    return None if a is None else ctypes.c_void_p(a.ctypes.data)
+
+
+class LikelihoodEngine:
+    """Batched full log-likelihood on one MI355X (sbz C-ABI context)."""
+
+    def __init__(self, obs, fam_of_site, n_states, n_zones, n_families, inheritance, device=0):
+        obs = np.ascontiguousarray(obs, dtype=np.int8)
+        n_sites, n_features = obs.shape
+        if fam_of_site is None:
+            fam_of_site = np.full(n_sites, packing.NONE, np.uint8)
+        self.fam_of_site = np.ascontiguousarray(fam_of_site, dtype=np.uint8)
+        self.inheritance = bool(inheritance)
+        self.dims = sbz_dims(n_sites, n_features, int(n_states), int(n_zones),
+                             int(n_families) if inheritance else 0,
+                             SBZ_INHERITANCE if inheritance else 0)
+        self.n_sites, self.n_features, self.n_states = n_sites, n_features, int(n_states)
+        self.n_zones = int(n_zones)
+        self.n_families = int(n_families) if inheritance else 0
+        self.n_components = 3 if inheritance else 2
+        self._lib = lib()
+        ctx = ctypes.c_void_p()
+        check(self._lib.sbz_open(int(device), ctypes.byref(self.dims), _ptr(obs),
+                                 _ptr(self.fam_of_site), ctypes.byref(ctx)))
+        self.ctx = ctx
+        self.device = device
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self._lib.sbz_close(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, hip_stream):
+        check(self._lib.sbz_set_stream(self.ctx, ctypes.c_void_p(hip_stream or 0)), self.ctx)
+
+    def synchronize(self):
+        check(self._lib.sbz_synchronize(self.ctx), self.ctx)
+
+    def lds_bytes(self, source_mode=False):
+        return int(self._lib.sbz_lik_lds_bytes(ctypes.byref(self.dims), int(bool(source_mode))))
+
+    def _check_shapes(self, B, zone_of_site, w, p_global, p_zones, p_fam, source):
+        N, F, S, Z, C = self.n_sites, self.n_features, self.n_states, self.n_zones, self.n_components
+        exp = {"zone_of_site": (zone_of_site, (B, N)), "w": (w, (B, F, C)),
+               "p_global": (p_global, (B, F, S)), "p_zones": (p_zones, (B, Z, F, S))}
+        if self.inheritance:
+            exp["p_fam"] = (p_fam, (B, self.n_families, F, S))
+        if source is not None:
+            exp["source"] = (source, (B, N, F))
+        for name, (arr, shape) in exp.items():
+            if arr is None or tuple(arr.shape) != shape:
+                raise ValueError(f"{name}: expected shape {shape}, got "
+                                 f"{None if arr is None else tuple(arr.shape)}")
+
+    def loglik(self, zone_of_site, w, p_global, p_zones, p_fam=None, source=None):
+        """Full log-likelihood of B chains from host arrays; returns float64 (B,)."""
+        zone_of_site = np.ascontiguousarray(zone_of_site, dtype=np.uint8)
+        B = zone_of_site.shape[0]
+        w = np.ascontiguousarray(w, dtype=np.float64)
+        p_global = np.ascontiguousarray(p_global, dtype=np.float64)
+        p_zones = np.ascontiguousarray(p_zones, dtype=np.float64)
+        if self.inheritance:
+            p_fam = np.ascontiguousarray(p_fam, dtype=np.float64)
+        else:
+            p_fam = None
+        if source is not None:
+            source = np.ascontiguousarray(source, dtype=np.uint8)
+        self._check_shapes(B, zone_of_site, w, p_global, p_zones, p_fam, source)
+        out = np.empty(B, dtype=np.float64)
+        check(self._lib.sbz_loglik_batch(self.ctx, B, _ptr(zone_of_site), _ptr(w), _ptr(p_global),
+                                         _ptr(p_zones), _ptr(p_fam), _ptr(source), _ptr(out)),
+              self.ctx)
+        return out
+
+    def loglik_device(self, B, zone_of_site, w, p_global, p_zones, p_fam, source, out_ll):
+        """Device-pointer variant (ints = device addresses, 0 for None); async on the stream."""
+        v = ctypes.c_void_p
+        check(self._lib.sbz_loglik_batch_device(self.ctx, int(B), v(zone_of_site), v(w), v(p_global),
+                                                v(p_zones), v(p_fam or 0), v(source or 0),
+                                                v(out_ll)), self.ctx)
+
+
+def pack_sample(sample, n_sites):
+    """Reference ``Sample`` (zone_sampling.py:49-115) -> packed per-chain arrays."""
+    zones = sample.zones
+    zone_of_site = packing.zones_to_zone_of_site(zones, n_sites)
+    p_global = np.asarray(sample.p_global)
+    if p_global.ndim == 3:
+        p_global = p_global[0]
+    src = None if sample.source is None else packing.source_to_index(sample.source)
+    pf = None if sample.p_families is None else np.asarray(sample.p_families, np.float64)
+    return (zone_of_site, np.asarray(sample.weights, np.float64), np.asarray(p_global, np.float64),
+            np.asarray(sample.p_zones, np.float64), pf, src)
+
+
+class GpuLikelihood:
+    """Drop-in for ``sbayes.model.Likelihood`` (sbayes/model.py:69-171) evaluated on the GPU."""
+
+    def __init__(self, data, inheritance, device=0, n_zones=None):
+        self.features = data.features
+        self.families = np.asarray(data.families, dtype=bool)
+        self.inheritance = inheritance
+        self.n_sites, self.n_features, self.n_categories = data.features.shape
+        self.na_features = (np.sum(self.features, axis=-1) == 0)
+        self.has_global = np.ones(self.n_sites, dtype=bool)
+        self.has_family = np.any(self.families, axis=0) if self.families.size else \
+            np.zeros(self.n_sites, bool)
+        self._obs = packing.features_to_obs(self.features)
+        n_fam = self.families.shape[0] if self.families.ndim == 2 else 0
+        self._fam = packing.families_to_fam_of_site(self.families if n_fam else None, self.n_sites)
+        self._n_families = n_fam
+        self._device = device
+        self._engine = None
+        self._engine_zones = n_zones
+
+    def _engine_for(self, n_zones):
+        if self._engine is None or self._engine.n_zones != n_zones:
+            if self._engine is not None:
+                self._engine.close()
+            self._engine = LikelihoodEngine(self._obs, self._fam, self.n_categories, n_zones,
+                                            self._n_families, self.inheritance, self._device)
+        return self._engine
+
+    def reset_cache(self):
+        """No device-side cache to reset: every evaluation is a full evaluation."""
+
+    def __call__(self, sample, caching=True):
+        zone_of_site, w, pg, pz, pf, src = pack_sample(sample, self.n_sites)
+        eng = self._engine_for(pz.shape[0])
+        ll = eng.loglik(zone_of_site[None], w[None], pg[None], pz[None],
+                        None if pf is None else pf[None], None if src is None else src[None])[0]
+        self.everything_updated(sample)
+        return float(ll)
+
+    def everything_updated(self, sample):
+        """Clear the 'lh' dirty flags exactly as the reference does (model.py:186-192)."""
+        wc = getattr(sample, "what_changed", None)
+        if not wc:
+            return
+        lh = wc["lh"]
+        lh["zones"].clear()
+        lh["p_global"].clear()
+        lh["p_zones"].clear()
+        lh["weights"] = False
+        if self.inheritance:
+            lh["p_families"].clear()

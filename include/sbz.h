@@ -1,0 +1,119 @@
+/*
+ * sbz.h — C-ABI of the MI355X-native sBayes likelihood + sampler core.
+ *
+ * The reference (sBayes, Python) has no native boundary: its hot path is called
+ * in-process.  The entry points below are exactly what a ctypes binding on the
+ * reference side would bind to replace that path (INTEGRATION.md shows the stub):
+ *
+ *   sbz_loglik_batch / sbz_loglik_batch_device
+ *       replaces  Likelihood.__call__(sample, caching=False)      sbayes/model.py:145-171
+ *       (incl.    update_component_likelihoods :230-249, update_weights :257-294,
+ *                 normalize_weights :436-452, combine_lh :173-184)  — B chains per call
+ *   sbz_mh_*
+ *       replaces  MCMCGenerative.step / generate_samples           sbayes/sampling/mcmc_generative.py:149-351
+ *       with the  operators of ZoneMCMC / ZoneMCMCWarmup           sbayes/sampling/zone_sampling.py:408-933,1272-1577
+ *
+ * Conventions
+ *   - Return 0 (SBZ_OK) on success, a negative SBZ_E* code otherwise; the message is
+ *     available from sbz_last_error(ctx).  No exceptions cross the ABI.  A log-likelihood
+ *     of -inf is a value, not an error (combine_lh source branch, sbayes/model.py:181-182).
+ *   - Host arrays are borrowed for the duration of the call, C-contiguous, in the layouts
+ *     documented per argument.  Device arrays (the *_device entry points) must be device
+ *     pointers valid on ctx's device; those calls are asynchronous on ctx's stream.
+ *   - One context per GPU per process; calls on one context must be serialised.
+ *
+ * Layouts (B = chains in the call, N sites, F features, S states, Z zones, Fam families,
+ * C = 3 with inheritance else 2):
+ *   obs          int8   [N][F]        state index 0..S-1, -1 = NA         (one-hot features, util.py:289-336)
+ *   fam_of_site  uint8  [N]           family index, 255 = no family       (families (Fam,N), disjoint)
+ *   zone_of_site uint8  [B][N]        zone index, 255 = no zone           (zones (Z,N), disjoint)
+ *   w            double [B][F][C]     unnormalised mixture weights         (Sample.weights)
+ *   p_global     double [B][F][S]                                          (Sample.p_global[0])
+ *   p_zones      double [B][Z][F][S]                                       (Sample.p_zones)
+ *   p_fam        double [B][Fam][F][S] or NULL without inheritance         (Sample.p_families)
+ *   source       uint8  [B][N][F]     component index per cell, or NULL   (Sample.source one-hot -> index)
+ */
+#ifndef SBZ_H
+#define SBZ_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SBZ_NONE 255
+
+enum sbz_status {
+    SBZ_OK = 0,
+    SBZ_EINVAL = -1,   /* bad argument / shape */
+    SBZ_EHIP = -2,     /* HIP runtime error */
+    SBZ_ENOMEM = -3,   /* device allocation failed */
+    SBZ_ESTATE = -4,   /* call out of order (e.g. no chains resident) */
+};
+
+enum sbz_flags {
+    SBZ_INHERITANCE = 1, /* model families: C = 3 components (Model.inheritance, model.py:45) */
+};
+
+typedef struct sbz_dims {
+    int32_t n_sites;
+    int32_t n_features;
+    int32_t n_states;   /* max states over features (S), <= 127 */
+    int32_t n_zones;    /* Z, 0..254 */
+    int32_t n_families; /* Fam, 0..254 (ignored without SBZ_INHERITANCE) */
+    int32_t flags;      /* SBZ_INHERITANCE */
+} sbz_dims;
+
+typedef struct sbz_ctx sbz_ctx;
+
+/* Library version string. */
+const char *sbz_version(void);
+
+/* Number of visible HIP devices (0 if none); never fails. */
+int sbz_device_count(void);
+
+/*
+ * Open a context on `device`, uploading the shared data once (obs, fam_of_site).
+ * Replaces the per-chain Model copies' shared Likelihood state
+ * (Likelihood.__init__, sbayes/model.py:105-131; mcmc_generative.py:80).
+ */
+int sbz_open(int device, const sbz_dims *dims, const int8_t *obs, const uint8_t *fam_of_site,
+             sbz_ctx **out);
+void sbz_close(sbz_ctx *ctx);
+const char *sbz_last_error(const sbz_ctx *ctx);
+
+/* Use `hip_stream` (a hipStream_t, e.g. torch.cuda.current_stream().cuda_stream) for
+ * every subsequent launch; NULL restores the context's own stream. */
+int sbz_set_stream(sbz_ctx *ctx, void *hip_stream);
+int sbz_synchronize(sbz_ctx *ctx);
+
+/*
+ * Full log-likelihood of B chains, host buffers (PCIe copies included; blocks until done).
+ * source == NULL: mixture branch  sum_{s,f} log sum_c w_norm*lh      (model.py:174-176)
+ * source != NULL: source branch   sum_{s,f} log (w_norm*lh)[source]  (model.py:177-184)
+ * out_ll: double[B] (host).
+ */
+int sbz_loglik_batch(sbz_ctx *ctx, int B, const uint8_t *zone_of_site, const double *w,
+                     const double *p_global, const double *p_zones, const double *p_fam,
+                     const uint8_t *source, double *out_ll);
+
+/* Same, all pointers on the device (out_ll: double[B] device); asynchronous on ctx's stream. */
+int sbz_loglik_batch_device(sbz_ctx *ctx, int B, const uint8_t *zone_of_site, const double *w,
+                            const double *p_global, const double *p_zones, const double *p_fam,
+                            const uint8_t *source, double *out_ll);
+
+/* Device memory helpers (so a host without torch can stage device buffers). */
+int sbz_device_alloc(sbz_ctx *ctx, uint64_t bytes, void **out);
+int sbz_device_free(sbz_ctx *ctx, void *ptr);
+int sbz_memcpy_h2d(sbz_ctx *ctx, void *dst, const void *src, uint64_t bytes);
+int sbz_memcpy_d2h(sbz_ctx *ctx, void *dst, const void *src, uint64_t bytes);
+
+/* Bytes of LDS the likelihood kernel needs per workgroup for these dims (0 if unsupported). */
+uint64_t sbz_lik_lds_bytes(const sbz_dims *dims, int source_mode);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SBZ_H */

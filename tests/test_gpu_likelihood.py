@@ -1,0 +1,164 @@
+"""GPU parity: the HIP likelihood vs the reference's golden values and the oracle.
+
+Tolerance (north_star): log-likelihoods within 1e-9 relative of the reference CPU
+path.  Each table entry is computed in the reference's operation order, so the only
+difference is the reduction (product accumulation + one log per lane + fp64 tree
+sum); in practice the error is ~1e-15 relative.
+"""
+import numpy as np
+import pytest
+
+from conftest import golden_cases, load_golden
+
+pytestmark = pytest.mark.gpu
+
+REL_TOL = 1e-9
+CASES = golden_cases()
+
+
+def _engine(d, device=0):
+    from contact_zones_amd.likelihood import LikelihoodEngine
+    inh = bool(d["inheritance"])
+    Fam = d["p_fam"].shape[1] if inh else 0
+    return LikelihoodEngine(d["obs"], d["fam_of_site"], d["p_global"].shape[2],
+                            d["p_zones"].shape[1], Fam, inh, device)
+
+
+def _assert_close(got, ref, tol=REL_TOL):
+    got, ref = np.asarray(got), np.asarray(ref)
+    inf = ~np.isfinite(ref)
+    np.testing.assert_array_equal(got[inf], ref[inf])
+    fin = ~inf
+    rel = np.abs(got[fin] - ref[fin]) / np.abs(ref[fin])
+    assert rel.size == 0 or rel.max() <= tol, f"max rel err {rel.max():.3e}"
+    return 0.0 if rel.size == 0 else float(rel.max())
+
+
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("mode", ["mixture", "source"])
+def test_golden(gpu_available, case, mode):
+    d = load_golden(case)
+    eng = _engine(d)
+    src = d["source"] if mode == "source" else None
+    got = eng.loglik(d["zone_of_site"], d["w"], d["p_global"], d["p_zones"], d.get("p_fam"), src)
+    _assert_close(got, d["ll_" + mode])
+
+
+def test_known_answer(gpu_available):
+    from contact_zones_amd.likelihood import LikelihoodEngine
+    d = load_golden("lik_kat")
+    S = d["p_global"].shape[2]
+    e3 = LikelihoodEngine(d["obs"], d["fam_of_site"], S, 1, 1, True)
+    e2 = LikelihoodEngine(d["obs"], d["fam_of_site"], S, 1, 0, False)
+    lf = e3.loglik(d["zone_of_site"], d["w3"], d["p_global"], d["p_zones"], d["p_fam"])[0]
+    ln = e2.loglik(d["zone_of_site"], d["w2"], d["p_global"], d["p_zones"])[0]
+    assert lf == pytest.approx(float(d["lh_with_family"]), rel=1e-13)
+    assert ln == pytest.approx(float(d["lh_without_family"]), rel=1e-13)
+    assert lf == pytest.approx(float(d["lh_direct"]), rel=1e-12)
+
+
+def _random_batch(rng, N, F, S, Z, Fam, B, inheritance, zone_size, na=0.02):
+    obs = rng.integers(0, S, size=(N, F)).astype(np.int8)
+    obs[rng.random((N, F)) < na] = -1
+    fam = rng.integers(0, max(Fam, 1), size=N).astype(np.uint8)
+    fam[rng.random(N) < 0.2] = 255
+    if Fam == 0:
+        fam[:] = 255
+    zos = np.full((B, N), 255, np.uint8)
+    for b in range(B):
+        perm = rng.permutation(N)
+        for z in range(Z):
+            zos[b, perm[z * zone_size:(z + 1) * zone_size]] = z
+    C = 3 if inheritance else 2
+    w = rng.dirichlet(np.ones(C), size=(B, F))
+    pg = rng.dirichlet(np.ones(S), size=(B, F))
+    pz = rng.dirichlet(np.ones(S), size=(B, Z, F))
+    pf = rng.dirichlet(np.ones(S), size=(B, Fam, F)) if inheritance else None
+    src = rng.integers(0, 1, size=(B, N, F)).astype(np.uint8)
+    src[(zos[:, :, None] != 255) & (rng.random((B, N, F)) < 0.5)] = 1
+    if inheritance:
+        src[(fam[None, :, None] != 255) & (rng.random((B, N, F)) < 0.25)] = 2
+    return obs, fam, zos, w, pg, pz, pf, src
+
+
+@pytest.mark.parametrize("shape", [
+    (200, 100, 5, 2, 0, 64, False, 25),      # cfg2, 64 chains
+    (28, 47, 3, 3, 5, 256, True, 4),         # cfg3 shape, 256 chains
+    (100, 36, 5, 6, 6, 128, True, 6),        # cfg4 shape, 128 chains per GPU
+    (2000, 500, 10, 8, 4, 4, True, 62),      # cfg5 shape (few chains vs the C oracle)
+    (1000, 33, 7, 3, 2, 5, True, 100),       # ragged feature tile, odd S
+])
+@pytest.mark.parametrize("mode", ["mixture", "source"])
+def test_random_vs_c_oracle(gpu_available, shape, mode):
+    from contact_zones_amd.likelihood import LikelihoodEngine
+    from oracle import oracle_c
+    N, F, S, Z, Fam, B, inh, zs = shape
+    rng = np.random.default_rng(hash(shape) % 2**32)
+    obs, fam, zos, w, pg, pz, pf, src = _random_batch(rng, N, F, S, Z, Fam, B, inh, zs)
+    eng = LikelihoodEngine(obs, fam, S, Z, Fam, inh)
+    s = src if mode == "source" else None
+    got = eng.loglik(zos, w, pg, pz, pf, s)
+    ref = oracle_c.loglik_batch(obs, fam, zos, w, pg, pz, pf, source=s, inheritance=inh)
+    _assert_close(got, ref, tol=1e-12)
+
+
+def test_deterministic_and_chain_independent(gpu_available):
+    """Bit-identical re-runs; a chain's value does not depend on its batch neighbours."""
+    from contact_zones_amd.likelihood import LikelihoodEngine
+    rng = np.random.default_rng(7)
+    obs, fam, zos, w, pg, pz, pf, src = _random_batch(rng, 300, 70, 6, 3, 2, 16, True, 20)
+    eng = LikelihoodEngine(obs, fam, 6, 3, 2, True)
+    a = eng.loglik(zos, w, pg, pz, pf)
+    b = eng.loglik(zos, w, pg, pz, pf)
+    np.testing.assert_array_equal(a, b)
+    perm = rng.permutation(16)
+    c = eng.loglik(zos[perm], w[perm], pg[perm], pz[perm], pf[perm])
+    np.testing.assert_array_equal(c, a[perm])
+    one = eng.loglik(zos[3:4], w[3:4], pg[3:4], pz[3:4], pf[3:4])
+    np.testing.assert_array_equal(one, a[3:4])
+
+
+def test_device_pointer_path_matches_host_path(gpu_available):
+    import torch
+    from contact_zones_amd.likelihood import LikelihoodEngine
+    rng = np.random.default_rng(8)
+    obs, fam, zos, w, pg, pz, pf, src = _random_batch(rng, 500, 64, 8, 4, 3, 32, True, 30)
+    eng = LikelihoodEngine(obs, fam, 8, 4, 3, True)
+    host = eng.loglik(zos, w, pg, pz, pf, src)
+    dev = torch.device("cuda:0")
+    t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev)
+         for k, v in dict(zos=zos, w=w, pg=pg, pz=pz, pf=pf, src=src).items()}
+    out = torch.empty(32, dtype=torch.float64, device=dev)
+    eng.set_stream(torch.cuda.current_stream().cuda_stream)
+    eng.loglik_device(32, t["zos"].data_ptr(), t["w"].data_ptr(), t["pg"].data_ptr(),
+                      t["pz"].data_ptr(), t["pf"].data_ptr(), t["src"].data_ptr(), out.data_ptr())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy(), host)
+
+
+def test_drop_in_likelihood_interface(gpu_available):
+    """GpuLikelihood(data, inheritance)(sample, caching=False) on reference-form inputs."""
+    from collections import namedtuple
+    from contact_zones_amd import packing
+    from contact_zones_amd.likelihood import GpuLikelihood
+    d = load_golden("lik_cfg3_balkan")
+    S = d["p_global"].shape[2]
+    Fam = d["p_fam"].shape[1]
+    Data = namedtuple("Data", ["features", "families"])
+    data = Data(features=packing.obs_to_features(d["obs"], S),
+                families=packing.index_to_groups(d["fam_of_site"], Fam))
+
+    class Sample:  # the attributes Likelihood.__call__ reads (zone_sampling.py:49-93)
+        def __init__(self, b, source):
+            self.zones = packing.index_to_groups(d["zone_of_site"][b], d["p_zones"].shape[1])
+            self.weights = d["w"][b]
+            self.p_global = d["p_global"][b][None]
+            self.p_zones = d["p_zones"][b]
+            self.p_families = d["p_fam"][b]
+            self.source = packing.index_to_source(d["source"][b], 3) if source else None
+            self.what_changed = None
+
+    lik = GpuLikelihood(data, inheritance=True)
+    for b in range(d["zone_of_site"].shape[0]):
+        assert lik(Sample(b, False), caching=False) == pytest.approx(d["ll_mixture"][b], rel=1e-12)
+        assert lik(Sample(b, True)) == pytest.approx(d["ll_source"][b], rel=1e-12)
