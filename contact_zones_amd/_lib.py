@@ -8,7 +8,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsbz.so")
+LIB_PATH = os.environ.get("SBZ_LIB_PATH") or os.path.join(_HERE, "libsbz.so")
 
 SBZ_OK = 0
 SBZ_INHERITANCE = 1
@@ -54,6 +54,9 @@ def lib():
     """Load libsbz.so once (raises if it is missing: there is no fallback path)."""
     global _lib
     if _lib is None:
+        # The library links the HIP runtime PyTorch ships (torch/lib/libamdhip64.so, DT_RPATH);
+        # importing torch first guarantees a single HIP/HSA runtime in the process.
+        import torch  # noqa: F401
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} not built: run `make -C contact_zones_amd/csrc` "
                               "(or __graft_entry__.build())")

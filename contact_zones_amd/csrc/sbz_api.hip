@@ -1,5 +1,6 @@
 // sbz_api.hip — C-ABI entry points of include/sbz.h (context, memory, likelihood).
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -50,6 +51,8 @@ static int check_dims(sbz_ctx *ctx, const sbz_dims *d) {
         return fail(ctx, SBZ_EINVAL, "n_sites and n_features must be positive");
     if (d->n_states < 1 || d->n_states > 127)
         return fail(ctx, SBZ_EINVAL, "n_states must be in 1..127");
+    if ((size_t)d->n_sites * d->n_features > (size_t)1 << 31)
+        return fail(ctx, SBZ_EINVAL, "n_sites * n_features must be < 2^31");
     if (d->n_zones < 0 || d->n_zones > 254) return fail(ctx, SBZ_EINVAL, "n_zones must be in 0..254");
     if (d->n_families < 0 || d->n_families > 254)
         return fail(ctx, SBZ_EINVAL, "n_families must be in 0..254");
@@ -97,7 +100,12 @@ int sbz_open(int device, const sbz_dims *dims, const int8_t *obs, const uint8_t 
     const bool inh = (dims->flags & SBZ_INHERITANCE) != 0;
     ctx->C = inh ? 3 : 2;
     ctx->FamC = inh ? dims->n_families + 1 : 1;
-    ctx->T = (dims->n_features + FT - 1) / FT;
+    ctx->spl = sites_per_lane(dims->n_sites);
+    {
+        const int chunk = 64 * ctx->spl;
+        ctx->Np = (dims->n_sites + chunk - 1) / chunk * chunk;
+    }
+    ctx->xs8 = (dims->n_states + 1) * 8 <= 256 ? 1 : 0;
     e = hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete ctx;
@@ -105,9 +113,11 @@ int sbz_open(int device, const sbz_dims *dims, const int8_t *obs, const uint8_t 
     }
     ctx->stream = ctx->own_stream;
 
-    const int N = dims->n_sites, F = dims->n_features, S = dims->n_states, T = ctx->T;
-    // obs -> tiled [T][N][FT], x in 0..S (S = NA), padded features 0; validate states.
-    std::vector<uint8_t> obs_t((size_t)T * N * FT, 0);
+    const int N = dims->n_sites, F = dims->n_features, S = dims->n_states, Np = ctx->Np;
+    // obs -> feature-major [F][Np], x in 0..S (S = NA) stored as x*8 when it fits a byte;
+    // padded sites hold 0.  Validate the states.
+    std::vector<uint8_t> obs_fm((size_t)F * Np, 0);
+    const int scale = ctx->xs8 ? 8 : 1;
     for (int s = 0; s < N; s++)
         for (int f = 0; f < F; f++) {
             const int x = obs[(size_t)s * F + f];
@@ -115,9 +125,9 @@ int sbz_open(int device, const sbz_dims *dims, const int8_t *obs, const uint8_t 
                 sbz_close(ctx);
                 return SBZ_EINVAL;
             }
-            obs_t[((size_t)(f / FT) * N + s) * FT + (f % FT)] = (uint8_t)(x < 0 ? S : x);
+            obs_fm[(size_t)f * Np + s] = (uint8_t)((x < 0 ? S : x) * scale);
         }
-    std::vector<uint8_t> famc(N, 0);
+    std::vector<uint8_t> famc(Np, 0);
     if (inh && fam_of_site) {
         for (int s = 0; s < N; s++) {
             const int fam = fam_of_site[s];
@@ -128,12 +138,12 @@ int sbz_open(int device, const sbz_dims *dims, const int8_t *obs, const uint8_t 
             famc[s] = fam == SBZ_NONE ? 0 : (uint8_t)(fam + 1);
         }
     }
-    if (hipMalloc(&ctx->d_obs_t, obs_t.size()) != hipSuccess ||
+    if (hipMalloc(&ctx->d_obs_fm, obs_fm.size()) != hipSuccess ||
         hipMalloc(&ctx->d_famc, famc.size()) != hipSuccess) {
         sbz_close(ctx);
         return SBZ_ENOMEM;
     }
-    if (hipMemcpy(ctx->d_obs_t, obs_t.data(), obs_t.size(), hipMemcpyHostToDevice) != hipSuccess ||
+    if (hipMemcpy(ctx->d_obs_fm, obs_fm.data(), obs_fm.size(), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(ctx->d_famc, famc.data(), famc.size(), hipMemcpyHostToDevice) != hipSuccess) {
         sbz_close(ctx);
         return SBZ_EHIP;
@@ -151,11 +161,12 @@ int sbz_open(int device, const sbz_dims *dims, const int8_t *obs, const uint8_t 
 void sbz_close(sbz_ctx *ctx) {
     if (!ctx) return;
     if (ctx->own_stream) hipStreamSynchronize(ctx->own_stream);
-    if (ctx->stream && ctx->stream != ctx->own_stream) hipStreamSynchronize(ctx->stream);
-    if (ctx->d_obs_t) hipFree(ctx->d_obs_t);
+    if (ctx->stream != ctx->own_stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->d_obs_fm) (void)hipFree(ctx->d_obs_fm);
     if (ctx->d_famc) hipFree(ctx->d_famc);
     free_buf(ctx->partial);
     free_buf(ctx->src_t);
+    free_buf(ctx->cls);
     free_buf(ctx->stage);
     free_buf(ctx->out);
     if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
@@ -164,7 +175,7 @@ void sbz_close(sbz_ctx *ctx) {
 
 int sbz_set_stream(sbz_ctx *ctx, void *hip_stream) {
     if (!ctx) return SBZ_EINVAL;
-    ctx->stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->own_stream;
+    ctx->stream = static_cast<hipStream_t>(hip_stream);
     return SBZ_OK;
 }
 

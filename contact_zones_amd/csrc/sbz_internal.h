@@ -10,11 +10,6 @@
 
 namespace sbz {
 
-// Features per likelihood tile: one 16-byte observation row per site per tile.
-constexpr int FT = 16;
-// Threads per likelihood workgroup (4 waves).
-constexpr int LIK_BLOCK = 256;
-
 // Device buffer that grows on demand (kept for the context's lifetime).
 struct DevBuf {
     void *ptr = nullptr;
@@ -22,17 +17,22 @@ struct DevBuf {
 };
 
 struct LikArgs {
-    int N, F, S, Z, Fam, C, FamC, T;  // T = ceil(F / FT) feature tiles
+    int N, F, S, Z, Fam, C, FamC;
+    int Np;          // sites padded to a multiple of 64 * sites-per-lane
+    int W, fpw;      // tasks (single-wave workgroups) per chain, features per task
+    int xs8;         // obs bytes hold x*8 (S + 1 <= 32) instead of x
+    uint64_t s_magic;  // ceil(2^32 / S): slot element -> parameter row division
     int B;
-    const uint8_t *obs_t;   // [T][N][FT]  x in 0..S (S = NA); padded features hold 0
-    const uint8_t *famc;    // [N]  0 = no family (or no inheritance), fam + 1 otherwise
-    const uint8_t *zone;    // [B][N]  zone index, 255 = none
+    const uint8_t *obs_fm;  // [F][Np]  x (or x*8), x = S for NA; padded sites hold 0
+    const uint8_t *famc;    // [Np]     0 = no family (or no inheritance), fam + 1 otherwise
+    const uint8_t *zone;    // [B][N]   zone index, 255 = none
     const double *w;        // [B][F][C]
     const double *pg;       // [B][F][S]
     const double *pz;       // [B][Z][F][S]
     const double *pf;       // [B][Fam][F][S] (C == 3 only)
-    const uint8_t *src_t;   // [B][T][N][FT] component index per cell, or nullptr (mixture)
-    double *partial;        // [B][T]
+    const uint8_t *src_fm;  // [B][F][Np] component index per cell, or nullptr (mixture)
+    const uint8_t *cls;     // [B][Np]    site class bytes (mixture table kernel)
+    double *partial;        // [B][W]
 };
 
 }  // namespace sbz
@@ -40,12 +40,13 @@ struct LikArgs {
 struct sbz_ctx {
     int device = 0;
     sbz_dims d{};
-    int C = 2, FamC = 1, T = 0;
+    int C = 2, FamC = 1;
+    int Np = 0, spl = 4, xs8 = 0;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
-    uint8_t *d_obs_t = nullptr;
+    uint8_t *d_obs_fm = nullptr;
     uint8_t *d_famc = nullptr;
-    sbz::DevBuf partial, src_t, stage, out;
+    sbz::DevBuf partial, src_t, cls, stage, out;
     std::string err;
 };
 
@@ -59,6 +60,8 @@ int hip_fail(sbz_ctx *ctx, hipError_t e, const char *what);
 size_t lik_lds_bytes(const sbz_dims &d, bool source_mode);
 // Raise the dynamic-LDS limit of the likelihood kernels (gfx950: 160 KiB per workgroup).
 int lik_configure(sbz_ctx *ctx);
+// Sites per lane of the likelihood kernels for n_sites (4, 8, 16 or 32).
+int sites_per_lane(int n_sites);
 
 // Launch the likelihood kernels for B chains (all pointers device); out_ll device [B].
 int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, const double *pg,

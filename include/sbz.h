@@ -83,8 +83,9 @@ int sbz_open(int device, const sbz_dims *dims, const int8_t *obs, const uint8_t 
 void sbz_close(sbz_ctx *ctx);
 const char *sbz_last_error(const sbz_ctx *ctx);
 
-/* Use `hip_stream` (a hipStream_t, e.g. torch.cuda.current_stream().cuda_stream) for
- * every subsequent launch; NULL restores the context's own stream. */
+/* Use `hip_stream` (a hipStream_t, e.g. torch.cuda.current_stream().cuda_stream) verbatim for
+ * every subsequent launch; NULL is the device's legacy null stream.  A new context launches on
+ * a non-blocking stream of its own. */
 int sbz_set_stream(sbz_ctx *ctx, void *hip_stream);
 int sbz_synchronize(sbz_ctx *ctx);
 

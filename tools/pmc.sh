@@ -1,0 +1,18 @@
+#!/bin/bash
+# PMC passes for the likelihood kernel (each pass its own rocprofv3 run; --pmc never combined
+# with sys/runtime traces).  Usage: bash tools/pmc.sh [bench args...]
+set -u
+export TMPDIR=/tmp
+OUT=${PMC_OUT:-gpurun_out/pmc}
+mkdir -p $OUT
+ARGS="--steps 10 --warmup 2 --cpu-seconds 0 $*"
+i=0
+for pass in \
+  "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS" \
+  "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VMEM SQ_INSTS_SALU" \
+  "FETCH_SIZE GRBM_GUI_ACTIVE" \
+  "WRITE_SIZE TCC_HIT TCC_MISS" ; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $pass --kernel-trace -d $OUT/p$i -o run --output-format csv -- python3 bench.py $ARGS > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
+done
+python3 tools/pmc_summary.py $OUT
