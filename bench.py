@@ -40,6 +40,8 @@ def parse():
     p.add_argument("--states", type=int, default=10)
     p.add_argument("--zones", type=int, default=8)
     p.add_argument("--families", type=int, default=4)
+    p.add_argument("--zone-size", type=int, default=50,
+                   help="sites per zone (default: the reference's MAX_M, default_config.json:30)")
     p.add_argument("--mode", choices=["mixture", "source"], default="mixture")
     p.add_argument("--cpu-seconds", type=float, default=12.0,
                    help="bounded CPU-baseline sample (0 disables)")
@@ -58,12 +60,12 @@ def make_shared(args, rng):
 
 
 def make_chains_torch(args, n_chains, gen, dev):
-    """Chain states on the device: disjoint zones of N/(4Z) sites, Dirichlet(1) parameters."""
+    """Chain states on the device: disjoint zones of --zone-size sites, Dirichlet(1) parameters."""
     import torch
     N, F, S, Z, Fam = args.sites, args.features, args.states, args.zones, args.families
     C = 3
 
-    zone_size = max(1, N // (4 * max(Z, 1)))
+    zone_size = min(args.zone_size, N // max(Z, 1))
     perm = torch.argsort(torch.rand(n_chains, N, generator=gen, device=dev), dim=1)
     zos = torch.full((n_chains, N), 255, dtype=torch.uint8, device=dev)
     for z in range(Z):
@@ -108,7 +110,7 @@ def cpu_baseline(args, seconds):
     N, F, S, Z, Fam = args.sites, args.features, args.states, args.zones, args.families
     zos = np.full(N, 255, np.uint8)
     perm = rng.permutation(N)
-    zs = max(1, N // (4 * max(Z, 1)))
+    zs = min(args.zone_size, N // max(Z, 1))
     for z in range(Z):
         zos[perm[z * zs:(z + 1) * zs]] = z
     w = rng.dirichlet(np.ones(3), size=F)

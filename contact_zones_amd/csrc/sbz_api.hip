@@ -97,6 +97,9 @@ int sbz_open(int device, const sbz_dims *dims, const int8_t *obs, const uint8_t 
     }
     ctx->device = device;
     ctx->d = *dims;
+    if (hipDeviceGetAttribute(&ctx->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+        ctx->n_cu <= 0)
+        ctx->n_cu = 256;
     const bool inh = (dims->flags & SBZ_INHERITANCE) != 0;
     ctx->C = inh ? 3 : 2;
     ctx->FamC = inh ? dims->n_families + 1 : 1;
@@ -114,20 +117,8 @@ int sbz_open(int device, const sbz_dims *dims, const int8_t *obs, const uint8_t 
     ctx->stream = ctx->own_stream;
 
     const int N = dims->n_sites, F = dims->n_features, S = dims->n_states, Np = ctx->Np;
-    // obs -> feature-major [F][Np], x in 0..S (S = NA) stored as x*8 when it fits a byte;
-    // padded sites hold 0.  Validate the states.
-    std::vector<uint8_t> obs_fm((size_t)F * Np, 0);
-    const int scale = ctx->xs8 ? 8 : 1;
-    for (int s = 0; s < N; s++)
-        for (int f = 0; f < F; f++) {
-            const int x = obs[(size_t)s * F + f];
-            if (x >= S) {
-                sbz_close(ctx);
-                return SBZ_EINVAL;
-            }
-            obs_fm[(size_t)f * Np + s] = (uint8_t)((x < 0 ? S : x) * scale);
-        }
-    std::vector<uint8_t> famc(Np, 0);
+    // family class of each site; validate the families
+    std::vector<uint8_t> famc_site(N, 0);
     if (inh && fam_of_site) {
         for (int s = 0; s < N; s++) {
             const int fam = fam_of_site[s];
@@ -135,16 +126,65 @@ int sbz_open(int device, const sbz_dims *dims, const int8_t *obs, const uint8_t 
                 sbz_close(ctx);
                 return SBZ_EINVAL;
             }
-            famc[s] = fam == SBZ_NONE ? 0 : (uint8_t)(fam + 1);
+            famc_site[s] = fam == SBZ_NONE ? 0 : (uint8_t)(fam + 1);
         }
     }
+    // family-sorted site order (stable): position p holds site perm[p]
+    std::vector<int> perm(Np, 0);
+    for (int s = 0; s < N; s++) perm[s] = s;
+    std::stable_sort(perm.begin(), perm.begin() + N,
+                     [&](int x, int y) { return famc_site[x] < famc_site[y]; });
+    std::vector<uint8_t> famc(Np, 0);
+    for (int p = 0; p < N; p++) famc[p] = famc_site[perm[p]];
+    // obs -> feature-major [F][Np] by position, x in 0..S (S = NA) stored as x*8 when it fits a
+    // byte; padded positions hold 0.  Validate the states.
+    std::vector<uint8_t> obs_fm((size_t)F * Np, 0);
+    const int scale = ctx->xs8 ? 8 : 1;
+    for (int p = 0; p < N; p++) {
+        const int s = perm[p];
+        for (int f = 0; f < F; f++) {
+            const int x = obs[(size_t)s * F + f];
+            if (x >= S) {
+                sbz_close(ctx);
+                return SBZ_EINVAL;
+            }
+            obs_fm[(size_t)f * Np + p] = (uint8_t)((x < 0 ? S : x) * scale);
+        }
+    }
+    if (const char *v = getenv("SBZ_LIK_KERNEL")) ctx->lik_kernel = strcmp(v, "zoned") == 0 ? 2 : 1;
+    if (const char *v = getenv("SBZ_LIK_TASKS")) ctx->tasks_per_cu = std::max(1, atoi(v));
+    if (const char *v = getenv("SBZ_LIK_ZSPL")) {
+        const int z = atoi(v);
+        ctx->zspl = (z == 4 || z == 16) ? z : 8;
+    } else {
+        ctx->zspl = N <= 4 * 64 ? 4 : 8;
+    }
+    // site counts by (family class, x) for the zone-sparse kernel: [F][128] int32
+    std::vector<int32_t> cnt;
+    if (lik_counts_apply(*dims)) {
+        const int S1 = S + 1;
+        cnt.assign((size_t)F * 128, 0);
+        for (int s = 0; s < N; s++)
+            for (int f = 0; f < F; f++)
+                cnt[(size_t)f * 128 + famc[s] * S1 + obs_fm[(size_t)f * Np + s] / scale]++;
+    }
+    if (!cnt.empty() &&
+        (hipMalloc(&ctx->d_cnt, cnt.size() * sizeof(int32_t)) != hipSuccess ||
+         hipMemcpy(ctx->d_cnt, cnt.data(), cnt.size() * sizeof(int32_t), hipMemcpyHostToDevice) !=
+             hipSuccess)) {
+        sbz_close(ctx);
+        return SBZ_ENOMEM;
+    }
     if (hipMalloc(&ctx->d_obs_fm, obs_fm.size()) != hipSuccess ||
-        hipMalloc(&ctx->d_famc, famc.size()) != hipSuccess) {
+        hipMalloc(&ctx->d_famc, famc.size()) != hipSuccess ||
+        hipMalloc(&ctx->d_perm, perm.size() * sizeof(int)) != hipSuccess) {
         sbz_close(ctx);
         return SBZ_ENOMEM;
     }
     if (hipMemcpy(ctx->d_obs_fm, obs_fm.data(), obs_fm.size(), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(ctx->d_famc, famc.data(), famc.size(), hipMemcpyHostToDevice) != hipSuccess) {
+        hipMemcpy(ctx->d_famc, famc.data(), famc.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(ctx->d_perm, perm.data(), perm.size() * sizeof(int), hipMemcpyHostToDevice) !=
+            hipSuccess) {
         sbz_close(ctx);
         return SBZ_EHIP;
     }
@@ -164,9 +204,13 @@ void sbz_close(sbz_ctx *ctx) {
     if (ctx->stream != ctx->own_stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->d_obs_fm) (void)hipFree(ctx->d_obs_fm);
     if (ctx->d_famc) hipFree(ctx->d_famc);
+    if (ctx->d_perm) hipFree(ctx->d_perm);
+    if (ctx->d_cnt) hipFree(ctx->d_cnt);
+    free_buf(ctx->zl);
+    free_buf(ctx->nzs);
     free_buf(ctx->partial);
     free_buf(ctx->src_t);
-    free_buf(ctx->cls);
+    free_buf(ctx->ticket);
     free_buf(ctx->stage);
     free_buf(ctx->out);
     if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);

@@ -21,18 +21,24 @@ struct LikArgs {
     int Np;          // sites padded to a multiple of 64 * sites-per-lane
     int W, fpw;      // tasks (single-wave workgroups) per chain, features per task
     int xs8;         // obs bytes hold x*8 (S + 1 <= 32) instead of x
-    uint64_t s_magic;  // ceil(2^32 / S): slot element -> parameter row division
     int B;
-    const uint8_t *obs_fm;  // [F][Np]  x (or x*8), x = S for NA; padded sites hold 0
-    const uint8_t *famc;    // [Np]     0 = no family (or no inheritance), fam + 1 otherwise
+    // Sites are stored in a family-sorted order (position p holds site perm[p]) so that
+    // neighbouring lanes mostly read the same table row (LDS bank-conflict free).
+    const uint8_t *obs_fm;  // [F][Np]  x (or x*8) by position, x = S for NA; padding holds 0
+    const uint8_t *famc;    // [Np]     by position: 0 = no family (or no inheritance), fam + 1
+    const int *perm;        // [Np]     site of each position (padding: 0)
     const uint8_t *zone;    // [B][N]   zone index, 255 = none
     const double *w;        // [B][F][C]
     const double *pg;       // [B][F][S]
     const double *pz;       // [B][Z][F][S]
     const double *pf;       // [B][Fam][F][S] (C == 3 only)
     const uint8_t *src_fm;  // [B][F][Np] component index per cell, or nullptr (mixture)
-    const uint8_t *cls;     // [B][Np]    site class bytes (mixture table kernel)
-    double *partial;        // [B][W]
+    const int *cnt;         // [F][128]   sites per (family class, x): fc * (S+1) + x (zone-sparse)
+    const uint32_t *zl;     // [B][N]     zoned sites: site | class << 24, first nzs[b] valid
+    const int *nzs;         // [B]        zoned sites per chain
+    double *partial;        // [B][W]     task partial sums
+    unsigned *ticket;       // [B]        finished tasks per chain (0 between launches)
+    double *out;            // [B]        log-likelihood per chain
 };
 
 }  // namespace sbz
@@ -46,7 +52,14 @@ struct sbz_ctx {
     hipStream_t stream = nullptr;
     uint8_t *d_obs_fm = nullptr;
     uint8_t *d_famc = nullptr;
-    sbz::DevBuf partial, src_t, cls, stage, out;
+    int *d_perm = nullptr;  // [Np] site index of each position (family-sorted order)
+    int *d_cnt = nullptr;  // [F][128] site counts by (family class, x), or null (dense kernel)
+    int zspl = 8;          // zoned sites per lane and chunk of the zone-sparse kernel
+    int lik_kernel = 1;    // SBZ_LIK_KERNEL: 1 dense (default), 2 zone-sparse ("zoned")
+    int tasks_per_cu = 0;  // SBZ_LIK_TASKS: single-wave tasks per CU per launch (0: occupancy)
+    int mix_occ = 0;       // resident mixture-kernel waves per CU (queried at first launch)
+    int n_cu = 256;        // compute units of the device
+    sbz::DevBuf partial, ticket, src_t, zl, nzs, stage, out;
     std::string err;
 };
 
@@ -60,6 +73,8 @@ int hip_fail(sbz_ctx *ctx, hipError_t e, const char *what);
 size_t lik_lds_bytes(const sbz_dims &d, bool source_mode);
 // Raise the dynamic-LDS limit of the likelihood kernels (gfx950: 160 KiB per workgroup).
 int lik_configure(sbz_ctx *ctx);
+// Whether the zone-sparse (counts) mixture kernel applies to these dims.
+bool lik_counts_apply(const sbz_dims &d);
 // Sites per lane of the likelihood kernels for n_sites (4, 8, 16 or 32).
 int sites_per_lane(int n_sites);
 

@@ -41,7 +41,7 @@ namespace {
 constexpr double LN2 = 0.69314718055994530941723212145818;
 constexpr int WAVE = 64;
 constexpr int ZR = 2;  // zone classes per lane held in registers
-constexpr int NW_BYTES = 16 * 8;  // nw[4][4] doubles ahead of the table
+constexpr int NW_BYTES = 16 * 8;  // nw[4][4] doubles ahead of the source-kernel table
 
 __device__ __forceinline__ bool safe_factor(double v) {
     return v == 0.0 || (v >= 0x1p-120 && v <= 0x1p120);
@@ -59,18 +59,39 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
-__device__ __forceinline__ int wave_or(int v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v |= __shfl_xor(v, off, 64);
-    return v;
-}
-
 // Make this wave's LDS writes visible to its other lanes.  The workgroup is one wave, so no
 // s_barrier is needed, and unlike __syncthreads() this does not drain the vector-memory
 // counter: the next feature's prefetched loads stay in flight.
 __device__ __forceinline__ void wave_lds_sync() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
+}
+
+// Store a task's partial sum; the chain's last task to finish adds the W partials in task order
+// (deterministic, independent of which task finishes last) into out[b] and re-arms the chain's
+// ticket for the next launch.  Hand-off without cache maintenance (MI355X_MICROARCH.md,
+// cross-workgroup hand-offs, first row): the partial is an sc1 store (relaxed agent-scope atomic
+// store), the storing lane waits vmcnt(0), then adds to the chain's ticket (agent atomic); the
+// lane whose add returned W-1 reads every partial with sc1 loads.  An agent-scope acq_rel fence
+// here would write back / invalidate caches once per task and cost ~2x the kernel.
+__device__ __forceinline__ void finish_chain(const LikArgs &a, int b, double tot) {
+    if (threadIdx.x != 0) return;
+    if (a.W == 1) {
+        a.out[b] = tot;
+        return;
+    }
+    double *pb = a.partial + (size_t)b * a.W;
+    __hip_atomic_store(&pb[blockIdx.x], tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev =
+        __hip_atomic_fetch_add(&a.ticket[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev != (unsigned)a.W - 1) return;
+    asm volatile("" ::: "memory");
+    double s = 0.0;
+    for (int t = 0; t < a.W; t++)
+        s += __hip_atomic_load(&pb[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    a.out[b] = s;
+    __hip_atomic_store(&a.ticket[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // normalize_weights (model.py:451-452) for the 4 (has_zone, has_family) classes, lanes 0..3.
@@ -91,29 +112,51 @@ __device__ __forceinline__ void store_nw(double *nw, int lane, double w0r, doubl
 }
 
 // ---------------------------------------------------------------------------------------
-// Mixture kernel (table path).  Requires S + 1 <= 64, Z + 1 <= ZR * (64 / (S + 1)),
-// Fam <= FR, (Z+1)(Fam+1) + 1 <= 256 and a per-feature slot of <= 4*64 doubles (checked on
-// the host; otherwise lik_mixture_generic_kernel runs).
+// Mixture tables (shared by the dense and zone-sparse mixture kernels).  Requires S + 1 <= 64,
+// Z + 1 <= ZR * (64 / (S + 1)), Fam <= FR and (Z+1)(Fam+1) + 1 <= 256 (checked on the host;
+// otherwise lik_mixture_generic_kernel runs).
 //
 // A task is (chain b, features [fa, fb)).  LDS (bytes from the dynamic base):
-//   [0, 128)   nw[4][4]: normalised weights of the 4 (has_zone, has_family) classes
-//   slot       one feature's parameters, `per` doubles: p_global[f][0..S) | p_zones[z][f][0..S)
-//              for z < Z | p_fam[fam][f][0..S) for fam < Fam | w[f][0..C)
-//   table      T[ncls + 1][S1] doubles, class = zc*FamC + fc; the last row is neutral (1.0)
-//   junk       64 doubles (table-build writes of lanes without an entry)
-// Parameter pipeline: the loads of feature f+2 are issued (branch-free, 4 per lane) at the
-// start of feature f into one of two register sets and written into the slot at the end of
-// feature f+1, once its table has been built; HBM latency is covered by two features of work.
+//   table      T[ncls + 1][S1] doubles, class = zc*FamC + fc; the last row is neutral (1.0).
+//              Rows 0..FamC-1 (zc = 0) are the no-zone classes T0[fc][x].
+//   junk       64 doubles (writes of lanes without an entry)
 // Lane (lx = lane % S1, lg = lane / S1) builds the entries of state x = lx for the zone
-// classes zc = lg + i*G, i < ZR (G = 64 / S1), every family class.
+// classes zc = lg + i*G, i < ZR (G = 64 / S1), every family class.  It loads exactly the
+// parameters those entries need (p_global[f][x], p_zones[zc-1][f][x], p_fam[fm][f][x]; uniform
+// row base + 32-bit lane offset) straight into registers, SBZ_PIPE - 1 features ahead; the
+// normalised weights are computed by lanes 0..11 (one division each) and broadcast to SGPRs
+// with v_readlane.  Every global load is unconditional (indices clamped): a load under a
+// branch makes the compiler's vmcnt bookkeeping conservative at the join, and a feature's
+// gathers would then wait for the next feature's loads.
 // ---------------------------------------------------------------------------------------
-constexpr int PL = 4;  // slot doubles per lane (per <= 4 * 64)
 #ifndef SBZ_ABLATE
 #define SBZ_ABLATE 0  // diagnostic builds only: 1 = skip gathers, 2 = skip table build (wrong results)
 #endif
 #ifndef SBZ_MIX_WAVES
-#define SBZ_MIX_WAVES 3  // launch bound: minimum waves per SIMD of the mixture table kernel
+#define SBZ_MIX_WAVES 3  // launch bound: minimum waves per SIMD of the dense mixture kernel
 #endif
+#ifndef SBZ_ZS_WAVES
+#define SBZ_ZS_WAVES 3  // launch bound: minimum waves per SIMD of the zone-sparse kernel
+#endif
+#ifndef SBZ_PIPE
+#define SBZ_PIPE 2  // parameter / observation register sets: loads run SBZ_PIPE - 1 features ahead
+#endif
+#ifndef SBZ_LDS_FENCE
+// 1: s_waitcnt lgkmcnt(0) around the table build.  0: compiler barrier only — a wave's LDS
+// instructions execute in issue order, so within a single-wave workgroup a read issued after a
+// write (by any lane) sees it, and a write issued after a read cannot overtake it.
+#define SBZ_LDS_FENCE 1
+#endif
+constexpr int NS = SBZ_PIPE;
+
+__device__ __forceinline__ void lds_phase() {
+#if SBZ_LDS_FENCE
+    wave_lds_sync();
+#else
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+#endif
+}
 
 // A parameter or normalised weight is "tame" if it is 0 or in [2^-60, 2^60]: every table entry
 // is then a sum of <= 3 products of tame values, i.e. 0 or in [2^-120, 3*2^120], and 8 such
@@ -121,121 +164,125 @@ constexpr int PL = 4;  // slot doubles per lane (per <= 4 * 64)
 // negative / NaN inputs) the wave renormalises after every factor for that feature.
 __device__ __forceinline__ bool tame(double v) { return v == 0.0 || (v >= 0x1p-60 && v <= 0x1p60); }
 
-template <int C, int SPL, int FR, bool XS8>
-__global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    constexpr int NO = SPL / 4;  // observation words (4 sites each) per lane per feature
-    double *nw = reinterpret_cast<double *>(lds);
-    const int lane = threadIdx.x;
-    const int b = blockIdx.y;
-    const int fa = blockIdx.x * a.fpw;
-    const int fb = min(a.F, fa + a.fpw);
-    const int S = a.S, S1 = a.S + 1, FamC = a.FamC, Z = a.Z;
-    const int Fam = (C == 3) ? a.Fam : 0;
-    const int ncls = (Z + 1) * FamC;
-    const int G = WAVE / S1;
-    const int lx = lane % S1, lg = lane / S1;
-    const bool na = lx == S;
-    const int lxc = min(lx, S - 1);  // the NA column and idle lanes read state 0
-    const int nps = (1 + Z + Fam) * S;  // parameter doubles of a slot (then C weights)
-    const int per = nps + C;
-    const uint32_t zfs = (uint32_t)(a.F * S);
-    const double *pgb = a.pg + (size_t)b * zfs;
-    const double *zbase = Z > 0 ? a.pz + (size_t)b * Z * zfs : pgb;
-    const double *fbase = Fam > 0 ? a.pf + (size_t)b * Fam * zfs : pgb;
-    const double *wb = a.w + (size_t)b * a.F * C;
-    double *slot = nw + 16;
-    double *tab = slot + ((per + 1) & ~1);
-    double *junk = tab + (ncls + 1) * S1 + lane;
-    const int row_bytes = S1 * 8;
-    const int tab_off = (int)((tab - nw) * 8);
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)u, l);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(u >> 32), l);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
 
-    // Per-lane source rows of the slot elements i = lane + 64k: element i of feature f is
-    // sbase[k][f * sstride[k]] (p_global / p_zones / p_fam rows: stride S; weights: stride C).
-    const double *sbase[PL];
-    uint32_t sstride[PL];
+// One feature's parameters as one lane needs them.
+template <int C, int FR>
+struct MixParams {
+    double g;       // p_global[f][lxc]
+    double z[ZR];   // p_zones[zc_i - 1][f][lxc]
+    double fm[FR];  // p_fam[fm][f][lxc]
+    double w[C];    // w[f][0..C) (wave-uniform)
+};
+
+template <int C, int FR>
+struct MixTable {
+    int lane, S, S1, FamC, Z, Fam, ncls, G, lx, lg, row_bytes;
+    uint32_t lxc;
+    int bp0;  // ds_bpermute byte address of the lane's slot-0 weights: lane 3*hz of lanes 0..11
+    bool na;
+    uint32_t zfs;
+    unsigned char *lds;
+    double *tab, *junk;
+    const double *pgb, *zbase, *fbase, *wb;
+    uint32_t pzo[ZR];  // lane offset of its p_zones rows (elements)
+
+    __device__ __forceinline__ MixTable(const LikArgs &a, unsigned char *lds_, int b) : lds(lds_) {
+        lane = threadIdx.x;
+        S = a.S;
+        S1 = a.S + 1;
+        FamC = a.FamC;
+        Z = a.Z;
+        Fam = (C == 3) ? a.Fam : 0;
+        ncls = (Z + 1) * FamC;
+        G = WAVE / S1;
+        lx = lane % S1;
+        lg = lane / S1;
+        na = lx == S;
+        lxc = (uint32_t)min(lx, S - 1);  // the NA column and idle lanes read state 0
+        bp0 = lg > 0 ? 12 : 0;
+        tab = reinterpret_cast<double *>(lds);
+        junk = tab + (ncls + 1) * S1 + lane;
+        row_bytes = S1 * 8;
+        zfs = (uint32_t)(a.F * S);
+        pgb = a.pg + (size_t)b * zfs;
+        zbase = Z > 0 ? a.pz + (size_t)b * Z * zfs : pgb;
+        fbase = Fam > 0 ? a.pf + (size_t)b * Fam * zfs : pgb;
+        wb = a.w + (size_t)b * a.F * C;
 #pragma unroll
-    for (int k = 0; k < PL; k++) {
-        const uint32_t ic = (uint32_t)min(lane + WAVE * k, per - 1);
-        const uint32_t seg = (uint32_t)(((uint64_t)ic * a.s_magic) >> 32);  // ic / S
-        const uint32_t r = ic - seg * (uint32_t)S;
-        if (seg == 0) {
-            sbase[k] = pgb + r;
-            sstride[k] = (uint32_t)S;
-        } else if (seg <= (uint32_t)Z) {
-            sbase[k] = zbase + (size_t)(seg - 1) * zfs + r;
-            sstride[k] = (uint32_t)S;
-        } else if (seg < (uint32_t)(1 + Z + Fam)) {
-            sbase[k] = fbase + (size_t)(seg - 1 - Z) * zfs + r;
-            sstride[k] = (uint32_t)S;
-        } else {
-            sbase[k] = wb + (ic - (uint32_t)nps);
-            sstride[k] = (uint32_t)C;
-        }
+        for (int i = 0; i < ZR; i++)
+            pzo[i] = (uint32_t)(max(min(lg + i * G, Z), 1) - 1) * zfs + lxc;
+        for (int x = lane; x < S1; x += WAVE) tab[ncls * S1 + x] = 1.0;  // neutral row
     }
-    auto load_slot = [&](int f, double (&r)[PL]) {
+
+    __device__ __forceinline__ void load(int f, MixParams<C, FR> &r) const {
+        const uint32_t fo = (uint32_t)f * (uint32_t)S;
+        r.g = pgb[fo + lxc];
 #pragma unroll
-        for (int k = 0; k < PL; k++) r[k] = sbase[k][(uint32_t)f * sstride[k]];
-    };
-    // store the slot (branch-free: out-of-range elements go to the lane's junk word); returns
-    // whether every stored value is tame
-    auto store_slot = [&](const double (&r)[PL]) -> int {
-        int ok = 1;
+        for (int i = 0; i < ZR; i++) r.z[i] = zbase[fo + pzo[i]];
 #pragma unroll
-        for (int k = 0; k < PL; k++) {
-            const bool in = lane + WAVE * k < per;
-            *(in ? slot + lane + WAVE * k : junk) = r[k];
-            ok &= (!in) | tame(r[k]);
+        for (int fm = 0; fm < FR; fm++)
+            r.fm[fm] = fbase[(uint32_t)min(fm, max(Fam - 1, 0)) * zfs + fo + lxc];
+#pragma unroll
+        for (int c = 0; c < C; c++) r.w[c] = wb[(uint32_t)f * C + c];
+    }
+
+    // Normalised weights and the table of one feature.  Returns `wide`: some input is not
+    // tame, so products over this feature must renormalise after every factor.
+    __device__ __forceinline__ bool build(const MixParams<C, FR> &r) const {
+        // 1. normalised weights (normalize_weights model.py:451-452:
+        //    w*has / ((w0*h0 + w1*h1) + w2*h2)), lane 3h + c, h = hz | hf << 1
+        const int l12 = min(lane, 11), h = l12 / 3, c = l12 - 3 * h;
+        const double hzf = (h & 1) ? 1.0 : 0.0, hff = (h & 2) ? 1.0 : 0.0;
+        const double w0 = r.w[0] * 1.0, w1 = r.w[1] * hzf;
+        double sum = w0 + w1, w2 = 0.0;
+        if (C == 3) {
+            w2 = r.w[2] * hff;
+            sum = sum + w2;
         }
-        return ok;
-    };
-    auto load_obs = [&](int f, int c0, uint32_t (&o)[NO]) {
-        const uint32_t *op = reinterpret_cast<const uint32_t *>(a.obs_fm + (size_t)f * a.Np + c0);
+        const double wc = c == 0 ? w0 : (c == 1 ? w1 : w2);
+        const double n = (C == 2 && c == 2) ? 0.0 : wc / sum;
+        int ok = (int)tame(n) & (int)tame(r.g);
 #pragma unroll
-        for (int k = 0; k < NO; k++) o[k] = op[lane + 64 * k];
-    };
-
-    for (int x = lane; x < S1; x += WAVE) tab[ncls * S1 + x] = 1.0;
-
-    double m[4] = {1.0, 1.0, 1.0, 1.0};  // four independent product chains
-    int e = 0;
-    uint32_t base2[SPL / 2];  // per-site class row offsets (bytes, < 64 KiB), two per register
-    uint32_t oa[NO], ob[NO];
-    double ra[PL], rb[PL];
-    int slot_ok = 1;  // the slot's values are tame
-
-    // One feature.  `cur`: f's observations; `nxt` <- f+1's.  `fill` <- f+2's parameters;
-    // `wr` holds f+1's parameters (issued during f-1), written to the slot at the end.
-    // Every global load is unconditional (feature index clamped to fb-1): a load under a branch
-    // makes the compiler's vmcnt bookkeeping conservative at the join, and the gathers of f would
-    // then wait for f+1's observations.  `live` = false only for the padding feature of an odd
-    // range, whose gathers are skipped (the skipped block issues no global loads).
-    auto feature = [&](int f, int c0, bool live, uint32_t (&cur)[NO], uint32_t (&nxt)[NO],
-                       double (&fill)[PL], double (&wr)[PL]) {
-        wave_lds_sync();  // the slot holds feature f
-        // 1. normalised weights, one division per lane: lane = h*3 + c (h = hz | hf<<1)
-        //    normalize_weights model.py:451-452: w*has / ((w0*h0 + w1*h1) + w2*h2)
-        int nok = 1;
-        if (lane < 12) {
-            const int h = lane / 3, c = lane - 3 * (lane / 3);
-            const double hz = (h & 1) ? 1.0 : 0.0, hf = (h & 2) ? 1.0 : 0.0;
-            const double w0 = slot[nps] * 1.0, w1 = slot[nps + 1] * hz;
-            double sum = w0 + w1, w2 = 0.0;
-            if (C == 3) {
-                w2 = slot[nps + 2] * hf;
-                sum = sum + w2;
+        for (int i = 0; i < ZR; i++) ok &= (int)tame(r.z[i]);
+#pragma unroll
+        for (int fm = 0; fm < FR; fm++) ok &= (int)tame(r.fm[fm]);
+        const bool wide = __ballot(!ok) != 0;
+        // Slot i >= 1 holds zone classes only (zc >= G >= 1): wave-uniform weights of h = 1 (no
+        // family) and h = 3 (family), read into SGPRs.  Slot 0 mixes zc = 0 (lanes lg == 0) and
+        // zone classes: each lane fetches its h = hz and h = hz | 2 weights with ds_bpermute.
+        double u[2][3];
+#pragma unroll
+        for (int cc = 0; cc < 3; cc++) {
+            u[0][cc] = (C == 2 && cc == 2) ? 0.0 : readlane_f64(n, 3 + cc);
+            u[1][cc] = (C == 2 && cc == 2) ? 0.0 : readlane_f64(n, 9 + cc);
+        }
+        double p[2][3];
+#pragma unroll
+        for (int hf = 0; hf < 2; hf++)
+#pragma unroll
+            for (int cc = 0; cc < 3; cc++) {
+                if (C == 2 && (hf == 1 || cc == 2)) {
+                    p[hf][cc] = 0.0;
+                    continue;
+                }
+                const uint64_t bits = (uint64_t)__double_as_longlong(n);
+                const int a = bp0 + 4 * (6 * hf + cc);
+                const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)(uint32_t)bits);
+                const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)(uint32_t)(bits >> 32));
+                p[hf][cc] = __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
             }
-            const double wc = c == 0 ? w0 : (c == 1 ? w1 : w2);
-            const double n = (C == 2 && c == 2) ? 0.0 : wc / sum;
-            nw[h * 4 + c] = n;
-            nok = tame(n);
-        }
-        const bool wide = __ballot(!(nok & slot_ok)) != 0;  // one v_cmp into an SGPR pair
-        wave_lds_sync();
         // 2. table: the reference cell (n0*l0 + n1*l1) + n2*l2 for every class.  Branch-free:
-        //    lanes without an entry write to their junk slot.
-        const double l0 = na ? 1.0 : slot[lxc];
-        const double lna = na ? 1.0 : 0.0;  // lh of a component the site lacks
+        //    lanes without an entry write to their junk slot.  The family term of a class
+        //    without family is n2 * l2 = (w2 * 0 / sum) * (0 or 1): +0 for tame inputs, left
+        //    out then (x + 0 == x); kept for untamed ones, where it may be NaN.
+        lds_phase();
+        const double l0 = na ? 1.0 : r.g;
 #pragma unroll
         for (int i = 0; i < ZR; i++) {
 #if SBZ_ABLATE & 2
@@ -243,32 +290,66 @@ __global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArg
 #endif
             const int zc = lg + i * G;
             const bool valid = (lane < G * S1) && (zc <= Z);
-            const int hz = zc > 0 ? 1 : 0;
-            const double lzv = slot[min(zc, Z) * S + lxc];
-            const double l1 = na ? 1.0 : (zc > 0 ? lzv : 0.0);
-            const double *n0 = nw + hz * 4, *n1 = nw + (hz | 2) * 4;  // no family / family
+            const double n00 = i == 0 ? p[0][0] : u[0][0], n01 = i == 0 ? p[0][1] : u[0][1];
+            // zone lh: 0 for a site outside every zone (model.py:241-247), 1 for NA
+            const double l1 = na ? 1.0 : ((i > 0 || zc > 0) ? r.z[i] : 0.0);
             double *row = valid ? tab + (zc * FamC) * S1 + lx : junk;
             const int rs = valid ? S1 : 0;
-            double v = n0[0] * l0 + n0[1] * l1;
-            if (C == 3) v = v + n0[2] * lna;
+            double v = n00 * l0 + n01 * l1;
+            if (C == 3 && wide) v = v + (i == 0 ? p[0][2] : u[0][2]) * (na ? 1.0 : 0.0);
             row[0] = v;
             if (C == 3) {
-                const double a1 = n1[0] * l0 + n1[1] * l1;
+                const double n10 = i == 0 ? p[1][0] : u[1][0], n11 = i == 0 ? p[1][1] : u[1][1];
+                const double n12 = i == 0 ? p[1][2] : u[1][2];
+                const double a1 = n10 * l0 + n11 * l1;
 #pragma unroll
-                for (int fm = 0; fm < FR; fm++) {
-                    if (fm < Fam) {
-                        const double lf = slot[(1 + Z + fm) * S + lxc];
-                        row[(fm + 1) * rs] = a1 + n1[2] * (na ? 1.0 : lf);
-                    }
-                }
+                for (int fm = 0; fm < FR; fm++)
+                    if (fm < Fam) row[(fm + 1) * rs] = a1 + n12 * (na ? 1.0 : r.fm[fm]);
             }
         }
-        wave_lds_sync();
+        lds_phase();
+        return wide;
+    }
+
+    __device__ __forceinline__ double at(uint32_t byte_addr) const {
+        return *reinterpret_cast<const double *>(lds + byte_addr);
+    }
+};
+
+// ---------------------------------------------------------------------------------------
+// Dense mixture kernel: every site of the task is gathered from the table.
+// The lane owns SPL sites (4*lane + 256*k + j); their class row offsets live in registers.
+// ---------------------------------------------------------------------------------------
+template <int C, int SPL, int FR, bool XS8>
+__global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    constexpr int NO = SPL / 4;  // observation words (4 sites each) per lane per feature
+    const int lane = threadIdx.x;
+    const int b = blockIdx.y;
+    const int fa = blockIdx.x * a.fpw;
+    const int fb = min(a.F, fa + a.fpw);
+    const MixTable<C, FR> t(a, lds, b);
+
+    auto load_obs = [&](int f, int c0, uint32_t (&o)[NO]) {
+        const uint32_t *op = reinterpret_cast<const uint32_t *>(a.obs_fm + (size_t)f * a.Np + c0);
+#pragma unroll
+        for (int k = 0; k < NO; k++) o[k] = op[(uint32_t)(lane + 64 * k)];
+    };
+
+    double m[4] = {1.0, 1.0, 1.0, 1.0};  // four independent product chains
+    int e = 0;
+    uint32_t base2[SPL / 2];  // per-site class row offsets (bytes, < 64 KiB), two per register
+    MixParams<C, FR> P[NS];   // parameter sets: feature f uses P[(f - fa) % NS]
+    uint32_t O[NS][NO];       // observation sets, same rotation
+
+    // One feature: build its table from `cur`, issue the loads of feature f + NS - 1 into
+    // `fill` (the sets feature f - 1 used), gather.  `live` = false for padding features.
+    auto feature = [&](int f, int c0, bool live, const MixParams<C, FR> &cur, const uint32_t (&ob)[NO],
+                       MixParams<C, FR> &fill, uint32_t (&ofill)[NO]) {
+        const bool wide = t.build(cur);
         __builtin_amdgcn_sched_barrier(0);
-        // 3. issue the loads of f+2's parameters and f+1's observations
-        load_slot(min(f + 2, fb - 1), fill);
-        load_obs(min(f + 1, fb - 1), c0, nxt);
-        // 4. gathers of feature f: cell (k, j) -> chain (k & 3)
+        t.load(min(f + NS - 1, fb - 1), fill);
+        load_obs(min(f + NS - 1, fb - 1), c0, ofill);
         if (SBZ_ABLATE & 1 || !live) {
             // padding feature (or diagnostic build): no gathers
         } else if (!wide) {
@@ -278,9 +359,8 @@ __global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArg
                 for (int j = 0; j < 4; j++) {
                     const uint32_t bw = base2[2 * k + (j >> 1)];
                     const uint32_t bs = (j & 1) ? (bw >> 16) : (bw & 0xffffu);
-                    const uint32_t xb = (cur[k] >> (8 * j)) & 0xffu;
-                    const uint32_t addr = bs + (XS8 ? xb : (xb << 3));
-                    m[k & 3] *= *reinterpret_cast<const double *>(lds + addr);
+                    const uint32_t xb = (ob[k] >> (8 * j)) & 0xffu;
+                    m[k & 3] *= t.at(bs + (XS8 ? xb : (xb << 3)));
                     if (j == 3 && (k & 1)) __builtin_amdgcn_sched_barrier(0);  // <= 8 reads in flight
                 }
 #pragma unroll
@@ -294,45 +374,240 @@ __global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArg
                 for (int j = 0; j < 4; j++) {
                     const uint32_t bw = base2[2 * k + (j >> 1)];
                     const uint32_t bs = (j & 1) ? (bw >> 16) : (bw & 0xffffu);
-                    const uint32_t xb = (cur[k] >> (8 * j)) & 0xffu;
-                    const uint32_t addr = bs + (XS8 ? xb : (xb << 3));
-                    m[0] *= *reinterpret_cast<const double *>(lds + addr);
+                    const uint32_t xb = (ob[k] >> (8 * j)) & 0xffu;
+                    m[0] *= t.at(bs + (XS8 ? xb : (xb << 3)));
                     renorm(m[0], e);
                 }
         }
-        // 5. the table of f is built, so the slot can take f+1's parameters
-        slot_ok = store_slot(wr);
     };
 
     for (int c0 = 0; c0 < a.Np; c0 += SPL * WAVE) {
-        // classes of this chunk's sites, the first two features' parameters, f0's observations
+        // classes of this chunk's sites (cls = zc*FamC + fc, padding -> the neutral row); the
+        // first NS - 1 features' parameters and observations
         {
-            const uint32_t *clw = reinterpret_cast<const uint32_t *>(a.cls + (size_t)b * a.Np + c0);
-            uint32_t cw[NO];
+            const uint8_t *zb = a.zone + (size_t)b * a.N;
+            uint32_t zs[SPL];
+            int4 pv[NO];
+            uint32_t fw[NO];
 #pragma unroll
-            for (int k = 0; k < NO; k++) cw[k] = clw[lane + 64 * k];
-            load_slot(fa, ra);
-            load_slot(min(fa + 1, fb - 1), rb);
-            load_obs(fa, c0, oa);
+            for (int k = 0; k < NO; k++) {
+                const uint32_t p0 = (uint32_t)(c0 + 4 * lane + 256 * k);  // < Np (arrays padded)
+                pv[k] = *reinterpret_cast<const int4 *>(a.perm + p0);
+                fw[k] = *reinterpret_cast<const uint32_t *>(a.famc + p0);
+            }
+#pragma unroll
+            for (int k = 0; k < NO; k++) {
+                zs[4 * k + 0] = zb[(uint32_t)pv[k].x];
+                zs[4 * k + 1] = zb[(uint32_t)pv[k].y];
+                zs[4 * k + 2] = zb[(uint32_t)pv[k].z];
+                zs[4 * k + 3] = zb[(uint32_t)pv[k].w];
+            }
+#pragma unroll
+            for (int j = 0; j < NS - 1; j++) {
+                t.load(min(fa + j, fb - 1), P[j]);
+                load_obs(min(fa + j, fb - 1), c0, O[j]);
+            }
 #pragma unroll
             for (int i = 0; i < SPL; i++) {
-                const int cls = (cw[i / 4] >> (8 * (i % 4))) & 0xff;  // padded sites: neutral row
-                const uint32_t off = (uint32_t)(tab_off + cls * row_bytes);
+                const int pos = c0 + 4 * lane + 256 * (i / 4) + (i % 4);
+                const int z = (int)zs[i];
+                const int fc = (int)((fw[i / 4] >> (8 * (i % 4))) & 0xffu);
+                const int cls = pos < a.N ? ((z < t.Z ? z + 1 : 0) * t.FamC + fc) : t.ncls;
+                const uint32_t off = (uint32_t)(cls * t.row_bytes);
                 if (i & 1) base2[i >> 1] |= off << 16;
                 else base2[i >> 1] = off;
             }
-            wave_lds_sync();  // previous chunk's gathers are done with the slot
-            slot_ok = store_slot(ra);
         }
-        for (int f = fa; f < fb; f += 2) {
-            feature(f, c0, true, oa, ob, ra, rb);
-            feature(f + 1, c0, f + 1 < fb, ob, oa, rb, ra);
+        for (int f = fa; f < fb; f += NS) {
+#pragma unroll
+            for (int j = 0; j < NS; j++)
+                feature(f + j, c0, f + j < fb, P[j], O[j], P[(j + NS - 1) % NS], O[(j + NS - 1) % NS]);
         }
     }
     double v = (log(m[0]) + log(m[1])) + (log(m[2]) + log(m[3]));
     v = v + (double)e * LN2;
     const double tot = wave_sum(v);
-    if (lane == 0) a.partial[(size_t)b * a.W + blockIdx.x] = tot;
+    finish_chain(a, b, tot);
+}
+
+// ---------------------------------------------------------------------------------------
+// Zone-sparse mixture kernel.  A site outside every zone has class (0, fc), so over those
+// sites   sum log T0[fc][x] = sum_{fc,x} n_out[fc][x] * log T0[fc][x].
+// With n_all[f][fc][x] (all sites, counted once when the context opens) and the chain's list
+// of zoned sites (zone_list_kernel):
+//   sum_sites log T = sum_{fc,x} n_all * log T0  +  log prod_zoned T[cls][x]
+//                                                 -  log prod_zoned T0[fc][x]
+// One log per (fc, x) entry instead of one gather per site: the gathers shrink to the zoned
+// sites (two each).  Identical to the per-cell sum up to rounding (~1e-15 relative).
+// When a T0 entry with a non-zero count is 0 (the subtraction would be inf - inf) or an input
+// is untamed, the feature takes the exact slow path: zoned sites by a per-factor renormalised
+// product, the other sites by one log per cell.
+// The lane owns ZSPL zoned sites per chunk (lane + 64k); more zoned sites -> more chunks
+// (the tables are rebuilt per chunk).
+// ---------------------------------------------------------------------------------------
+constexpr int CP = 128;  // count entries per feature (FamC * S1 <= CP)
+
+template <int C, int ZSPL, int FR, bool XS8>
+__global__ __launch_bounds__(WAVE, SBZ_ZS_WAVES) void lik_zoned_kernel(LikArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int lane = threadIdx.x;
+    const int b = blockIdx.y;
+    const int fa = blockIdx.x * a.fpw;
+    const int fb = min(a.F, fa + a.fpw);
+    const MixTable<C, FR> t(a, lds, b);
+    const int NC = t.FamC * t.S1;
+    const int nz = a.nzs[b];
+    const uint32_t *zlb = a.zl + (size_t)b * a.N;
+    const uint32_t neutral = (uint32_t)(t.ncls * t.row_bytes);
+
+    double m1[2] = {1.0, 1.0}, m0[2] = {1.0, 1.0};  // products over zoned sites of T and T0
+    int e = 0;                                      // exponent of m1 / m0
+    double acc = 0.0;                               // sum n_all * log T0 (and slow-path logs)
+    uint32_t site[ZSPL], desc[ZSPL];                // zoned site; row offsets T | T0 << 16
+    MixParams<C, FR> P[NS];
+    uint32_t O[NS][ZSPL];                           // zoned sites' observation bytes (x or x*8)
+    int CN[NS][2];                                  // n_all of entries lane, lane + 64
+
+    auto load_zobs = [&](int f, uint32_t (&o)[ZSPL]) {
+        const uint8_t *op = a.obs_fm + (size_t)f * a.Np;
+#pragma unroll
+        for (int k = 0; k < ZSPL; k++) o[k] = op[site[k]];
+    };
+    auto load_cnt = [&](int f, int (&c)[2]) {
+        const int *cp = a.cnt + (size_t)f * CP;
+        c[0] = cp[lane];
+        c[1] = cp[lane + WAVE];
+    };
+    // slow path: sum over the chain's non-zoned sites of log T0[fc][x] (one log per cell)
+    auto outside_logs = [&](int f) {
+        const uint8_t *zb = a.zone + (size_t)b * a.N;
+        const uint8_t *op = a.obs_fm + (size_t)f * a.Np;
+        double sacc = 0.0;
+        for (int s = lane; s < a.N; s += WAVE) {
+            const uint32_t xb = op[s];
+            const uint32_t row = (uint32_t)(a.famc[s] * t.row_bytes);
+            const double v = t.at(row + (XS8 ? xb : (xb << 3)));
+            sacc += zb[a.perm[s]] < (uint32_t)t.Z ? 0.0 : log(v);
+        }
+        return sacc;
+    };
+
+    auto feature = [&](int f, bool live, bool first, int zb0, const MixParams<C, FR> &cur,
+                       const uint32_t (&ob)[ZSPL], const int (&cc)[2], MixParams<C, FR> &fill,
+                       uint32_t (&ofill)[ZSPL], int (&cfill)[2]) {
+        const bool wide = t.build(cur);
+        __builtin_amdgcn_sched_barrier(0);
+        t.load(min(f + NS - 1, fb - 1), fill);
+        load_zobs(min(f + NS - 1, fb - 1), ofill);
+        load_cnt(min(f + NS - 1, fb - 1), cfill);
+        if (live) {
+            // counts term against the no-zone rows T0 = tab[0 .. NC)
+            double cl = 0.0;
+            int zero_hit = 0;
+#pragma unroll
+            for (int q = 0; q < 2; q++) {
+                if (q == 1 && NC <= WAVE) break;
+                const int l = lane + WAVE * q;
+                const double v = t.tab[min(l, NC - 1)];
+                const bool use = l < NC && cc[q] > 0;
+                zero_hit |= use && v == 0.0;  // checked in every chunk: T0 is gathered per chunk
+                if (first) cl += use ? (double)cc[q] * log(v) : 0.0;
+            }
+            const bool slow = wide || __ballot(zero_hit) != 0;
+            if (SBZ_ABLATE & 1) {
+                acc += cl;
+            } else if (!slow) {
+                acc += cl;
+#pragma unroll
+                for (int k = 0; k < ZSPL; k++) {
+                    if (zb0 + WAVE * k < nz) {  // uniform: slot k holds a zoned site in some lane
+                        const uint32_t d = desc[k];
+                        m1[k & 1] *= t.at((d & 0xffffu) + (XS8 ? ob[k] : (ob[k] << 3)));
+                        m0[k & 1] *= t.at((d >> 16) + (XS8 ? ob[k] : (ob[k] << 3)));
+                    }
+                }
+                int e1a, e1b, e0a, e0b;
+                e1a = __builtin_amdgcn_frexp_exp(m1[0]);
+                m1[0] = __builtin_amdgcn_frexp_mant(m1[0]);
+                e1b = __builtin_amdgcn_frexp_exp(m1[1]);
+                m1[1] = __builtin_amdgcn_frexp_mant(m1[1]);
+                e0a = __builtin_amdgcn_frexp_exp(m0[0]);
+                m0[0] = __builtin_amdgcn_frexp_mant(m0[0]);
+                e0b = __builtin_amdgcn_frexp_exp(m0[1]);
+                m0[1] = __builtin_amdgcn_frexp_mant(m0[1]);
+                e += (e1a + e1b) - (e0a + e0b);
+            } else {
+                // exact slow path (rare: zero / untamed table entries)
+#pragma unroll
+                for (int k = 0; k < ZSPL; k++) {
+                    const uint32_t d = desc[k];
+                    m1[0] *= t.at((d & 0xffffu) + (XS8 ? ob[k] : (ob[k] << 3)));
+                    renorm(m1[0], e);
+                }
+                if (first) acc += outside_logs(f);
+            }
+        }
+    };
+
+    const int nchunk = max(1, (nz + WAVE * ZSPL - 1) / (WAVE * ZSPL));
+    for (int ch = 0; ch < nchunk; ch++) {
+        const int zb0 = ch * WAVE * ZSPL;
+#pragma unroll
+        for (int k = 0; k < ZSPL; k++) {
+            const int j = zb0 + lane + WAVE * k;
+            const uint32_t ent = zlb[min(j, a.N - 1)];
+            const uint32_t cls = ent >> 24;
+            const uint32_t fc = cls - (cls / (uint32_t)t.FamC) * (uint32_t)t.FamC;
+            const bool in = j < nz;
+            site[k] = in ? (ent & 0xffffffu) : 0u;
+            desc[k] = in ? ((uint32_t)(cls * t.row_bytes) | ((uint32_t)(fc * t.row_bytes) << 16))
+                         : (neutral | (neutral << 16));
+        }
+#pragma unroll
+        for (int j = 0; j < NS - 1; j++) {
+            t.load(min(fa + j, fb - 1), P[j]);
+            load_zobs(min(fa + j, fb - 1), O[j]);
+            load_cnt(min(fa + j, fb - 1), CN[j]);
+        }
+        for (int f = fa; f < fb; f += NS) {
+#pragma unroll
+            for (int j = 0; j < NS; j++) {
+                const int jf = (j + NS - 1) % NS;
+                feature(f + j, f + j < fb, ch == 0, zb0, P[j], O[j], CN[j], P[jf], O[jf], CN[jf]);
+            }
+        }
+    }
+    double v = (log(m1[0]) + log(m1[1])) - (log(m0[0]) + log(m0[1]));
+    v = v + (double)e * LN2;
+    v = v + acc;
+    const double tot = wave_sum(v);
+    finish_chain(a, b, tot);
+}
+
+// Per-chain ordered list of zoned sites for lik_zoned_kernel: zl[b][j] = position | cls << 24
+// (position in the family-sorted site order, cls = (z+1)*FamC + fc), j < nzs[b].  One wave per
+// chain.
+__global__ void zone_list_kernel(int N, int Z, int FamC, const uint8_t *zone, const uint8_t *famc,
+                                 const int *perm, uint32_t *zl, int *nzs) {
+    const int b = blockIdx.x;
+    const int lane = threadIdx.x;
+    const uint8_t *zb = zone + (size_t)b * N;
+    uint32_t *out = zl + (size_t)b * N;
+    int count = 0;
+    for (int s0 = 0; s0 < N; s0 += WAVE) {
+        const int s = s0 + lane;
+        const int z = s < N ? zb[perm[s]] : SBZ_NONE;
+        const bool in = z < Z;
+        const uint64_t mask = __ballot(in);
+        if (in) {
+            const int pos = count + (int)__builtin_amdgcn_mbcnt_hi(
+                                        (uint32_t)(mask >> 32),
+                                        __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+            out[pos] = (uint32_t)s | ((uint32_t)((z + 1) * FamC + famc[s]) << 24);
+        }
+        count += __popcll(mask);
+    }
+    if (lane == 0) nzs[b] = count;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -356,8 +631,8 @@ __global__ __launch_bounds__(WAVE) void lik_mixture_generic_kernel(LikArgs a) {
     const uint8_t *zb = a.zone + (size_t)b * a.N;
     const int div = a.xs8 ? 8 : 1;
     double lsum = 0.0;
-    for (int s = lane; s < a.N; s += WAVE) {
-        const int z = zb[s];
+    for (int s = lane; s < a.N; s += WAVE) {  // s: position in the family-sorted site order
+        const int z = zb[a.perm[s]];
         const bool hz = z < Z;
         const int fc = (C == 3) ? a.famc[s] : 0;
         const bool hf = fc > 0;
@@ -382,7 +657,7 @@ __global__ __launch_bounds__(WAVE) void lik_mixture_generic_kernel(LikArgs a) {
         }
     }
     const double tot = wave_sum(lsum);
-    if (lane == 0) a.partial[(size_t)b * a.W + blockIdx.x] = tot;
+    finish_chain(a, b, tot);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -406,7 +681,7 @@ __global__ __launch_bounds__(WAVE) void lik_source_kernel(LikArgs a) {
     const int fa = blockIdx.x * a.fpw;
     const int fb = min(a.F, fa + a.fpw);
     if (fa >= fb) {
-        if (lane == 0) a.partial[(size_t)b * a.W + blockIdx.x] = 0.0;
+        finish_chain(a, b, 0.0);
         return;
     }
     const int S = a.S, S1 = a.S + 1, Z = a.Z;
@@ -434,10 +709,10 @@ __global__ __launch_bounds__(WAVE) void lik_source_kernel(LikArgs a) {
         for (int k = 0; k < SPL / 4; k++)
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                const int s = c0 + 4 * lane + 256 * k + j;
+                const int s = c0 + 4 * lane + 256 * k + j;  // position (family-sorted order)
                 uint32_t r = (uint32_t)rn | ((uint32_t)rn << 8) | ((uint32_t)rn << 16);
                 if (s < a.N) {
-                    const int z = zb[s];
+                    const int z = zb[a.perm[s]];
                     const bool hz = z < Z;
                     const int fc = (C == 3) ? a.famc[s] : 0;
                     const bool hf = fc > 0;
@@ -468,14 +743,14 @@ __global__ __launch_bounds__(WAVE) void lik_source_kernel(LikArgs a) {
                 for (int z = 0; z < Z; z++) {
                     const double l1 = na ? 1.0 : pzb[z * zfs + off];
                     const double v0 = nw[1 * 4 + 1] * l1, v1 = nw[3 * 4 + 1] * l1;
-                    bad |= !safe_factor(v0) | !safe_factor(v1);
+                    bad |= (int)!safe_factor(v0) | (int)!safe_factor(v1);
                     tab[(off1 + 2 * z) * S1 + x] = v0;
                     tab[(off1 + 2 * z + 1) * S1 + x] = v1;
                 }
                 for (int i = 0; i < Fam; i++) {
                     const double l2 = na ? 1.0 : pfb[i * zfs + off];
                     const double v0 = nw[2 * 4 + 2] * l2, v1 = nw[3 * 4 + 2] * l2;
-                    bad |= !safe_factor(v0) | !safe_factor(v1);
+                    bad |= (int)!safe_factor(v0) | (int)!safe_factor(v1);
                     tab[(off2 + 2 * i) * S1 + x] = v0;
                     tab[(off2 + 2 * i + 1) * S1 + x] = v1;
                 }
@@ -512,39 +787,13 @@ __global__ __launch_bounds__(WAVE) void lik_source_kernel(LikArgs a) {
     }
     const double v = log(m) + (double)e * LN2;
     const double tot = wave_sum(v);
-    if (lane == 0) a.partial[(size_t)b * a.W + blockIdx.x] = tot;
+    finish_chain(a, b, tot);
 }
 
-// Per-chain site class bytes for the mixture table kernel: cls = zc*FamC + fc
-// (zc = 0 no zone | z+1, fc = 0 no family | fam+1), padded sites -> ncls (the neutral row).
-__global__ void site_class_kernel(int B, int N, int Np, int Z, int FamC, const uint8_t *zone,
-                                  const uint8_t *famc, uint8_t *cls) {
-    const int ncls = (Z + 1) * FamC;
-    const size_t total = (size_t)B * Np;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-         i += (size_t)gridDim.x * blockDim.x) {
-        const int s = (int)(i % Np);
-        const size_t b = i / Np;
-        int c = ncls;
-        if (s < N) {
-            const int z = zone[b * N + s];
-            c = ((z < Z) ? z + 1 : 0) * FamC + famc[s];
-        }
-        cls[i] = (uint8_t)c;
-    }
-}
-
-// Sum the W task partials of each chain in task order (deterministic).
-__global__ void lik_reduce_kernel(int B, int W, const double *partial, double *out) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= B) return;
-    double s = 0.0;
-    for (int t = 0; t < W; t++) s += partial[(size_t)b * W + t];
-    out[b] = s;
-}
-
-// Row-major source [B][N][F] -> feature-major [B][F][Np] (padded sites -> component 0).
-__global__ void repack_source_kernel(int B, int N, int F, int Np, const uint8_t *src, uint8_t *dst) {
+// Row-major source [B][N][F] -> feature-major [B][F][Np] in the family-sorted site order
+// (padded sites -> component 0).
+__global__ void repack_source_kernel(int B, int N, int F, int Np, const int *perm, const uint8_t *src,
+                                     uint8_t *dst) {
     const size_t total = (size_t)B * F * Np;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
          i += (size_t)gridDim.x * blockDim.x) {
@@ -552,24 +801,34 @@ __global__ void repack_source_kernel(int B, int N, int F, int Np, const uint8_t 
         const size_t r = i / Np;
         const int f = (int)(r % F);
         const int b = (int)(r / F);
-        dst[i] = s < N ? src[((size_t)b * N + s) * F + f] : 0;
+        dst[i] = s < N ? src[((size_t)b * N + perm[s]) * F + f] : 0;
     }
 }
 
+// The mixture table kernel for these template choices (dense or zone-sparse).
 template <int C, int FR, bool XS8>
-void launch_mix_x(int spl, dim3 grid, size_t lds, hipStream_t st, const LikArgs &a) {
+const void *mix_kernel_x(bool zoned, int spl, int zspl) {
+    if (zoned) {
+        switch (zspl) {
+            case 4: return reinterpret_cast<const void *>(&lik_zoned_kernel<C, 4, FR, XS8>);
+            case 16: return reinterpret_cast<const void *>(&lik_zoned_kernel<C, 16, FR, XS8>);
+            default: return reinterpret_cast<const void *>(&lik_zoned_kernel<C, 8, FR, XS8>);
+        }
+    }
     switch (spl) {
-        case 4: lik_mixture_kernel<C, 4, FR, XS8><<<grid, WAVE, lds, st>>>(a); break;
-        case 8: lik_mixture_kernel<C, 8, FR, XS8><<<grid, WAVE, lds, st>>>(a); break;
-        case 16: lik_mixture_kernel<C, 16, FR, XS8><<<grid, WAVE, lds, st>>>(a); break;
-        default: lik_mixture_kernel<C, 32, FR, XS8><<<grid, WAVE, lds, st>>>(a); break;
+        case 4: return reinterpret_cast<const void *>(&lik_mixture_kernel<C, 4, FR, XS8>);
+        case 8: return reinterpret_cast<const void *>(&lik_mixture_kernel<C, 8, FR, XS8>);
+        case 16: return reinterpret_cast<const void *>(&lik_mixture_kernel<C, 16, FR, XS8>);
+        default: return reinterpret_cast<const void *>(&lik_mixture_kernel<C, 32, FR, XS8>);
     }
 }
 
-template <int C, int FR>
-void launch_mix(int spl, dim3 grid, size_t lds, hipStream_t st, const LikArgs &a) {
-    if (a.xs8) launch_mix_x<C, FR, true>(spl, grid, lds, st, a);
-    else launch_mix_x<C, FR, false>(spl, grid, lds, st, a);
+const void *mix_kernel(int C, int fr, bool xs8, bool zoned, int spl, int zspl) {
+    if (C == 3) {
+        if (fr == 4) return xs8 ? mix_kernel_x<3, 4, true>(zoned, spl, zspl) : mix_kernel_x<3, 4, false>(zoned, spl, zspl);
+        return xs8 ? mix_kernel_x<3, 8, true>(zoned, spl, zspl) : mix_kernel_x<3, 8, false>(zoned, spl, zspl);
+    }
+    return xs8 ? mix_kernel_x<2, 4, true>(zoned, spl, zspl) : mix_kernel_x<2, 4, false>(zoned, spl, zspl);
 }
 
 template <int C>
@@ -584,6 +843,9 @@ void launch_source(int spl, dim3 grid, size_t lds, hipStream_t st, const LikArgs
 
 template <int C, int FR, bool XS8>
 void configure_mix_x(std::vector<const void *> &v) {
+    v.push_back(reinterpret_cast<const void *>(&lik_zoned_kernel<C, 4, FR, XS8>));
+    v.push_back(reinterpret_cast<const void *>(&lik_zoned_kernel<C, 8, FR, XS8>));
+    v.push_back(reinterpret_cast<const void *>(&lik_zoned_kernel<C, 16, FR, XS8>));
     v.push_back(reinterpret_cast<const void *>(&lik_mixture_kernel<C, 4, FR, XS8>));
     v.push_back(reinterpret_cast<const void *>(&lik_mixture_kernel<C, 8, FR, XS8>));
     v.push_back(reinterpret_cast<const void *>(&lik_mixture_kernel<C, 16, FR, XS8>));
@@ -614,6 +876,13 @@ struct MixPlan {
     int fr = 0;
 };
 
+size_t mix_lds_bytes(const sbz_dims &d, int C) {
+    const size_t S1 = (size_t)d.n_states + 1;
+    const size_t Fam = C == 3 ? (size_t)d.n_families : 0;
+    const size_t ncls = (size_t)(d.n_zones + 1) * (Fam + 1);
+    return ((ncls + 1) * S1 + WAVE) * 8;
+}
+
 MixPlan plan_mixture(const sbz_dims &d, int C) {
     MixPlan p;
     const int S1 = d.n_states + 1;
@@ -622,21 +891,20 @@ MixPlan plan_mixture(const sbz_dims &d, int C) {
     const int G = WAVE / S1;
     if (d.n_zones + 1 > ZR * G) return p;
     if ((d.n_zones + 1) * (Fam + 1) + 1 > 256) return p;  // class ids are bytes
-    if ((1 + d.n_zones + Fam) * d.n_states + C > PL * WAVE) return p;
+    if (mix_lds_bytes(d, C) > 64 * 1024) return p;       // row offsets are 16-bit
     if (C == 2 || Fam <= 4) p.fr = 4;
     else if (Fam <= 8) p.fr = 8;
     return p;
 }
 
-size_t mix_lds_bytes(const sbz_dims &d, int C) {
-    const size_t S1 = (size_t)d.n_states + 1;
-    const size_t Fam = C == 3 ? (size_t)d.n_families : 0;
-    const size_t ncls = (size_t)(d.n_zones + 1) * (Fam + 1);
-    const size_t per = (1 + d.n_zones + Fam) * d.n_states + C;
-    return NW_BYTES + ((per + 1) & ~(size_t)1) * 8 + ((ncls + 1) * S1 + WAVE) * 8;
-}
-
 }  // namespace
+
+bool lik_counts_apply(const sbz_dims &d) {
+    const bool inh = (d.flags & SBZ_INHERITANCE) != 0;
+    const int C = inh ? 3 : 2;
+    const int FamC = inh ? d.n_families + 1 : 1;
+    return plan_mixture(d, C).fr != 0 && FamC * (d.n_states + 1) <= CP && d.n_sites < (1 << 24);
+}
 
 int sites_per_lane(int n_sites) {
     if (n_sites <= 4 * WAVE) return 4;
@@ -689,6 +957,7 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
     a.B = B;
     a.obs_fm = ctx->d_obs_fm;
     a.famc = ctx->d_famc;
+    a.perm = ctx->d_perm;
     a.zone = zone;
     a.w = w;
     a.pg = pg;
@@ -696,23 +965,37 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
     a.pf = pf;
 
     MixPlan plan;
+    bool zoned = false;
+    const void *mix_fn = nullptr;
     size_t lds = 0;
     int rc;
     if (!src_mode) {
         plan = plan_mixture(d, ctx->C);
         if (plan.fr) {
-            rc = ensure(ctx, ctx->cls, (size_t)B * ctx->Np);
-            if (rc) return rc;
-            const size_t n = (size_t)B * ctx->Np;
-            site_class_kernel<<<(int)std::min<size_t>((n + 255) / 256, 4096), 256, 0, ctx->stream>>>(
-                B, d.n_sites, ctx->Np, d.n_zones, ctx->FamC, zone, ctx->d_famc,
-                static_cast<uint8_t *>(ctx->cls.ptr));
-            a.cls = static_cast<const uint8_t *>(ctx->cls.ptr);
+            zoned = ctx->d_cnt != nullptr && ctx->lik_kernel == 2;
+            if (zoned) {
+                rc = ensure(ctx, ctx->zl, (size_t)B * d.n_sites * sizeof(uint32_t));
+                if (rc) return rc;
+                rc = ensure(ctx, ctx->nzs, (size_t)B * sizeof(int));
+                if (rc) return rc;
+                zone_list_kernel<<<B, WAVE, 0, ctx->stream>>>(
+                    d.n_sites, d.n_zones, ctx->FamC, zone, ctx->d_famc, ctx->d_perm,
+                    static_cast<uint32_t *>(ctx->zl.ptr), static_cast<int *>(ctx->nzs.ptr));
+                a.zl = static_cast<const uint32_t *>(ctx->zl.ptr);
+                a.nzs = static_cast<const int *>(ctx->nzs.ptr);
+                a.cnt = ctx->d_cnt;
+            }
             lds = mix_lds_bytes(d, ctx->C);
-            a.s_magic = ((1ull << 32) + d.n_states - 1) / d.n_states;  // ceil(2^32 / S)
-            // long tasks (the parameter pipeline amortises the set-up): ~2 rounds of
-            // 24 waves on 256 CUs
-            const int W = std::max(1, std::min((F + 1) / 2, (256 * 48 + B - 1) / B));
+            mix_fn = mix_kernel(ctx->C, plan.fr, ctx->xs8 != 0, zoned, ctx->spl, ctx->zspl);
+            // Long tasks: one resident round of single-wave tasks (occupancy x CUs) over the
+            // launch, so every wave streams its features with no tail of late tasks.
+            if (ctx->mix_occ == 0) {
+                int occ = 0;
+                hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, mix_fn, WAVE, lds);
+                ctx->mix_occ = (e == hipSuccess && occ > 0) ? occ : 8;
+            }
+            const int per_cu = ctx->tasks_per_cu > 0 ? ctx->tasks_per_cu : ctx->mix_occ;
+            const int W = std::max(1, std::min((F + 1) / 2, (ctx->n_cu * per_cu + B - 1) / B));
             a.fpw = (F + W - 1) / W;
         }
     } else {
@@ -731,13 +1014,21 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
     rc = ensure(ctx, ctx->partial, (size_t)B * a.W * sizeof(double));
     if (rc) return rc;
     a.partial = static_cast<double *>(ctx->partial.ptr);
+    if (ctx->ticket.bytes < (size_t)B * sizeof(unsigned) || !ctx->ticket.ptr) {
+        rc = ensure(ctx, ctx->ticket, (size_t)B * sizeof(unsigned));
+        if (rc) return rc;
+        hipError_t e = hipMemsetAsync(ctx->ticket.ptr, 0, ctx->ticket.bytes, ctx->stream);
+        if (e != hipSuccess) return hip_fail(ctx, e, "hipMemsetAsync(ticket)");
+    }
+    a.ticket = static_cast<unsigned *>(ctx->ticket.ptr);
+    a.out = out_ll;
 
     if (src_mode) {
         const size_t bytes = (size_t)B * F * ctx->Np;
         rc = ensure(ctx, ctx->src_t, bytes);
         if (rc) return rc;
         const int blocks = (int)std::min<size_t>((bytes + 255) / 256, 8192);
-        repack_source_kernel<<<blocks, 256, 0, ctx->stream>>>(B, d.n_sites, F, ctx->Np, source,
+        repack_source_kernel<<<blocks, 256, 0, ctx->stream>>>(B, d.n_sites, F, ctx->Np, ctx->d_perm, source,
                                                              static_cast<uint8_t *>(ctx->src_t.ptr));
         a.src_fm = static_cast<const uint8_t *>(ctx->src_t.ptr);
     }
@@ -751,14 +1042,10 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
         if (ctx->C == 3) lik_mixture_generic_kernel<3><<<grid, WAVE, 0, st>>>(a);
         else lik_mixture_generic_kernel<2><<<grid, WAVE, 0, st>>>(a);
     } else {
-        if (ctx->C == 3) {
-            if (plan.fr == 4) launch_mix<3, 4>(ctx->spl, grid, lds, st, a);
-            else launch_mix<3, 8>(ctx->spl, grid, lds, st, a);
-        } else {
-            launch_mix<2, 4>(ctx->spl, grid, lds, st, a);
-        }
+        void *args[] = {&a};
+        hipError_t e = hipLaunchKernel(mix_fn, grid, dim3(WAVE), args, lds, st);
+        if (e != hipSuccess) return hip_fail(ctx, e, "mixture kernel launch");
     }
-    lik_reduce_kernel<<<(B + 63) / 64, 64, 0, st>>>(B, a.W, a.partial, out_ll);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(ctx, e, "likelihood launch");
     return SBZ_OK;

@@ -34,9 +34,20 @@ def _assert_close(got, ref, tol=REL_TOL):
     return 0.0 if rel.size == 0 else float(rel.max())
 
 
+# Mixture-mode kernels: "dense" = every site gathered from the table (default), "zoned" =
+# zone-sparse counts kernel (SBZ_LIK_KERNEL is read when a context opens).
+MODES = [("mixture", "dense"), ("mixture", "zoned"), ("source", "dense")]
+
+
+@pytest.fixture
+def lik_kernel(request, monkeypatch):
+    monkeypatch.setenv("SBZ_LIK_KERNEL", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("case", CASES)
-@pytest.mark.parametrize("mode", ["mixture", "source"])
-def test_golden(gpu_available, case, mode):
+@pytest.mark.parametrize("mode,lik_kernel", MODES, indirect=["lik_kernel"])
+def test_golden(gpu_available, case, mode, lik_kernel):
     d = load_golden(case)
     eng = _engine(d)
     src = d["source"] if mode == "source" else None
@@ -88,8 +99,8 @@ def _random_batch(rng, N, F, S, Z, Fam, B, inheritance, zone_size, na=0.02):
     (2000, 500, 10, 8, 4, 4, True, 62),      # cfg5 shape (few chains vs the C oracle)
     (1000, 33, 7, 3, 2, 5, True, 100),       # ragged feature tile, odd S
 ])
-@pytest.mark.parametrize("mode", ["mixture", "source"])
-def test_random_vs_c_oracle(gpu_available, shape, mode):
+@pytest.mark.parametrize("mode,lik_kernel", MODES, indirect=["lik_kernel"])
+def test_random_vs_c_oracle(gpu_available, shape, mode, lik_kernel):
     from contact_zones_amd.likelihood import LikelihoodEngine
     from oracle import oracle_c
     N, F, S, Z, Fam, B, inh, zs = shape
@@ -162,3 +173,54 @@ def test_drop_in_likelihood_interface(gpu_available):
     for b in range(d["zone_of_site"].shape[0]):
         assert lik(Sample(b, False), caching=False) == pytest.approx(d["ll_mixture"][b], rel=1e-12)
         assert lik(Sample(b, True)) == pytest.approx(d["ll_source"][b], rel=1e-12)
+
+
+@pytest.mark.parametrize("zspl", ["4", "8", "16"])
+def test_zone_sparse_paths(gpu_available, monkeypatch, zspl):
+    """Zone-sparse kernel: several chunks of zoned sites, no zoned sites, all sites zoned,
+    zero no-zone table entries (exact slow path, finite and -inf) and untamed inputs."""
+    from contact_zones_amd.likelihood import LikelihoodEngine
+    from oracle import oracle_c
+    monkeypatch.setenv("SBZ_LIK_ZSPL", zspl)
+    monkeypatch.setenv("SBZ_LIK_KERNEL", "zoned")
+    N, F, S, Z, Fam, B = 1500, 40, 6, 4, 3, 7
+    rng = np.random.default_rng(11)
+    obs, fam, zos, w, pg, pz, pf, _ = _random_batch(rng, N, F, S, Z, Fam, B, True, 100)
+    zos[0] = rng.integers(0, Z, size=N)          # every site zoned (3 chunks at 8 per lane)
+    zos[1] = 255                                 # no zoned site
+    zos[2] = 255
+    zos[2, rng.permutation(N)[:700]] = rng.integers(0, Z, size=700)   # 700 zoned: 2 chunks at 8
+    # state 0 of feature 0 observed only at sites zoned in chains 3 and 4
+    zoned34 = (zos[3] != 255) & (zos[4] != 255)
+    obs[~zoned34 & (obs[:, 0] == 0), 0] = 1
+    for b in (3, 4):
+        pg[b, 0, 0] = 0.0
+        pf[b, :, 0, 0] = 0.0
+    # chain 4: one site outside every zone observes that state -> log 0 = -inf
+    s_out = int(np.flatnonzero(zos[4] == 255)[0])
+    obs[s_out, 0] = 0
+    zos[3, s_out] = 0                            # chain 3 keeps it zoned -> finite
+    # chain 5: untamed (tiny) parameters -> per-factor renormalisation
+    pg[5, :, 1] = 1e-200
+    # chain 6: a zero zone parameter on an observed state -> a zoned cell of exactly 0 (-inf
+    # unless another component covers it)
+    pz[6, :, :, 2] = 0.0
+    eng = LikelihoodEngine(obs, fam, S, Z, Fam, True)
+    got = eng.loglik(zos, w, pg, pz, pf)
+    ref = oracle_c.loglik_batch(obs, fam, zos, w, pg, pz, pf, inheritance=True)
+    assert np.isfinite(ref[3]) and ref[4] == -np.inf
+    _assert_close(got, ref, tol=1e-12)
+
+
+def test_chain_tickets_rearm_across_launches(gpu_available):
+    """The last-task reduction re-arms each chain's ticket: back-to-back launches of different
+    batch sizes (and task counts) reproduce single-chain values bit for bit."""
+    from contact_zones_amd.likelihood import LikelihoodEngine
+    rng = np.random.default_rng(21)
+    obs, fam, zos, w, pg, pz, pf, _ = _random_batch(rng, 700, 90, 5, 3, 2, 24, True, 30)
+    eng = LikelihoodEngine(obs, fam, 5, 3, 2, True)
+    ref = np.concatenate([eng.loglik(zos[b:b + 1], w[b:b + 1], pg[b:b + 1], pz[b:b + 1], pf[b:b + 1])
+                          for b in range(24)])
+    for sl in (slice(0, 24), slice(3, 8), slice(0, 1), slice(5, 22), slice(0, 24)):
+        got = eng.loglik(zos[sl], w[sl], pg[sl], pz[sl], pf[sl])
+        np.testing.assert_array_equal(got, ref[sl])
