@@ -101,6 +101,27 @@ def algorithmic_bytes(args, B, source=False):
     return P, D, B * P + D
 
 
+def workload_key(args, B):
+    return (f"{args.sites}x{args.features}x{args.states}/Z{args.zones}x{args.zone_size}/"
+            f"Fam{args.families}/B{B}/{args.mode}")
+
+
+def pmc_traffic(args, B):
+    """HBM bytes per launch of the dominant kernel from the newest committed PMC summary
+    (profiles/r*_pmc.json, written by tools/pmc.sh + tools/pmc_summary.py on this workload),
+    or None when no summary matches the workload."""
+    import glob
+    here = os.path.dirname(os.path.abspath(__file__))
+    for fn in sorted(glob.glob(os.path.join(here, "profiles", "r*_pmc.json")), reverse=True):
+        try:
+            d = json.load(open(fn))
+        except (OSError, ValueError):
+            continue
+        if d.get("_meta", {}).get("workload_key") == workload_key(args, B) and "_hbm" in d:
+            return d["_hbm"]["traffic_bytes"], os.path.relpath(fn, here)
+    return None, None
+
+
 def cpu_baseline(args, seconds):
     """Time the numpy restatement of Likelihood.__call__ (oracle, kind 'port') on 1 core."""
     import numpy as np
@@ -203,6 +224,7 @@ def main():
     launch_s = ev_ms / 1e3 / args.steps  # this rank's device time per step (lik + reduce launch)
     achieved = per_launch / launch_s / 1e9
 
+    traffic, traffic_src = pmc_traffic(args, B)
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -225,6 +247,8 @@ def main():
                 "global_chains": B * world,
                 "mode": args.mode,
                 "pool_batches": args.pool,
+                "zone_size": args.zone_size,
+                "workload_key": workload_key(args, B),
                 "parallelism": f"chains sharded over {world} GPU(s)",
             },
             "roofline": {
@@ -233,7 +257,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "bytes_per_eval": P + D / B,
                 "bytes_per_launch": per_launch,
                 "launch_us": launch_s * 1e6,

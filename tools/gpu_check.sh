@@ -12,6 +12,6 @@ run timeout -k 10 400 python bench.py --steps $STEPS --warmup 20 ${BENCH_ARGS:-}
 cat gpurun_out/bench.json
 if [ "${PROFILE:-1}" = "1" ]; then
   export TMPDIR=/tmp
-  run timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 50 --warmup 5 --cpu-seconds 0 ${BENCH_ARGS:-} > gpurun_out/prof.log 2>&1
+  run timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps $STEPS --warmup 20 --cpu-seconds 0 ${BENCH_ARGS:-} > gpurun_out/prof.log 2>&1
   find gpurun_out/prof -name "*kernel_stats.csv" -exec cat {} \;
 fi

@@ -5,7 +5,7 @@ set -u
 export TMPDIR=/tmp
 OUT=${PMC_OUT:-gpurun_out/pmc}
 mkdir -p $OUT
-ARGS="--steps 10 --warmup 2 --cpu-seconds 0 $*"
+ARGS="--steps 20 --warmup 4 --cpu-seconds 0 $*"
 i=0
 for pass in \
   "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS" \
