@@ -1,0 +1,304 @@
+"""Capture seeded Metropolis-Hastings trajectories from the reference sampler (BUILD CONTAINER ONLY).
+
+For each case the reference's own ZoneMCMC / ZoneMCMCWarmup (sbayes/sampling/zone_sampling.py)
+runs `generate_samples` with np.random and python `random` seeded.  Every random decision the
+step loop consumes is recorded per chain, in consumption order, as a "tape" of float64 items:
+
+  op          operator id (OPS below), from np.random.choice(fn_operators, p=...)
+                                          (mcmc_generative.py:294)
+  z / f / fam np.random.choice(range(n))  (zone_sampling.py:417, 466, 506-507, 584-585, 729, 810, 889)
+  u_conn      random.random()             (connected step, zone_sampling.py:733, 817)
+  k           random.choice(seq) index    (the k-th candidate / member in ascending order, 742, 825, 896)
+  a, b        random.sample(pop, 2)       (the two altered weights / states, 421, 470, 510, 588)
+  d0, d1      np.random.dirichlet(alpha)  (the two components of the proposal, dirichlet_proposal :555)
+  u_acc       random.random()             (accept, mcmc_generative.py:318)
+
+The outcome of every step is recorded too: operator, accepted flag, the chain's log-likelihood
+after the step, and its zone assignment (zone_of_site).  The replay (oracle/mh_numpy.py on the
+CPU, the HIP sampler on the GPU) consumes the same tape and must reproduce the outcomes.
+Writes tests/golden/mh_<case>.npz.  Run: python tests/golden/make_golden_mh.py
+"""
+import os
+import random
+import sys
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+sys.path.insert(0, ROOT)
+
+import refenv  # noqa: E402
+from contact_zones_amd import packing  # noqa: E402
+
+refenv.setup()
+
+# canonical operator ids (contact_zones_amd/sampler.py OPS uses the same order)
+OPS = ["shrink_zone", "grow_zone", "swap_zone", "alter_weights", "alter_p_global",
+       "alter_p_zones", "alter_p_families", "gibbsish_sample_zones"]
+
+
+class Tape:
+    """Per-chain record of the decisions, in consumption order."""
+
+    def __init__(self):
+        self.chain = None
+        self.items = {}
+
+    def put(self, *vals):
+        if self.chain is None:  # initial-sample generation: not part of the step tape
+            return
+        self.items.setdefault(self.chain, []).extend(float(v) for v in vals)
+
+
+TAPE = Tape()
+
+
+class RecordingRandom:
+    """Stand-in for the `random` module as used by the samplers (`_random`), recording draws."""
+
+    def __init__(self, seed):
+        self._rng = random.Random(seed)
+
+    def random(self):
+        u = self._rng.random()
+        TAPE.put(u)
+        return u
+
+    def choice(self, seq):
+        k = self._rng._randbelow(len(seq))  # random.choice (Python 3.10): seq[_randbelow(len(seq))]
+        TAPE.put(k)
+        return seq[k]
+
+    def sample(self, population, k):
+        out = self._rng.sample(population, k)
+        TAPE.put(*out)
+        return out
+
+    def choices(self, population, weights=None, *, cum_weights=None, k=1):
+        return self._rng.choices(population, weights, cum_weights=cum_weights, k=k)
+
+
+def install_recorders(seed, zs_mod, mg_mod):
+    rec = RecordingRandom(seed)
+    zs_mod._random = rec
+    mg_mod._random = rec
+    orig_choice = np.random.choice
+    orig_dirichlet = np.random.dirichlet
+
+    def choice(a, size=None, replace=True, p=None):
+        out = orig_choice(a, size, replace, p)
+        if p is not None:  # operator choice: record the canonical id of the chosen operator
+            TAPE.put(OPS.index(out[0].__name__))
+        else:
+            TAPE.put(out)
+        return out
+
+    def dirichlet(alpha, size=None):
+        out = orig_dirichlet(alpha, size)
+        TAPE.put(*out)
+        return out
+
+    np.random.choice = choice
+    np.random.dirichlet = dirichlet
+
+    def restore():
+        np.random.choice = orig_choice
+        np.random.dirichlet = orig_dirichlet
+
+    return restore
+
+
+def run_case(name, data, model_cfg, mcmc_cfg, steps, seed, warmup, n_chains):
+    from sbayes.model import Model
+    from sbayes.sampling import zone_sampling as zs
+    from sbayes.sampling import mcmc_generative as mg
+
+    np.random.seed(seed)
+    restore = install_recorders(seed, zs, mg)
+    TAPE.chain, TAPE.items = None, {}
+    try:
+        model = Model(data=data, config=model_cfg)
+        a = mcmc_cfg["STEPS"]
+        ops = {"shrink_zone": a["area"] * 0.4, "grow_zone": a["area"] * 0.4,
+               "swap_zone": a["area"] * 0.2, "gibbsish_sample_zones": a["area"] * 0.0,
+               "alter_weights": a["weights"], "alter_p_global": a["universal"],
+               "alter_p_zones": a["contact"]}
+        if model_cfg["INHERITANCE"]:
+            ops["alter_p_families"] = a["inheritance"]
+        tot = sum(ops.values())
+        ops = {k: v / tot for k, v in ops.items()}
+        cls = zs.ZoneMCMCWarmup if warmup else zs.ZoneMCMC
+        sampler = cls(data=data, model=model, n_chains=n_chains, operators=ops,
+                      var_proposal=mcmc_cfg["PROPOSAL_PRECISION"],
+                      p_grow_connected=mcmc_cfg["P_GROW_CONNECTED"],
+                      initial_size=mcmc_cfg["M_INITIAL"], logger=None)
+
+        N = data.features.shape[0]
+        init, steps_out = {}, {c: [] for c in range(n_chains)}
+        orig_step = sampler.step
+        orig_init = sampler.generate_initial_sample
+
+        def gen_init(c=0):
+            TAPE.chain = None
+            s = orig_init(c)
+            init[c] = s.copy()
+            return s
+
+        def step(sample, c):
+            TAPE.chain = c
+            acc0 = sampler.statistics["accepted_steps"]
+            n0 = len(TAPE.items.get(c, []))
+            new = orig_step(sample, c)
+            TAPE.chain = None
+            op = int(TAPE.items[c][n0])
+            steps_out[c].append((op, sampler.statistics["accepted_steps"] > acc0,
+                                 float(sampler._ll[c]),
+                                 packing.zones_to_zone_of_site(new.zones, N)))
+            return new
+
+        sampler.step = step
+        sampler.generate_initial_sample = gen_init
+        if warmup:
+            best = sampler.generate_samples(n_steps=0, n_samples=0, warm_up=True, warm_up_steps=steps)
+        else:
+            sampler.generate_samples(steps, max(1, steps // 10))
+            best = None
+    finally:
+        restore()
+
+    C = 3 if model_cfg["INHERITANCE"] else 2
+    out = {}
+    out["obs"] = packing.features_to_obs(data.features)
+    out["states"] = np.asarray(data.states, bool)
+    adj = data.network["adj_mat"].tocsr()
+    adj.sort_indices()
+    assert np.all(adj.data != 0)
+    out["adj_indptr"] = adj.indptr.astype(np.int32)
+    out["adj_indices"] = adj.indices.astype(np.int32)
+    fam_of_site = (packing.families_to_fam_of_site(data.families, N) if model_cfg["INHERITANCE"]
+                   else np.full(N, 255, np.uint8))
+    out["fam_of_site"] = fam_of_site
+    out["inheritance"] = np.array(model_cfg["INHERITANCE"])
+    out["warmup"] = np.array(warmup)
+    out["n_zones"] = np.array(model_cfg["N_AREAS"])
+    out["min_size"] = np.array(model_cfg["MIN_M"])
+    max_size = sampler.max_size if warmup else [model_cfg["MAX_M"]] * n_chains
+    p_grow = sampler.p_grow_connected if warmup else [mcmc_cfg["P_GROW_CONNECTED"]] * n_chains
+    out["max_size"] = np.asarray(max_size, np.int32)
+    out["p_grow_connected"] = np.asarray(p_grow, np.float64)
+    prec = mcmc_cfg["PROPOSAL_PRECISION"]
+    out["precision"] = np.array([prec["weights"], prec["universal"], prec["contact"],
+                                 prec["inheritance"] if prec["inheritance"] is not None else 0.0])
+    probs = np.zeros(len(OPS))
+    for k, v in ops.items():
+        probs[OPS.index(k)] = v
+    out["op_probs"] = probs
+    out["init_zone_of_site"] = np.stack([packing.zones_to_zone_of_site(init[c].zones, N)
+                                         for c in range(n_chains)])
+    out["init_w"] = np.stack([init[c].weights for c in range(n_chains)])
+    out["init_p_global"] = np.stack([init[c].p_global[0] for c in range(n_chains)])
+    out["init_p_zones"] = np.stack([init[c].p_zones for c in range(n_chains)])
+    if model_cfg["INHERITANCE"]:
+        out["init_p_fam"] = np.stack([init[c].p_families for c in range(n_chains)])
+    L = max(len(TAPE.items.get(c, [])) for c in range(n_chains))
+    tape = np.full((n_chains, L), np.nan)
+    for c in range(n_chains):
+        tape[c, :len(TAPE.items[c])] = TAPE.items[c]
+    out["tape"] = tape
+    out["tape_len"] = np.array([len(TAPE.items[c]) for c in range(n_chains)])
+    out["step_op"] = np.array([[s[0] for s in steps_out[c]] for c in range(n_chains)], np.int8)
+    out["step_accept"] = np.array([[s[1] for s in steps_out[c]] for c in range(n_chains)], bool)
+    out["step_ll"] = np.array([[s[2] for s in steps_out[c]] for c in range(n_chains)])
+    out["step_zone_of_site"] = np.array([[s[3] for s in steps_out[c]] for c in range(n_chains)],
+                                        np.uint8)
+    if warmup:
+        out["best_zone_of_site"] = packing.zones_to_zone_of_site(best.zones, N)
+    path = os.path.join(HERE, f"mh_{name}.npz")
+    np.savez_compressed(path, **out)
+    acc = out["step_accept"].mean()
+    print(f"{name:22s} chains={n_chains} steps={steps} tape={L} accept={acc:.3f} "
+          f"ops={np.bincount(out['step_op'].ravel(), minlength=len(OPS))} -> {os.path.getsize(path)} B")
+    assert C in (2, 3)
+
+
+def sim_data(inheritance_families=0, seed=1):
+    """sim_exp1 simulated by the reference (as make_golden_lik.case_cfg1_sim); optional
+    synthetic families (the simulation config has none) for the inheritance model."""
+    from sbayes.experiment_setup import Experiment
+    from sbayes.simulation import Simulation
+    exp_dir = refenv.scratch_copy("experiments/simulation/sim_exp1")
+    np.random.seed(seed)
+    random.seed(seed)
+    exp = Experiment(experiment_name="golden", config_file=os.path.join(exp_dir, "config.json"), log=False)
+    exp.load_config(os.path.join(exp_dir, "config.json"), custom_settings={
+        "simulation": {"I_CONTACT": 3, "E_CONTACT": 0.5, "STRENGTH": 1, "AREA": 4}})
+    sim = Simulation(experiment=exp)
+    sim.run_simulation()
+    N = sim.features.shape[0]
+    fams = None
+    if inheritance_families:
+        rng = np.random.default_rng(seed + 100)
+        lab = rng.integers(0, inheritance_families + 1, size=N)  # label 0: no family
+        fams = np.stack([lab == i + 1 for i in range(inheritance_families)])
+    return types.SimpleNamespace(features=sim.features, states=sim.states, network=sim.network,
+                                 families=fams)
+
+
+def small_data(seed=7, N=40, F=12, S=4, fam=2):
+    """A small random network (Delaunay of random points, the reference's compute_network) that
+    hits the size bounds and the no-candidate rejections often."""
+    from sbayes.preprocessing import compute_network
+    rng = np.random.default_rng(seed)
+    sites = {"id": list(range(N)), "locations": rng.random((N, 2)) * 100,
+             "names": [f"s{i}" for i in range(N)]}
+    net = compute_network(sites)
+    states = np.ones((F, S), bool)
+    states[rng.random((F, S)) < 0.25] = False
+    states[:, :2] = True
+    x = np.zeros((N, F, S), bool)
+    for f in range(F):
+        st = np.flatnonzero(states[f])
+        xs = rng.choice(st, size=N)
+        x[np.arange(N), f, xs] = True
+    x[rng.random((N, F)) < 0.05] = False  # NA cells
+    lab = rng.integers(0, fam + 1, size=N)
+    fams = np.stack([lab == i + 1 for i in range(fam)])
+    return types.SimpleNamespace(features=x, states=states, network=net, families=fams)
+
+
+def model_cfg(Z, inheritance, min_m=3, max_m=50):
+    return {"N_AREAS": Z, "MIN_M": min_m, "MAX_M": max_m, "INHERITANCE": inheritance,
+            "SAMPLE_SOURCE": False,
+            "PRIOR": {"geo": {"type": "uniform"}, "area_size": {"type": "none"},
+                      "weights": {"type": "uniform"}, "universal": {"type": "uniform"},
+                      "inheritance": {"type": "uniform"}, "contact": {"type": "uniform"}}}
+
+
+def mcmc_cfg(area=0.4, m_initial=5, p_grow=0.85, inheritance=0.1):
+    return {"P_GROW_CONNECTED": p_grow, "M_INITIAL": m_initial,
+            "PROPOSAL_PRECISION": {"weights": 15, "universal": 40, "contact": 20, "inheritance": 20},
+            "STEPS": {"area": area, "weights": 0.2, "universal": 0.1, "contact": 0.2,
+                      "inheritance": inheritance}}
+
+
+def main():
+    d = sim_data()
+    run_case("cfg1_sim", d, model_cfg(1, False), mcmc_cfg(inheritance=0.0), steps=300, seed=3,
+             warmup=False, n_chains=2)
+    d3 = sim_data(inheritance_families=3)
+    run_case("cfg1_sim_inh_z2", d3, model_cfg(2, True), mcmc_cfg(), steps=300, seed=4,
+             warmup=False, n_chains=2)
+    run_case("cfg1_sim_warmup", d3, model_cfg(2, True), mcmc_cfg(), steps=200, seed=5,
+             warmup=True, n_chains=4)
+    s = small_data()
+    run_case("small_bounds", s, model_cfg(3, True, min_m=3, max_m=6), mcmc_cfg(area=0.8, m_initial=4),
+             steps=400, seed=6, warmup=False, n_chains=3)
+    run_case("small_warmup", s, model_cfg(2, True, min_m=3, max_m=8), mcmc_cfg(area=0.8, m_initial=4),
+             steps=300, seed=8, warmup=True, n_chains=4)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,39 @@
+"""The CPU MH restatement (oracle/mh_numpy.py) replays the reference's captured trajectories
+bit for bit (tests/golden/make_golden_mh.py: seeded ZoneMCMC / ZoneMCMCWarmup runs)."""
+import numpy as np
+import pytest
+
+from conftest import golden_cases, load_golden
+
+MH_CASES = golden_cases(prefix="mh_", exclude=())
+
+
+@pytest.mark.parametrize("case", MH_CASES)
+def test_oracle_replays_reference_trajectory(case):
+    from oracle import mh_numpy
+    fx = load_golden(case)
+    lls = []
+    for c in range(fx["tape"].shape[0]):
+        r = mh_numpy.replay(fx, c)
+        np.testing.assert_array_equal(r["op"], fx["step_op"][c])
+        np.testing.assert_array_equal(r["accept"], fx["step_accept"][c])
+        np.testing.assert_array_equal(r["zos"], fx["step_zone_of_site"][c])
+        np.testing.assert_array_equal(r["ll"], fx["step_ll"][c])
+        assert r["tape_used"] == int(fx["tape_len"][c])
+        lls.append(r["ll"][-1])
+    if bool(fx["warmup"]):
+        # best chain = argmax(ll + prior) after the warm-up (mcmc_generative.py:195-200)
+        best = int(np.argmax(lls))
+        np.testing.assert_array_equal(fx["step_zone_of_site"][best, -1], fx["best_zone_of_site"])
+
+
+def test_fixtures_cover_every_operator_and_rejection_kind():
+    ops = np.zeros(7, int)
+    rejected_zone_moves = 0
+    for case in MH_CASES:
+        fx = load_golden(case)
+        ops += np.bincount(fx["step_op"].ravel(), minlength=8)[:7]
+        zone = fx["step_op"] <= 2
+        rejected_zone_moves += int(np.sum(zone & ~fx["step_accept"]))
+    assert np.all(ops > 50), ops
+    assert rejected_zone_moves > 50
