@@ -27,6 +27,29 @@ class sbz_dims(ctypes.Structure):
                 ("n_families", ctypes.c_int32), ("flags", ctypes.c_int32)]
 
 
+_D = ctypes.c_double
+
+
+class sbz_mh_config(ctypes.Structure):
+    _fields_ = [("op_prob", _D * 8), ("precision", _D * 4), ("min_size", ctypes.c_int32),
+                ("warmup", ctypes.c_int32)]
+
+
+class sbz_chains(ctypes.Structure):
+    """Device pointers of a sampler run (include/sbz.h)."""
+    _fields_ = [("zone_of_site", ctypes.c_void_p), ("w", ctypes.c_void_p),
+                ("p_global", ctypes.c_void_p), ("p_zones", ctypes.c_void_p),
+                ("p_fam", ctypes.c_void_p), ("ll", ctypes.c_void_p),
+                ("max_size", ctypes.c_void_p), ("p_grow_connected", ctypes.c_void_p),
+                ("tape", ctypes.c_void_p), ("tape_stride", ctypes.c_int64),
+                ("tape_len", ctypes.c_void_p), ("tape_pos", ctypes.c_void_p),
+                ("seed", ctypes.c_uint64), ("chain_id0", ctypes.c_uint64),
+                ("counter", ctypes.c_void_p), ("accepted", ctypes.c_void_p),
+                ("proposed", ctypes.c_void_p), ("status", ctypes.c_void_p),
+                ("trace_op", ctypes.c_void_p), ("trace_accept", ctypes.c_void_p),
+                ("trace_ll", ctypes.c_void_p), ("trace_zos", ctypes.c_void_p)]
+
+
 # name -> (restype, argtypes); every symbol declared in include/sbz.h
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -45,6 +68,9 @@ SIGNATURES = {
     "sbz_memcpy_h2d": (_I, [_P, _P, _P, ctypes.c_uint64]),
     "sbz_memcpy_d2h": (_I, [_P, _P, _P, ctypes.c_uint64]),
     "sbz_lik_lds_bytes": (ctypes.c_uint64, [ctypes.POINTER(sbz_dims), _I]),
+    "sbz_set_network": (_I, [_P, _P, ctypes.c_int32, _P, _P]),
+    "sbz_mh_run_device": (_I, [_P, _I, _I, ctypes.POINTER(sbz_mh_config), ctypes.POINTER(sbz_chains)]),
+    "sbz_mh_lds_bytes": (ctypes.c_uint64, [ctypes.POINTER(sbz_dims)]),
 }
 
 _lib = None

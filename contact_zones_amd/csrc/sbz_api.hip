@@ -23,8 +23,8 @@ int hip_fail(sbz_ctx *ctx, hipError_t e, const char *what) {
 int ensure(sbz_ctx *ctx, DevBuf &buf, size_t bytes) {
     if (buf.bytes >= bytes && buf.ptr) return SBZ_OK;
     if (buf.ptr) {
-        hipStreamSynchronize(ctx->stream);
-        hipFree(buf.ptr);
+        (void)hipStreamSynchronize(ctx->stream);
+        (void)hipFree(buf.ptr);
         buf.ptr = nullptr;
         buf.bytes = 0;
     }
@@ -40,7 +40,7 @@ int ensure(sbz_ctx *ctx, DevBuf &buf, size_t bytes) {
 }
 
 static void free_buf(DevBuf &b) {
-    if (b.ptr) hipFree(b.ptr);
+    if (b.ptr) (void)hipFree(b.ptr);
     b.ptr = nullptr;
     b.bytes = 0;
 }
@@ -175,6 +175,18 @@ int sbz_open(int device, const sbz_dims *dims, const int8_t *obs, const uint8_t 
         sbz_close(ctx);
         return SBZ_ENOMEM;
     }
+    // site-major observations and family classes for the sampler's per-site deltas
+    {
+        std::vector<uint8_t> obs_sm((size_t)N * F);
+        for (size_t i = 0; i < obs_sm.size(); i++) obs_sm[i] = (uint8_t)(obs[i] < 0 ? S : obs[i]);
+        if (hipMalloc(&ctx->d_obs_sm, obs_sm.size()) != hipSuccess ||
+            hipMalloc(&ctx->d_fam_site, (size_t)N) != hipSuccess ||
+            hipMemcpy(ctx->d_obs_sm, obs_sm.data(), obs_sm.size(), hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(ctx->d_fam_site, famc_site.data(), (size_t)N, hipMemcpyHostToDevice) != hipSuccess) {
+            sbz_close(ctx);
+            return SBZ_ENOMEM;
+        }
+    }
     if (hipMalloc(&ctx->d_obs_fm, obs_fm.size()) != hipSuccess ||
         hipMalloc(&ctx->d_famc, famc.size()) != hipSuccess ||
         hipMalloc(&ctx->d_perm, perm.size() * sizeof(int)) != hipSuccess) {
@@ -200,12 +212,15 @@ int sbz_open(int device, const sbz_dims *dims, const int8_t *obs, const uint8_t 
 
 void sbz_close(sbz_ctx *ctx) {
     if (!ctx) return;
-    if (ctx->own_stream) hipStreamSynchronize(ctx->own_stream);
+    if (ctx->own_stream) (void)hipStreamSynchronize(ctx->own_stream);
     if (ctx->stream != ctx->own_stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->d_obs_fm) (void)hipFree(ctx->d_obs_fm);
-    if (ctx->d_famc) hipFree(ctx->d_famc);
-    if (ctx->d_perm) hipFree(ctx->d_perm);
-    if (ctx->d_cnt) hipFree(ctx->d_cnt);
+    if (ctx->d_famc) (void)hipFree(ctx->d_famc);
+    if (ctx->d_perm) (void)hipFree(ctx->d_perm);
+    for (void *p : {(void *)ctx->d_obs_sm, (void *)ctx->d_fam_site, (void *)ctx->d_adj_ptr,
+                    (void *)ctx->d_adj_idx, (void *)ctx->d_app_list, (void *)ctx->d_app_cnt})
+        if (p) (void)hipFree(p);
+    if (ctx->d_cnt) (void)hipFree(ctx->d_cnt);
     free_buf(ctx->zl);
     free_buf(ctx->nzs);
     free_buf(ctx->partial);
@@ -213,7 +228,7 @@ void sbz_close(sbz_ctx *ctx) {
     free_buf(ctx->ticket);
     free_buf(ctx->stage);
     free_buf(ctx->out);
-    if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
+    if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;
 }
 
@@ -242,7 +257,7 @@ int sbz_loglik_batch_device(sbz_ctx *ctx, int B, const uint8_t *zone_of_site, co
     if (B < 0 || !zone_of_site || !w || !p_global || !out_ll ||
         (ctx->d.n_zones > 0 && !p_zones))
         return fail(ctx, SBZ_EINVAL, "null argument or negative B");
-    hipSetDevice(ctx->device);
+    (void)hipSetDevice(ctx->device);
     return launch_loglik(ctx, B, zone_of_site, w, p_global, p_zones, p_fam, source, out_ll);
 }
 
@@ -254,7 +269,7 @@ int sbz_loglik_batch(sbz_ctx *ctx, int B, const uint8_t *zone_of_site, const dou
         (ctx->d.n_zones > 0 && !p_zones))
         return fail(ctx, SBZ_EINVAL, "null argument or negative B");
     if (B == 0) return SBZ_OK;
-    hipSetDevice(ctx->device);
+    (void)hipSetDevice(ctx->device);
     const sbz_dims &d = ctx->d;
     const size_t N = d.n_sites, F = d.n_features, S = d.n_states, Z = d.n_zones,
                  Fam = d.n_families, C = ctx->C;
@@ -299,9 +314,59 @@ int sbz_loglik_batch(sbz_ctx *ctx, int B, const uint8_t *zone_of_site, const dou
     return SBZ_OK;
 }
 
+int sbz_set_network(sbz_ctx *ctx, const uint8_t *applicable, int32_t nnz, const int32_t *adj_indptr,
+                    const int32_t *adj_indices) {
+    if (!ctx) return SBZ_EINVAL;
+    const int N = ctx->d.n_sites, F = ctx->d.n_features, S = ctx->d.n_states;
+    if (!applicable || !adj_indptr || (nnz > 0 && !adj_indices) || nnz < 0)
+        return fail(ctx, SBZ_EINVAL, "null network argument");
+    if (adj_indptr[0] != 0 || adj_indptr[N] != nnz)
+        return fail(ctx, SBZ_EINVAL, "adj_indptr must start at 0 and end at nnz");
+    for (int s = 0; s < N; s++)
+        if (adj_indptr[s + 1] < adj_indptr[s]) return fail(ctx, SBZ_EINVAL, "adj_indptr not monotone");
+    for (int i = 0; i < nnz; i++)
+        if (adj_indices[i] < 0 || adj_indices[i] >= N)
+            return fail(ctx, SBZ_EINVAL, "adjacency index out of range");
+    std::vector<int> list((size_t)F * S, 0), cnt(F, 0);
+    for (int f = 0; f < F; f++)
+        for (int x = 0; x < S; x++)
+            if (applicable[(size_t)f * S + x]) list[(size_t)f * S + cnt[f]++] = x;
+    (void)hipSetDevice(ctx->device);
+    for (void *p : {(void *)ctx->d_adj_ptr, (void *)ctx->d_adj_idx, (void *)ctx->d_app_list,
+                    (void *)ctx->d_app_cnt})
+        if (p) (void)hipFree(p);
+    ctx->d_adj_ptr = ctx->d_adj_idx = ctx->d_app_list = ctx->d_app_cnt = nullptr;
+    const size_t bp = (size_t)(N + 1) * 4, bi = (size_t)std::max(nnz, 1) * 4;
+    if (hipMalloc(&ctx->d_adj_ptr, bp) != hipSuccess || hipMalloc(&ctx->d_adj_idx, bi) != hipSuccess ||
+        hipMalloc(&ctx->d_app_list, list.size() * 4) != hipSuccess ||
+        hipMalloc(&ctx->d_app_cnt, cnt.size() * 4) != hipSuccess)
+        return fail(ctx, SBZ_ENOMEM, "network allocation failed");
+    hipError_t e = hipMemcpy(ctx->d_adj_ptr, adj_indptr, bp, hipMemcpyHostToDevice);
+    if (e == hipSuccess && nnz > 0)
+        e = hipMemcpy(ctx->d_adj_idx, adj_indices, (size_t)nnz * 4, hipMemcpyHostToDevice);
+    ctx->adj_nnz = nnz;
+    if (e == hipSuccess) e = hipMemcpy(ctx->d_app_list, list.data(), list.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(ctx->d_app_cnt, cnt.data(), cnt.size() * 4, hipMemcpyHostToDevice);
+    return e == hipSuccess ? SBZ_OK : hip_fail(ctx, e, "network upload");
+}
+
+int sbz_mh_run_device(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg,
+                      const sbz_chains *chains) {
+    if (!ctx) return SBZ_EINVAL;
+    if (!cfg || !chains || B < 0 || n_steps < 0) return fail(ctx, SBZ_EINVAL, "bad sampler arguments");
+    (void)hipSetDevice(ctx->device);
+    return launch_mh(ctx, B, n_steps, cfg, chains);
+}
+
+uint64_t sbz_mh_lds_bytes(const sbz_dims *dims) {
+    if (!dims) return 0;
+    const size_t b = mh_lds_bytes(*dims, (dims->flags & SBZ_INHERITANCE) ? 3 : 2);
+    return b > 64 * 1024 ? 0 : b;
+}
+
 int sbz_device_alloc(sbz_ctx *ctx, uint64_t bytes, void **out) {
     if (!ctx || !out) return SBZ_EINVAL;
-    hipSetDevice(ctx->device);
+    (void)hipSetDevice(ctx->device);
     hipError_t e = hipMalloc(out, std::max<uint64_t>(bytes, 1));
     return e == hipSuccess ? SBZ_OK : fail(ctx, SBZ_ENOMEM, hipGetErrorString(e));
 }

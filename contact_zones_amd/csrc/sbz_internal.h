@@ -54,6 +54,12 @@ struct sbz_ctx {
     uint8_t *d_famc = nullptr;
     int *d_perm = nullptr;  // [Np] site index of each position (family-sorted order)
     int *d_cnt = nullptr;  // [F][128] site counts by (family class, x), or null (dense kernel)
+    // sampler data (sbz_open / sbz_set_network)
+    uint8_t *d_obs_sm = nullptr;    // [N][F] x by site (S = NA)
+    uint8_t *d_fam_site = nullptr;  // [N] family class by site
+    int *d_adj_ptr = nullptr, *d_adj_idx = nullptr;  // CSR network
+    int adj_nnz = 0;
+    int *d_app_list = nullptr, *d_app_cnt = nullptr; // [F][S] applicable states, [F] counts
     int zspl = 8;          // zoned sites per lane and chunk of the zone-sparse kernel
     int lik_kernel = 1;    // SBZ_LIK_KERNEL: 1 dense (default), 2 zone-sparse ("zoned")
     int tasks_per_cu = 0;  // SBZ_LIK_TASKS: single-wave tasks per CU per launch (0: occupancy)
@@ -77,6 +83,10 @@ int lik_configure(sbz_ctx *ctx);
 bool lik_counts_apply(const sbz_dims &d);
 // Sites per lane of the likelihood kernels for n_sites (4, 8, 16 or 32).
 int sites_per_lane(int n_sites);
+
+// Sampler (sbz_mh.hip)
+size_t mh_lds_bytes(const sbz_dims &d, int C);
+int launch_mh(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg, const sbz_chains *chains);
 
 // Launch the likelihood kernels for B chains (all pointers device); out_ll device [B].
 int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, const double *pg,

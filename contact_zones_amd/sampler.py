@@ -1,0 +1,177 @@
+"""Batched Metropolis-Hastings on the GPU (sbz_mh_run_device) — the sampler side of the hot path.
+
+``Sampler`` runs many independent chains of the sBayes zone model on one MI355X: each chain is
+one wave that executes ``MCMCGenerative.step`` (sbayes/sampling/mcmc_generative.py:282-351)
+with the ZoneMCMC / ZoneMCMCWarmup operators (sbayes/sampling/zone_sampling.py:408-933,
+1272-1577) for n steps per launch.  Chain state stays resident in HBM (torch tensors);
+``ChainState`` holds it.  Draws come from Philox (production) or from a replay tape of the
+reference's own decisions (parity tests).
+
+Supported model: SAMPLE_SOURCE = false, uniform priors (the reference default priors,
+config/default_config.json:35-42).  Operator names and their canonical order follow
+``include/sbz.h`` (sbz_op).
+"""
+import ctypes
+
+import numpy as np
+
+from ._lib import check, sbz_chains, sbz_mh_config
+
+OPS = ["shrink_zone", "grow_zone", "swap_zone", "alter_weights", "alter_p_global",
+       "alter_p_zones", "alter_p_families", "gibbsish_sample_zones"]
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def op_probabilities(operators):
+    """Operator weights (dict name -> weight, as MCMC.steps_per_operator builds them,
+    mcmc_setup.py:70-95) -> float64[8] in canonical order."""
+    p = np.zeros(len(OPS))
+    for name, v in operators.items():
+        if name not in OPS:
+            raise ValueError(f"unknown operator {name!r} (sampler supports {OPS[:7]})")
+        p[OPS.index(name)] = float(v)
+    if p[OPS.index("gibbsish_sample_zones")] != 0.0:
+        raise ValueError("gibbsish_sample_zones must have weight 0 (as in the reference, mcmc_setup.py:77)")
+    return p
+
+
+def precisions(var_proposal):
+    """PROPOSAL_PRECISION dict (weights, universal, contact, inheritance) -> float64[4]."""
+    if isinstance(var_proposal, dict):
+        inh = var_proposal.get("inheritance")
+        return np.array([var_proposal["weights"], var_proposal["universal"],
+                         var_proposal["contact"], 0.0 if inh is None else inh], np.float64)
+    return np.asarray(var_proposal, np.float64)
+
+
+class ChainState:
+    """Device-resident state of B chains (torch tensors on the engine's GPU)."""
+
+    def __init__(self, engine, zone_of_site, w, p_global, p_zones, p_fam=None):
+        torch = _torch()
+        dev = torch.device("cuda", engine.device)
+        self.engine = engine
+        f64 = torch.float64
+        self.zone_of_site = torch.as_tensor(np.ascontiguousarray(zone_of_site, np.uint8), device=dev)
+        self.B = int(self.zone_of_site.shape[0])
+        self.w = torch.as_tensor(np.ascontiguousarray(w, np.float64), device=dev, dtype=f64)
+        self.p_global = torch.as_tensor(np.ascontiguousarray(p_global, np.float64), device=dev, dtype=f64)
+        self.p_zones = torch.as_tensor(np.ascontiguousarray(p_zones, np.float64), device=dev, dtype=f64)
+        self.p_fam = (torch.as_tensor(np.ascontiguousarray(p_fam, np.float64), device=dev, dtype=f64)
+                      if engine.inheritance else None)
+        engine._check_shapes(self.B, self.zone_of_site, self.w, self.p_global, self.p_zones,
+                             self.p_fam, None)
+        self.ll = torch.empty(self.B, dtype=f64, device=dev)
+        self.accepted = torch.zeros((self.B, 8), dtype=torch.int64, device=dev)
+        self.proposed = torch.zeros((self.B, 8), dtype=torch.int64, device=dev)
+        self.counter = torch.zeros(self.B, dtype=torch.int64, device=dev)
+        self.refresh_ll()
+
+    def refresh_ll(self):
+        """Recompute every chain's log-likelihood from scratch (the likelihood kernel)."""
+        torch = _torch()
+        eng = self.engine
+        eng.set_stream(torch.cuda.current_stream(self.ll.device).cuda_stream)
+        eng.loglik_device(self.B, self.zone_of_site.data_ptr(), self.w.data_ptr(),
+                          self.p_global.data_ptr(), self.p_zones.data_ptr(),
+                          self.p_fam.data_ptr() if self.p_fam is not None else 0, 0,
+                          self.ll.data_ptr())
+        return self.ll
+
+    def to_numpy(self):
+        out = {"zone_of_site": self.zone_of_site.cpu().numpy(), "w": self.w.cpu().numpy(),
+               "p_global": self.p_global.cpu().numpy(), "p_zones": self.p_zones.cpu().numpy(),
+               "ll": self.ll.cpu().numpy()}
+        if self.p_fam is not None:
+            out["p_fam"] = self.p_fam.cpu().numpy()
+        return out
+
+
+class Sampler:
+    """MH sampler over a LikelihoodEngine's context (same data, same GPU)."""
+
+    def __init__(self, engine, applicable_states, adj_indptr, adj_indices, operators, var_proposal,
+                 min_size, warmup=False):
+        self.engine = engine
+        states = np.ascontiguousarray(applicable_states, dtype=np.uint8)
+        if states.shape != (engine.n_features, engine.n_states):
+            raise ValueError(f"applicable_states: expected {(engine.n_features, engine.n_states)}")
+        if np.any(states.sum(axis=1) < 2):
+            raise ValueError("every feature needs at least 2 applicable states (random.sample(., 2))")
+        indptr = np.ascontiguousarray(adj_indptr, dtype=np.int32)
+        indices = np.ascontiguousarray(adj_indices, dtype=np.int32)
+        lib = engine._lib
+        check(lib.sbz_set_network(engine.ctx, states.ctypes.data_as(ctypes.c_void_p),
+                                  int(indices.size), indptr.ctypes.data_as(ctypes.c_void_p),
+                                  indices.ctypes.data_as(ctypes.c_void_p)), engine.ctx)
+        self.cfg = sbz_mh_config()
+        probs = operators if isinstance(operators, np.ndarray) else op_probabilities(operators)
+        for i in range(8):
+            self.cfg.op_prob[i] = float(probs[i])
+        prec = precisions(var_proposal)
+        for i in range(4):
+            self.cfg.precision[i] = float(prec[i])
+        self.cfg.min_size = int(min_size)
+        self.cfg.warmup = int(bool(warmup))
+
+    def run(self, state, n_steps, max_size, p_grow_connected, seed=0, chain_id0=0, tape=None,
+            tape_len=None, tape_pos=None, trace=False, trace_zones=False):
+        """Run n_steps MH steps on every chain of `state` (in place).
+
+        max_size / p_grow_connected: scalars or per-chain arrays (warm-up: get_max_size_list and
+        the 0.95 / configured mix, zone_sampling.py:1276-1291).  With `tape` (float64 [B, L]),
+        the chains replay recorded decisions; `tape_pos` (int64 [B] device tensor) carries the
+        cursor between calls.  Returns a dict of device tensors (traces when requested)."""
+        torch = _torch()
+        eng = self.engine
+        dev = state.ll.device
+        B = state.B
+        ms = torch.as_tensor(np.broadcast_to(np.asarray(max_size, np.int32), (B,)).copy(), device=dev)
+        pg = torch.as_tensor(np.broadcast_to(np.asarray(p_grow_connected, np.float64), (B,)).copy(),
+                             device=dev)
+        ch = sbz_chains()
+        ch.zone_of_site = state.zone_of_site.data_ptr()
+        ch.w = state.w.data_ptr()
+        ch.p_global = state.p_global.data_ptr()
+        ch.p_zones = state.p_zones.data_ptr()
+        ch.p_fam = state.p_fam.data_ptr() if state.p_fam is not None else None
+        ch.ll = state.ll.data_ptr()
+        ch.max_size = ms.data_ptr()
+        ch.p_grow_connected = pg.data_ptr()
+        out = {"status": torch.zeros(B, dtype=torch.int32, device=dev)}
+        ch.status = out["status"].data_ptr()
+        keep = [ms, pg]
+        if tape is not None:
+            t = torch.as_tensor(np.ascontiguousarray(tape, np.float64), device=dev)
+            tl = torch.as_tensor(np.asarray(tape_len, np.int64), device=dev)
+            tp = tape_pos if tape_pos is not None else torch.zeros(B, dtype=torch.int64, device=dev)
+            ch.tape = t.data_ptr()
+            ch.tape_stride = int(t.shape[1])
+            ch.tape_len = tl.data_ptr()
+            ch.tape_pos = tp.data_ptr()
+            out["tape_pos"] = tp
+            keep += [t, tl]
+        ch.seed = int(seed) & (2**64 - 1)
+        ch.chain_id0 = int(chain_id0)
+        ch.counter = state.counter.data_ptr()
+        ch.accepted = state.accepted.data_ptr()
+        ch.proposed = state.proposed.data_ptr()
+        if trace:
+            out["op"] = torch.empty((B, n_steps), dtype=torch.int8, device=dev)
+            out["accept"] = torch.empty((B, n_steps), dtype=torch.uint8, device=dev)
+            out["ll"] = torch.empty((B, n_steps), dtype=torch.float64, device=dev)
+            ch.trace_op = out["op"].data_ptr()
+            ch.trace_accept = out["accept"].data_ptr()
+            ch.trace_ll = out["ll"].data_ptr()
+        if trace_zones:
+            out["zone_of_site"] = torch.empty((B, n_steps, eng.n_sites), dtype=torch.uint8, device=dev)
+            ch.trace_zos = out["zone_of_site"].data_ptr()
+        eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        check(eng._lib.sbz_mh_run_device(eng.ctx, B, int(n_steps), ctypes.byref(self.cfg),
+                                         ctypes.byref(ch)), eng.ctx)
+        out["_keep"] = keep  # the launch is asynchronous: keep its inputs alive
+        return out

@@ -9,8 +9,8 @@
  *       replaces  Likelihood.__call__(sample, caching=False)      sbayes/model.py:145-171
  *       (incl.    update_component_likelihoods :230-249, update_weights :257-294,
  *                 normalize_weights :436-452, combine_lh :173-184)  — B chains per call
- *   sbz_mh_*
- *       replaces  MCMCGenerative.step / generate_samples           sbayes/sampling/mcmc_generative.py:149-351
+ *   sbz_set_network / sbz_mh_run_device
+ *       replaces  MCMCGenerative.step (the generate_samples hot loops) sbayes/sampling/mcmc_generative.py:149-351
  *       with the  operators of ZoneMCMC / ZoneMCMCWarmup           sbayes/sampling/zone_sampling.py:408-933,1272-1577
  *
  * Conventions
@@ -112,6 +112,62 @@ int sbz_memcpy_d2h(sbz_ctx *ctx, void *dst, const void *src, uint64_t bytes);
 
 /* Bytes of LDS the likelihood kernel needs per workgroup for these dims (0 if unsupported). */
 uint64_t sbz_lik_lds_bytes(const sbz_dims *dims, int source_mode);
+
+/* ------------------------------------------------------------------------------------------
+ * Metropolis-Hastings sampler  (MCMCGenerative.step, sbayes/sampling/mcmc_generative.py:282-351,
+ * operators of ZoneMCMC / ZoneMCMCWarmup, sbayes/sampling/zone_sampling.py:408-933, 1272-1577;
+ * SAMPLE_SOURCE = false, uniform priors).  One wave runs one chain for n_steps in one launch.
+ * ------------------------------------------------------------------------------------------ */
+
+/* Canonical operator order of sbz_mh_config.op_prob. */
+enum sbz_op {
+    SBZ_OP_SHRINK_ZONE = 0, SBZ_OP_GROW_ZONE = 1, SBZ_OP_SWAP_ZONE = 2, SBZ_OP_ALTER_WEIGHTS = 3,
+    SBZ_OP_ALTER_P_GLOBAL = 4, SBZ_OP_ALTER_P_ZONES = 5, SBZ_OP_ALTER_P_FAMILIES = 6,
+    SBZ_OP_GIBBSISH_SAMPLE_ZONES = 7 /* reference weight 0 (mcmc_setup.py:77); must stay 0 */
+};
+
+typedef struct sbz_mh_config {
+    double op_prob[8];    /* operator weights, SBZ_OP_* order (normalised here) (mcmc_setup.py:70-95) */
+    double precision[4];  /* PROPOSAL_PRECISION: weights, universal, contact, inheritance */
+    int32_t min_size;     /* MIN_M (model.py:43) */
+    int32_t warmup;       /* 1: ZoneMCMCWarmup semantics (shrink back-probability 1/(size+1)) */
+} sbz_mh_config;
+
+/* Chain state and I/O of a run; every pointer is a device pointer, chain-major (B chains). */
+typedef struct sbz_chains {
+    uint8_t *zone_of_site;            /* [B][N] in/out (255 = no zone) */
+    double *w, *p_global, *p_zones, *p_fam;  /* in/out, layouts as sbz_loglik_batch */
+    double *ll;                       /* [B] in/out: the chain's current log-likelihood */
+    const int32_t *max_size;          /* [B] MAX_M per chain (warm-up: get_max_size_list) */
+    const double *p_grow_connected;   /* [B] per chain (warm-up: 0.95 or the configured value) */
+    /* draws: a replay tape of the reference's decisions (tests/golden/make_golden_mh.py) ... */
+    const double *tape;               /* [B][tape_stride] or NULL for Philox */
+    int64_t tape_stride;
+    const int64_t *tape_len;          /* [B] */
+    int64_t *tape_pos;                /* [B] in/out cursor */
+    /* ... or Philox4x32-10 keyed by seed, counter (ctr, global chain id) */
+    uint64_t seed;
+    uint64_t chain_id0;               /* global id of chain 0 (rank offset) */
+    uint64_t *counter;                /* [B] in/out, or NULL (start at 0) */
+    int64_t *accepted, *proposed;     /* [B][8] accumulated per operator, or NULL */
+    int32_t *status;                  /* [B] 1 = tape exhausted, or NULL */
+    int8_t *trace_op;                 /* [B][n_steps] or NULL */
+    uint8_t *trace_accept;            /* [B][n_steps] (with trace_op) */
+    double *trace_ll;                 /* [B][n_steps] (with trace_op) */
+    uint8_t *trace_zos;               /* [B][n_steps][N] or NULL (tests) */
+} sbz_chains;
+
+/* Sampler-only data: applicable states (uint8 [F][S], data.states) and the site network as CSR
+ * (data.network['adj_mat'], sbayes/util.py:139-155; rows sorted).  Call once after sbz_open. */
+int sbz_set_network(sbz_ctx *ctx, const uint8_t *applicable, int32_t nnz, const int32_t *adj_indptr,
+                    const int32_t *adj_indices);
+
+/* Run n_steps MH steps on B device-resident chains; asynchronous on ctx's stream. */
+int sbz_mh_run_device(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg,
+                      const sbz_chains *chains);
+
+/* Bytes of LDS the sampler needs per chain for these dims (0 if above the 64 KiB limit). */
+uint64_t sbz_mh_lds_bytes(const sbz_dims *dims);
 
 #ifdef __cplusplus
 }
