@@ -216,6 +216,35 @@ def run_case(name, data, model_cfg, mcmc_cfg, steps, seed, warmup, n_chains):
                                         np.uint8)
     if warmup:
         out["best_zone_of_site"] = packing.zones_to_zone_of_site(best.zones, N)
+        out["best_w"] = np.asarray(best.weights)
+        out["best_p_global"] = np.asarray(best.p_global)[0]
+        out["best_p_zones"] = np.asarray(best.p_zones)
+        if model_cfg["INHERITANCE"]:
+            out["best_p_fam"] = np.asarray(best.p_families)
+    else:
+        # the reference's own statistics dict (mcmc_generative.py:56-71, 205-237)
+        st = sampler.statistics
+        out["stat_n_samples"] = np.array(max(1, steps // 10))
+        out["stat_sample_id"] = np.asarray(st["sample_id"], np.int64)
+        out["stat_sample_likelihood"] = np.asarray(st["sample_likelihood"], np.float64)
+        out["stat_sample_prior"] = np.asarray(st["sample_prior"], np.float64)
+        out["stat_sample_zones"] = np.asarray(st["sample_zones"], bool)
+        out["stat_sample_weights"] = np.asarray(st["sample_weights"], np.float64)
+        out["stat_sample_p_global"] = np.asarray(st["sample_p_global"], np.float64)
+        out["stat_sample_p_zones"] = np.asarray(st["sample_p_zones"], np.float64)
+        if model_cfg["INHERITANCE"]:
+            out["stat_sample_p_families"] = np.asarray(st["sample_p_families"], np.float64)
+        out["stat_accepted_steps"] = np.array(st["accepted_steps"])
+        out["stat_acceptance_ratio"] = np.array(st["acceptance_ratio"])
+        out["stat_accept_operator"] = np.array([st["accept_operator"].get(k, 0) for k in OPS])
+        out["stat_reject_operator"] = np.array([st["reject_operator"].get(k, 0) for k in OPS])
+        out["stat_last_zones"] = np.asarray(st["last_sample"].zones, bool)
+        out["stat_last_weights"] = np.asarray(st["last_sample"].weights, np.float64)
+    # run metadata (for the host-side drop-in tests: initial samples, warm-up lists)
+    out["seed"] = np.array(seed)
+    out["initial_size"] = np.array(mcmc_cfg["M_INITIAL"])
+    out["max_m"] = np.array(model_cfg["MAX_M"])
+    out["p_grow_base"] = np.array(mcmc_cfg["P_GROW_CONNECTED"])
     path = os.path.join(HERE, f"mh_{name}.npz")
     np.savez_compressed(path, **out)
     acc = out["step_accept"].mean()

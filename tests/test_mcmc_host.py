@@ -1,0 +1,121 @@
+"""Host side of the batched sampler drop-in (CPU): initial samples, warm-up chain lists and the
+model checks, pinned to the reference's own values captured in tests/golden/mh_*.npz."""
+import random
+import types
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from conftest import golden_cases, load_golden
+from contact_zones_amd import packing
+from contact_zones_amd.mcmc import (BatchedZoneMCMC, BatchedZoneMCMCWarmup, InitialSamples,
+                                    check_model, get_max_size_list)
+from contact_zones_amd.sampler import OPS
+
+MH_CASES = golden_cases("mh_", exclude=())
+
+
+def objects_from_fixture(fx):
+    """Reference-shaped (model, data, kwargs) for a captured case."""
+    N = fx["obs"].shape[0]
+    S = fx["states"].shape[1]
+    inh = bool(fx["inheritance"])
+    n_fam = fx["init_p_fam"].shape[1] if inh else 0
+    adj = sp.csr_matrix((np.ones(fx["adj_indices"].size), fx["adj_indices"], fx["adj_indptr"]),
+                        shape=(N, N))
+    data = types.SimpleNamespace(
+        features=packing.obs_to_features(fx["obs"], S), states=fx["states"],
+        network={"adj_mat": adj},
+        families=packing.index_to_groups(fx["fam_of_site"], n_fam) if inh else None)
+    model = types.SimpleNamespace(n_zones=int(fx["n_zones"]), min_size=int(fx["min_size"]),
+                                  max_size=int(fx["max_m"]), inheritance=inh, sample_source=False)
+    ops = {OPS[i]: float(p) for i, p in enumerate(fx["op_probs"]) if p > 0 or OPS[i] == "gibbsish_sample_zones"}
+    prec = fx["precision"]
+    var_proposal = {"weights": prec[0], "universal": prec[1], "contact": prec[2],
+                    "inheritance": prec[3] if inh else None}
+    kw = dict(model=model, data=data, operators=ops, n_chains=fx["init_w"].shape[0],
+              var_proposal=var_proposal, p_grow_connected=float(fx["p_grow_base"]),
+              initial_size=int(fx["initial_size"]))
+    return kw
+
+
+def make_sampler(fx, **extra):
+    kw = objects_from_fixture(fx)
+    cls = BatchedZoneMCMCWarmup if bool(fx["warmup"]) else BatchedZoneMCMC
+    return cls(rng=random.Random(int(fx["seed"])), **kw, **extra)
+
+
+@pytest.mark.parametrize("case", MH_CASES)
+def test_initial_samples_match_reference(case):
+    """generate_initial_sample for every chain, in the reference's draw order, from the same
+    seeded python random source: zones, weights and p_* identical to the reference's."""
+    fx = load_golden(case)
+    smp = make_sampler(fx)
+    N = fx["obs"].shape[0]
+    for c in range(fx["init_w"].shape[0]):
+        s = smp.generate_initial_sample(c)
+        np.testing.assert_array_equal(packing.zones_to_zone_of_site(s.zones, N), fx["init_zone_of_site"][c])
+        np.testing.assert_array_equal(s.weights, fx["init_w"][c])
+        np.testing.assert_array_equal(s.p_global[0], fx["init_p_global"][c])
+        np.testing.assert_array_equal(s.p_zones, fx["init_p_zones"][c])
+        if bool(fx["inheritance"]):
+            np.testing.assert_array_equal(s.p_families, fx["init_p_fam"][c])
+
+
+@pytest.mark.parametrize("case", [c for c in MH_CASES if "warmup" in c])
+def test_warmup_chain_lists_match_reference(case):
+    """ZoneMCMCWarmup: max_size list (util.get_max_size_list) and p_grow_connected choices."""
+    fx = load_golden(case)
+    smp = make_sampler(fx)
+    np.testing.assert_array_equal(np.asarray(smp.max_size), fx["max_size"])
+    np.testing.assert_array_equal(np.asarray(smp.p_grow_connected), fx["p_grow_connected"])
+
+
+def test_max_size_list():
+    assert get_max_size_list(2.25, 6, 3, 4) == [2, 3, 4]
+    assert get_max_size_list(13.75, 50, 15, 4) == [13] * 4 + [22] * 4 + [31] * 4 + [40] * 3
+
+
+def test_initial_sample_reuses_previous_sample():
+    """initial_sample (the warm-up winner) is taken as is; missing zones are grown."""
+    fx = load_golden("mh_small_bounds")
+    kw = objects_from_fixture(fx)
+    s0 = make_sampler(fx).generate_initial_sample(0)
+    init = InitialSamples(kw["data"].features.astype(bool), fx["states"], fx["adj_indptr"],
+                          fx["adj_indices"], kw["data"].families, 3, 4, True,
+                          s0, random.Random(1))
+    s = init(0)
+    np.testing.assert_array_equal(s.zones, s0.zones)
+    np.testing.assert_array_equal(s.p_zones, s0.p_zones)
+    np.testing.assert_array_equal(s.p_families, s0.p_families)
+    assert s.p_global is s0.p_global  # the reference does not copy it (zone_sampling.py:1068)
+
+
+def test_model_checks():
+    ok = types.SimpleNamespace(sample_source=False, inheritance=True, prior=types.SimpleNamespace(
+        config={"geo": {"type": "uniform"}, "area_size": {"type": "none"},
+                "weights": {"type": "uniform"}, "universal": {"type": "uniform"},
+                "inheritance": {"type": "uniform"}, "contact": {"type": "uniform"}}))
+    check_model(ok)
+    with pytest.raises(NotImplementedError):
+        check_model(types.SimpleNamespace(sample_source=True, inheritance=False))
+    bad = types.SimpleNamespace(**vars(ok))
+    bad.prior = types.SimpleNamespace(config=dict(ok.prior.config, universal={"type": "counts"}))
+    with pytest.raises(NotImplementedError):
+        check_model(bad)
+    bad.prior = types.SimpleNamespace(config=dict(ok.prior.config, area_size={"type": "uniform"}))
+    with pytest.raises(NotImplementedError):
+        check_model(bad)
+
+
+def test_unsupported_options_raise():
+    fx = load_golden("mh_cfg1_sim")
+    kw = objects_from_fixture(fx)
+    with pytest.raises(NotImplementedError):
+        BatchedZoneMCMC(mc3=True, **kw)
+    with pytest.raises(NotImplementedError):
+        BatchedZoneMCMC(sample_from_prior=True, **kw)
+    kw2 = dict(kw, operators={"grow_zone": 1.0, "gibbs_sample_sources": 0.5})
+    with pytest.raises(ValueError):
+        BatchedZoneMCMC(**kw2)

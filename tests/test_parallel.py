@@ -1,0 +1,82 @@
+"""Chain sharding and the sampler's collectives, world_size 2 over gloo on the CPU (the same code
+runs over RCCL on the GPU box; see contact_zones_amd/parallel.py)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from contact_zones_amd.parallel import (all_reduce_sum, best_chain, broadcast_arrays,
+                                        broadcast_seed, gather_rows, owner_of, shard_range)
+
+
+def test_shard_range_covers_every_chain_once():
+    for n in (0, 1, 5, 15, 256, 2048, 2049):
+        for w in (1, 2, 3, 4, 8):
+            seen = []
+            for r in range(w):
+                lo, hi = shard_range(n, r, w)
+                assert 0 <= lo <= hi <= n
+                assert hi - lo in (n // w, n // w + 1)
+                seen += list(range(lo, hi))
+                for c in range(lo, hi):
+                    assert owner_of(c, n, w) == r
+            assert seen == list(range(n))
+    with pytest.raises(ValueError):
+        shard_range(4, 2, 2)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, results):
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    try:
+        out = {}
+        out["seed"] = broadcast_seed(1234 if rank == 0 else 999)
+        out["sum"] = all_reduce_sum(torch.tensor([[rank + 1, 10], [2, 3]], dtype=torch.int64)).tolist()
+        # log posterior per global chain: 7 chains, max 5.0 at chains 2 and 5 (tie -> 2)
+        post = np.array([1.0, -2.0, 5.0, 0.0, 3.0, 5.0, 4.0])
+        lo, hi = shard_range(7, rank, world)
+        out["best"] = best_chain(post[lo:hi], lo)
+        # no chain on one rank: still participates
+        lo0, hi0 = (0, 3) if rank == 0 else (3, 3)
+        out["best_empty"] = best_chain(np.array([0.5, 2.0, -1.0])[lo0:hi0], lo0)
+        owner = owner_of(5, 7, world)
+        arrs = [np.arange(12, dtype=np.float64).reshape(3, 4), np.array([[True, False]]),
+                np.zeros((0, 3))] if rank == owner else None
+        got = broadcast_arrays(arrs, owner)
+        out["bcast"] = [(a.dtype.str, a.shape, a.tolist()) for a in got]
+        local = torch.arange(lo * 10, hi * 10, dtype=torch.float64).reshape(hi - lo, 10)
+        out["gather"] = gather_rows(local, 7).tolist()
+        results[rank] = out
+    finally:
+        dist.destroy_process_group()
+
+
+def test_collectives_world_size_2():
+    port = _free_port()
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    with mp.Manager() as m:
+        results = m.dict()
+        mp.spawn(_worker, args=(2, port, results), nprocs=2, join=True)
+        res = dict(results)
+    for r in range(2):
+        o = res[r]
+        assert o["seed"] == 1234
+        assert o["sum"] == [[3, 20], [4, 6]]
+        assert o["best"] == (2, 5.0)
+        assert o["best_empty"] == (1, 2.0)
+        assert o["bcast"][0] == ("<f8", (3, 4), np.arange(12.0).reshape(3, 4).tolist())
+        assert o["bcast"][1] == ("|b1", (1, 2), [[True, False]])
+        assert o["bcast"][2][1] == (0, 3)
+        assert o["gather"] == np.arange(70, dtype=np.float64).reshape(7, 10).tolist()
