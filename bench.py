@@ -46,6 +46,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0,
                    help="bounded CPU-baseline sample (0 disables)")
     p.add_argument("--seed", type=int, default=5)
+    p.add_argument("--mh-steps", type=int, default=20000,
+                   help="sampler leg: timed MH steps per chain (0 disables the leg)")
+    p.add_argument("--mh-burnin", type=int, default=20000, help="sampler leg: untimed MH steps")
     return p.parse_args()
 
 
@@ -151,6 +154,119 @@ def cpu_baseline(args, seconds):
                       f"1 chain at {N}x{F}x{S}, Z={Z}, Fam={Fam}: {n} evals in {el:.1f} s, 1 thread"}
 
 
+# sampler leg: the reference defaults (config/default_config.json:6-20, 29-30)
+MH_STEPS_CFG = {"area": 0.05, "weights": 0.4, "universal": 0.05, "contact": 0.4, "inheritance": 0.1}
+MH_PRECISION = {"weights": 15, "universal": 40, "contact": 20, "inheritance": 20}
+MH_MIN_M, MH_MAX_M, MH_M_INITIAL, MH_P_GROW = 3, 50, 5, 0.85
+
+
+def mh_operators():
+    """MCMC.steps_per_operator (mcmc_setup.py:70-95), SAMPLE_SOURCE = false, normalised."""
+    a = MH_STEPS_CFG
+    ops = {"shrink_zone": a["area"] * 0.4, "grow_zone": a["area"] * 0.4, "swap_zone": a["area"] * 0.2,
+           "gibbsish_sample_zones": 0.0, "alter_weights": a["weights"],
+           "alter_p_global": a["universal"], "alter_p_zones": a["contact"],
+           "alter_p_families": a["inheritance"]}
+    tot = sum(ops.values())
+    return {k: v / tot for k, v in ops.items()}
+
+
+def make_network(N, rng):
+    """Delaunay adjacency of random locations (the reference's compute_network) as sorted CSR."""
+    import numpy as np
+    from scipy.spatial import Delaunay
+    import scipy.sparse as sp
+    indptr, indices = Delaunay(rng.random((N, 2))).vertex_neighbor_vertices
+    a = sp.csr_matrix((np.ones(indices.size), indices, indptr), shape=(N, N))
+    a.sort_indices()
+    return a.indptr.astype(np.int32), a.indices.astype(np.int32)
+
+
+def sampler_leg(args, eng, obs, fam, dev, rank, world, stream):
+    """B chains x K MH steps in one launch (ZoneMCMC.step, default operators); ESS of the
+    log-likelihood traces (contact_zones_amd/diagnostics.py)."""
+    import random
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from contact_zones_amd import packing
+    from contact_zones_amd.diagnostics import ess
+    from contact_zones_amd.mcmc import InitialSamples
+    from contact_zones_amd.sampler import ChainState, Sampler, precisions
+    N, F, S, Z, Fam = args.sites, args.features, args.states, args.zones, args.families
+    B, K = args.chains, args.mh_steps
+    rng = np.random.default_rng(args.seed + 17)
+    indptr, indices = make_network(N, rng)  # same network on every rank
+    states = np.ones((F, S), bool)
+    feats = packing.obs_to_features(obs, S)
+    fams = packing.index_to_groups(fam, Fam)
+    init = InitialSamples(feats, states, indptr, indices, fams, Z, MH_M_INITIAL, True, None,
+                          random.Random(args.seed * 1000003 + rank))
+    pg0, pf0, w0 = init.p_global()[0], init.p_families(), init.weights()
+    zos = np.empty((B, N), np.uint8)
+    pz = np.empty((B, Z, F, S))
+    for b in range(B):  # generate_initial_sample per chain (zones + p_zones MLE; the rest shared)
+        zones = init.zones()
+        zos[b] = packing.zones_to_zone_of_site(zones, N)
+        pz[b] = init.p_zones(zones)
+    rep = lambda a: np.broadcast_to(a, (B,) + a.shape).copy()  # noqa: E731
+    st = ChainState(eng, zos, rep(w0), rep(pg0), pz, rep(pf0))
+    smp = Sampler(eng, states, indptr, indices, mh_operators(), precisions(MH_PRECISION), MH_MIN_M)
+    seed = args.seed * 7919
+    if args.mh_burnin > 0:
+        smp.run(st, args.mh_burnin, MH_MAX_M, MH_P_GROW, seed=seed, chain_id0=rank * B)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    out = smp.run(st, K, MH_MAX_M, MH_P_GROW, seed=seed, chain_id0=rank * B, trace=True)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    status = out["status"].cpu().numpy()
+    if np.any(status != 0):
+        raise SystemExit(f"sampler leg: chain status {np.unique(status)}")
+    ll_trace = out["ll"].cpu().numpy()
+    ll_full = st.ll.clone()
+    st.refresh_ll()  # drift of the incremental log-likelihood over burn-in + K steps
+    drift = float(((st.ll - ll_full).abs() / st.ll.abs()).max())
+    e = ess(ll_trace)
+    acc = out["accept"].float().mean().item()
+    t = torch.tensor([wall, ev0.elapsed_time(ev1) / 1e3, float(e.sum()), drift, acc],
+                     dtype=torch.float64, device=dev)
+    if world > 1:
+        red = t.clone()
+        dist.all_reduce(red, op=dist.ReduceOp.MAX)
+        sm = t.clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        t = torch.stack([red[0], red[1], sm[2], red[3], sm[4] / world])
+    wall_max, dev_s, ess_tot, drift_max, acc_mean = (float(v) for v in t)
+    return {
+        "mh_steps_per_sec": B * K * world / wall_max,
+        "ess_per_sec": ess_tot / wall_max,
+        "ess_total": ess_tot,
+        "ess_per_chain_mean": ess_tot / (B * world),
+        "chains": B * world,
+        "steps": K,
+        "burnin": args.mh_burnin,
+        "wall_s": wall_max,
+        "device_s": dev_s,
+        "us_per_step": dev_s / K * 1e6,
+        "acceptance": acc_mean,
+        "ll_drift_rel_max": drift_max,
+        "operators": "default_config.json STEPS (area .05 / weights .4 / universal .05 / contact .4 / "
+                     "inheritance .1), PROPOSAL_PRECISION 15/40/20/20, MIN_M 3, MAX_M 50, M_INITIAL 5, "
+                     "P_GROW_CONNECTED .85; Delaunay network of random locations; Philox draws",
+    }
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -225,6 +341,9 @@ def main():
     achieved = per_launch / launch_s / 1e9
 
     traffic, traffic_src = pmc_traffic(args, B)
+    sampler = None
+    if args.mh_steps > 0 and args.mode == "mixture":
+        sampler = sampler_leg(args, eng, obs, fam, dev, rank, world, stream)
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -265,9 +384,17 @@ def main():
             },
             "device_time_s": ev_max,
         }
+        if sampler is not None:
+            line["sampler"] = sampler
         if world == 1 and args.cpu_seconds > 0:
             line["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
             line["speedup_vs_cpu"] = value / line["cpu_baseline"]["value"]
+            if sampler is not None:
+                # a reference MH step costs one Likelihood.__call__ (combine + weights are ~94% of
+                # the step at cfg5): its steps/s is the CPU evals/s
+                cpu_steps = line["cpu_baseline"]["value"]
+                sampler["cpu_reference_steps_per_sec_est"] = cpu_steps
+                sampler["speedup_vs_cpu_steps"] = sampler["mh_steps_per_sec"] / cpu_steps
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
