@@ -46,9 +46,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0,
                    help="bounded CPU-baseline sample (0 disables)")
     p.add_argument("--seed", type=int, default=5)
-    p.add_argument("--mh-steps", type=int, default=20000,
+    p.add_argument("--mh-steps", type=int, default=50000,
                    help="sampler leg: timed MH steps per chain (0 disables the leg)")
-    p.add_argument("--mh-burnin", type=int, default=20000, help="sampler leg: untimed MH steps")
+    p.add_argument("--mh-burnin", type=int, default=200000, help="sampler leg: untimed MH steps")
     return p.parse_args()
 
 
