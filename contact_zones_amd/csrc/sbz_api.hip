@@ -151,7 +151,8 @@ int sbz_open(int device, const sbz_dims *dims, const int8_t *obs, const uint8_t 
             obs_fm[(size_t)f * Np + p] = (uint8_t)((x < 0 ? S : x) * scale);
         }
     }
-    if (const char *v = getenv("SBZ_LIK_KERNEL")) ctx->lik_kernel = strcmp(v, "zoned") == 0 ? 2 : 1;
+    if (const char *v = getenv("SBZ_LIK_KERNEL"))
+        ctx->lik_kernel = strcmp(v, "zoned") == 0 ? 2 : (strcmp(v, "db") == 0 ? 3 : 1);
     if (const char *v = getenv("SBZ_LIK_TASKS")) ctx->tasks_per_cu = std::max(1, atoi(v));
     if (const char *v = getenv("SBZ_LIK_ZSPL")) {
         const int z = atoi(v);

@@ -61,7 +61,8 @@ struct sbz_ctx {
     int adj_nnz = 0;
     int *d_app_list = nullptr, *d_app_cnt = nullptr; // [F][S] applicable states, [F] counts
     int zspl = 8;          // zoned sites per lane and chunk of the zone-sparse kernel
-    int lik_kernel = 1;    // SBZ_LIK_KERNEL: 1 dense (default), 2 zone-sparse ("zoned")
+    int lik_kernel = 1;    // SBZ_LIK_KERNEL: 1 dense (default), 2 zone-sparse ("zoned"),
+                           // 3 dense double-buffered ("db", where the table fits 4 KiB)
     int tasks_per_cu = 0;  // SBZ_LIK_TASKS: single-wave tasks per CU per launch (0: occupancy)
     int mix_occ = 0;       // resident mixture-kernel waves per CU (queried at first launch)
     int n_cu = 256;        // compute units of the device

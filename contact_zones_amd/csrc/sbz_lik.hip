@@ -30,6 +30,7 @@
 //     (deterministic, bit-reproducible).
 #include <algorithm>
 #include <cmath>
+#include <type_traits>
 #include <vector>
 
 #include "sbz_internal.h"
@@ -130,7 +131,8 @@ __device__ __forceinline__ void store_nw(double *nw, int lane, double w0r, doubl
 // gathers would then wait for the next feature's loads.
 // ---------------------------------------------------------------------------------------
 #ifndef SBZ_ABLATE
-#define SBZ_ABLATE 0  // diagnostic builds only: 1 = skip gathers, 2 = skip table build (wrong results)
+#define SBZ_ABLATE 0  // diagnostic builds only: 1 = skip gathers, 2 = skip table build,
+                      // 4 = skip tame checks, 8 = skip NA selects (wrong results)
 #endif
 #ifndef SBZ_MIX_WAVES
 #define SBZ_MIX_WAVES 3  // launch bound: minimum waves per SIMD of the dense mixture kernel
@@ -146,6 +148,12 @@ __device__ __forceinline__ void store_nw(double *nw, int lane, double w0r, doubl
 // instructions execute in issue order, so within a single-wave workgroup a read issued after a
 // write (by any lane) sees it, and a write issued after a read cannot overtake it.
 #define SBZ_LDS_FENCE 1
+#endif
+#ifndef SBZ_DB_LAUNDER
+#define SBZ_DB_LAUNDER 0  // double-buffered kernel: launder the row offsets each feature
+#endif
+#ifndef SBZ_DB_GBAR
+#define SBZ_DB_GBAR 1  // double-buffered kernel: scheduling barrier every 8 gathers (VGPR bound)
 #endif
 constexpr int NS = SBZ_PIPE;
 
@@ -164,50 +172,64 @@ __device__ __forceinline__ void lds_phase() {
 // negative / NaN inputs) the wave renormalises after every factor for that feature.
 __device__ __forceinline__ bool tame(double v) { return v == 0.0 || (v >= 0x1p-60 && v <= 0x1p60); }
 
-__device__ __forceinline__ double readlane_f64(double v, int l) {
-    const uint64_t u = (uint64_t)__double_as_longlong(v);
-    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)u, l);
-    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(u >> 32), l);
-    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-}
-
-// One feature's parameters as one lane needs them.
+// One feature's parameters as one lane needs them (the weights come from MixTable::prep).
 template <int C, int FR>
 struct MixParams {
     double g;       // p_global[f][lxc]
     double z[ZR];   // p_zones[zc_i - 1][f][lxc]
     double fm[FR];  // p_fam[fm][f][lxc]
-    double w[C];    // w[f][0..C) (wave-uniform)
 };
 
-template <int C, int FR>
+// Normalised weights are computed for NWC features at a time (MixTable::prep) and kept in LDS.
+constexpr int NWC = 32;
+constexpr int NW_PER_F = 12;  // [h = hz | hf << 1][c]
+
+// Double-buffered layout (DB, lik_mixture_db_kernel): two tables of DB_TAB_BYTES each, so the
+// table of feature f+1 is built while feature f is gathered; every zone class has FR + 1 family
+// rows (rows >= Fam unused) so the build has no branches.
+constexpr int DB_TAB_BYTES = 4096;
+
+template <int C, int FR, bool DB = false>
 struct MixTable {
-    int lane, S, S1, FamC, Z, Fam, ncls, G, lx, lg, row_bytes;
+    static constexpr int RPZ_DB = (C == 3) ? FR + 1 : 1;  // rows per zone class (DB layout)
+    int lane, S, S1, FamC, RPZ, Z, Fam, ncls, G, lx, lg, row_bytes;
     uint32_t lxc;
-    int bp0;  // ds_bpermute byte address of the lane's slot-0 weights: lane 3*hz of lanes 0..11
     bool na;
     uint32_t zfs;
     unsigned char *lds;
     double *tab, *junk;
+    double *nwt;       // [NWC][NW_PER_F] normalised weights of features nwf0 .. nwf0 + NWC
+    int nwf0;          // first feature of the weights in nwt (wave-uniform)
+    uint64_t nwbad;    // bits 2k, 2k+1: feature nwf0 + k has an untamed normalised weight
+    int hz0;           // has-zone flag of the lane's slot-0 class (lg > 0)
     const double *pgb, *zbase, *fbase, *wb;
     uint32_t pzo[ZR];  // lane offset of its p_zones rows (elements)
 
-    __device__ __forceinline__ MixTable(const LikArgs &a, unsigned char *lds_, int b) : lds(lds_) {
+    __device__ __forceinline__ MixTable(const LikArgs &a, unsigned char *lds_, int b,
+                                        double *tab0 = nullptr, double *tab1 = nullptr)
+        : lds(lds_) {
         lane = threadIdx.x;
         S = a.S;
         S1 = a.S + 1;
         FamC = a.FamC;
+        RPZ = DB ? RPZ_DB : FamC;
         Z = a.Z;
         Fam = (C == 3) ? a.Fam : 0;
-        ncls = (Z + 1) * FamC;
+        ncls = (Z + 1) * RPZ;
         G = WAVE / S1;
         lx = lane % S1;
         lg = lane / S1;
-        na = lx == S;
+        na = (SBZ_ABLATE & 8) ? false : lx == S;
         lxc = (uint32_t)min(lx, S - 1);  // the NA column and idle lanes read state 0
-        bp0 = lg > 0 ? 12 : 0;
-        tab = reinterpret_cast<double *>(lds);
-        junk = tab + (ncls + 1) * S1 + lane;
+        // LDS: non-DB  [table | junk | nwt] from the dynamic base;
+        //      DB      two static tables (tab0, tab1), [junk | nwt] from the dynamic base
+        tab = DB ? tab0 : reinterpret_cast<double *>(lds);
+        double *dyn = DB ? reinterpret_cast<double *>(lds) : tab + (ncls + 1) * S1;
+        junk = dyn + lane;
+        nwt = dyn + WAVE;
+        nwf0 = -(1 << 30);
+        nwbad = 0;
+        hz0 = lg > 0 ? 1 : 0;
         row_bytes = S1 * 8;
         zfs = (uint32_t)(a.F * S);
         pgb = a.pg + (size_t)b * zfs;
@@ -217,7 +239,10 @@ struct MixTable {
 #pragma unroll
         for (int i = 0; i < ZR; i++)
             pzo[i] = (uint32_t)(max(min(lg + i * G, Z), 1) - 1) * zfs + lxc;
-        for (int x = lane; x < S1; x += WAVE) tab[ncls * S1 + x] = 1.0;  // neutral row
+        for (int x = lane; x < S1; x += WAVE) {  // neutral row (both buffers)
+            tab[ncls * S1 + x] = 1.0;
+            if (DB) tab1[ncls * S1 + x] = 1.0;
+        }
     }
 
     __device__ __forceinline__ void load(int f, MixParams<C, FR> &r) const {
@@ -228,60 +253,77 @@ struct MixTable {
 #pragma unroll
         for (int fm = 0; fm < FR; fm++)
             r.fm[fm] = fbase[(uint32_t)min(fm, max(Fam - 1, 0)) * zfs + fo + lxc];
-#pragma unroll
-        for (int c = 0; c < C; c++) r.w[c] = wb[(uint32_t)f * C + c];
     }
 
-    // Normalised weights and the table of one feature.  Returns `wide`: some input is not
-    // tame, so products over this feature must renormalise after every factor.
-    __device__ __forceinline__ bool build(const MixParams<C, FR> &r) const {
-        // 1. normalised weights (normalize_weights model.py:451-452:
-        //    w*has / ((w0*h0 + w1*h1) + w2*h2)), lane 3h + c, h = hz | hf << 1
-        const int l12 = min(lane, 11), h = l12 / 3, c = l12 - 3 * h;
-        const double hzf = (h & 1) ? 1.0 : 0.0, hff = (h & 2) ? 1.0 : 0.0;
-        const double w0 = r.w[0] * 1.0, w1 = r.w[1] * hzf;
-        double sum = w0 + w1, w2 = 0.0;
-        if (C == 3) {
-            w2 = r.w[2] * hff;
-            sum = sum + w2;
+    // normalize_weights (model.py:451-452): w*has / ((w0*h0 + w1*h1) + w2*h2) for the 4 classes
+    // h = hz | hf << 1 of features f0 .. f0 + NWC (clamped to fb - 1), into nwt.  Lane 2k + hp
+    // computes feature k's h = 2hp and 2hp + 1 (one division per weight, as the reference).
+    // Runs once per NWC features instead of once per feature.
+    __device__ __forceinline__ void prep(int f0, int fb) {
+        const int k = lane >> 1, hp = lane & 1;
+        const uint32_t f = (uint32_t)min(f0 + k, fb - 1);
+        const double w0r = wb[f * C], w1r = wb[f * C + 1], w2r = C == 3 ? wb[f * C + 2] : 0.0;
+        int ok = 1;
+        double n[2][3];
+#pragma unroll
+        for (int hz = 0; hz < 2; hz++) {
+            const double hzf = hz ? 1.0 : 0.0, hff = hp ? 1.0 : 0.0;
+            const double w0 = w0r * 1.0, w1 = w1r * hzf;
+            double sum = w0 + w1, w2 = 0.0;
+            if (C == 3) {
+                w2 = w2r * hff;
+                sum = sum + w2;
+            }
+            n[hz][0] = w0 / sum;
+            n[hz][1] = w1 / sum;
+            n[hz][2] = C == 3 ? w2 / sum : 0.0;
+            ok &= (int)tame(n[hz][0]) & (int)tame(n[hz][1]) & (int)tame(n[hz][2]);
         }
-        const double wc = c == 0 ? w0 : (c == 1 ? w1 : w2);
-        const double n = (C == 2 && c == 2) ? 0.0 : wc / sum;
-        int ok = (int)tame(n) & (int)tame(r.g);
+        lds_phase();  // earlier features' reads of nwt are done
+        double *o = nwt + k * NW_PER_F + 6 * hp;  // h = 2hp + hz -> offset 3h
+#pragma unroll
+        for (int hz = 0; hz < 2; hz++)
+#pragma unroll
+            for (int c = 0; c < 3; c++) o[3 * hz + c] = n[hz][c];
+        nwbad = __ballot(!ok);
+        nwf0 = f0;
+        lds_phase();
+    }
+
+    // The table of feature f (its weights in nwt: nwf0 <= f < nwf0 + NWC).  Returns `wide`:
+    // some input is not tame, so products over this feature must renormalise after every factor.
+    __device__ __forceinline__ bool build(const MixParams<C, FR> &r, int f, double *dbtab = nullptr) const {
+        const int k = f - nwf0;
+        int ok = (int)tame(r.g);
 #pragma unroll
         for (int i = 0; i < ZR; i++) ok &= (int)tame(r.z[i]);
 #pragma unroll
         for (int fm = 0; fm < FR; fm++) ok &= (int)tame(r.fm[fm]);
-        const bool wide = __ballot(!ok) != 0;
-        // Slot i >= 1 holds zone classes only (zc >= G >= 1): wave-uniform weights of h = 1 (no
-        // family) and h = 3 (family), read into SGPRs.  Slot 0 mixes zc = 0 (lanes lg == 0) and
-        // zone classes: each lane fetches its h = hz and h = hz | 2 weights with ds_bpermute.
-        double u[2][3];
-#pragma unroll
-        for (int cc = 0; cc < 3; cc++) {
-            u[0][cc] = (C == 2 && cc == 2) ? 0.0 : readlane_f64(n, 3 + cc);
-            u[1][cc] = (C == 2 && cc == 2) ? 0.0 : readlane_f64(n, 9 + cc);
-        }
-        double p[2][3];
+#if SBZ_ABLATE & 4
+        ok = 1;  // diagnostic build: no tame checks
+#endif
+        const bool wide = ((nwbad >> (2 * k)) & 3ull) != 0 || __ballot(!ok) != 0;
+        // 1. normalised weights from nwt.  Slot i >= 1 holds zone classes only (zc >= G >= 1):
+        //    wave-uniform weights of h = 1 (no family) and h = 3 (family).  Slot 0 mixes zc = 0
+        //    (lanes lg == 0, h = 0 / 2) and zone classes (h = 1 / 3).
+        const double *nk = nwt + k * NW_PER_F;
+        double u[2][3], p[2][3];
 #pragma unroll
         for (int hf = 0; hf < 2; hf++)
 #pragma unroll
             for (int cc = 0; cc < 3; cc++) {
-                if (C == 2 && (hf == 1 || cc == 2)) {
-                    p[hf][cc] = 0.0;
-                    continue;
-                }
-                const uint64_t bits = (uint64_t)__double_as_longlong(n);
-                const int a = bp0 + 4 * (6 * hf + cc);
-                const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)(uint32_t)bits);
-                const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)(uint32_t)(bits >> 32));
-                p[hf][cc] = __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+                const bool used = !(C == 2 && (hf == 1 || cc == 2));
+                u[hf][cc] = used ? nk[3 * (1 + 2 * hf) + cc] : 0.0;
+                p[hf][cc] = used ? nk[3 * (hz0 + 2 * hf) + cc] : 0.0;
             }
         // 2. table: the reference cell (n0*l0 + n1*l1) + n2*l2 for every class.  Branch-free:
         //    lanes without an entry write to their junk slot.  The family term of a class
         //    without family is n2 * l2 = (w2 * 0 / sum) * (0 or 1): +0 for tame inputs, left
         //    out then (x + 0 == x); kept for untamed ones, where it may be NaN.
-        lds_phase();
+        // DB: no fences — a wave's LDS operations complete in issue order, and the buffer being
+        // written was last read by the gathers of feature f - 1, issued earlier.
+        if (!DB) lds_phase();
+        double *const tb = DB ? dbtab : tab;
         const double l0 = na ? 1.0 : r.g;
 #pragma unroll
         for (int i = 0; i < ZR; i++) {
@@ -293,10 +335,15 @@ struct MixTable {
             const double n00 = i == 0 ? p[0][0] : u[0][0], n01 = i == 0 ? p[0][1] : u[0][1];
             // zone lh: 0 for a site outside every zone (model.py:241-247), 1 for NA
             const double l1 = na ? 1.0 : ((i > 0 || zc > 0) ? r.z[i] : 0.0);
-            double *row = valid ? tab + (zc * FamC) * S1 + lx : junk;
+            double *row = valid ? tb + (zc * RPZ) * S1 + lx : junk;
             const int rs = valid ? S1 : 0;
             double v = n00 * l0 + n01 * l1;
-            if (C == 3 && wide) v = v + (i == 0 ? p[0][2] : u[0][2]) * (na ? 1.0 : 0.0);
+            if (C == 3 && DB) {
+                // the reference's third term, l2 = 0 (no family) or 1 (NA): +0 for tame inputs
+                v = v + (i == 0 ? p[0][2] : u[0][2]) * (na ? 1.0 : 0.0);
+            } else if (C == 3 && wide) {
+                v = v + (i == 0 ? p[0][2] : u[0][2]) * (na ? 1.0 : 0.0);
+            }
             row[0] = v;
             if (C == 3) {
                 const double n10 = i == 0 ? p[1][0] : u[1][0], n11 = i == 0 ? p[1][1] : u[1][1];
@@ -304,10 +351,10 @@ struct MixTable {
                 const double a1 = n10 * l0 + n11 * l1;
 #pragma unroll
                 for (int fm = 0; fm < FR; fm++)
-                    if (fm < Fam) row[(fm + 1) * rs] = a1 + n12 * (na ? 1.0 : r.fm[fm]);
+                    if (DB || fm < Fam) row[(fm + 1) * rs] = a1 + n12 * (na ? 1.0 : r.fm[fm]);
             }
         }
-        lds_phase();
+        if (!DB) lds_phase();
         return wide;
     }
 
@@ -328,7 +375,7 @@ __global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArg
     const int b = blockIdx.y;
     const int fa = blockIdx.x * a.fpw;
     const int fb = min(a.F, fa + a.fpw);
-    const MixTable<C, FR> t(a, lds, b);
+    MixTable<C, FR> t(a, lds, b);
 
     auto load_obs = [&](int f, int c0, uint32_t (&o)[NO]) {
         const uint32_t *op = reinterpret_cast<const uint32_t *>(a.obs_fm + (size_t)f * a.Np + c0);
@@ -346,7 +393,9 @@ __global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArg
     // `fill` (the sets feature f - 1 used), gather.  `live` = false for padding features.
     auto feature = [&](int f, int c0, bool live, const MixParams<C, FR> &cur, const uint32_t (&ob)[NO],
                        MixParams<C, FR> &fill, uint32_t (&ofill)[NO]) {
-        const bool wide = t.build(cur);
+        const int fk = min(f, fb - 1);
+        if (fk < t.nwf0 || fk >= t.nwf0 + NWC) t.prep(fk, fb);  // uniform, once per NWC features
+        const bool wide = t.build(cur, fk);
         __builtin_amdgcn_sched_barrier(0);
         t.load(min(f + NS - 1, fb - 1), fill);
         load_obs(min(f + NS - 1, fb - 1), c0, ofill);
@@ -431,6 +480,155 @@ __global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArg
 }
 
 // ---------------------------------------------------------------------------------------
+// Dense mixture kernel, double-buffered (opt-in, SBZ_LIK_KERNEL=db; needs the table to fit
+// DB_TAB_BYTES).  Measured at cfg5: 99 us per launch vs 95 us for lik_mixture_kernel — without
+// the LDS fences and with one parameter set, but at 168 VGPRs, and with the build after the
+// gathers (letting the compiler interleave them spilled), so it is not the default.
+// Step f gathers feature f from one table buffer, then builds feature f + 1's table into the
+// other with no LDS fence between them (distinct static LDS arrays; the buffer address folds
+// into the ds_read offset).  One parameter register set: feature f + 2's parameters load right
+// after build(f + 1) consumed f + 1's.
+// ---------------------------------------------------------------------------------------
+template <int C, int SPL, int FR>
+__global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_db_kernel(LikArgs a) {
+    __shared__ __attribute__((aligned(16))) double tab0[DB_TAB_BYTES / 8];
+    __shared__ __attribute__((aligned(16))) double tab1[DB_TAB_BYTES / 8];
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    constexpr int NO = SPL / 4;  // observation words (4 sites each) per lane per feature
+    const int lane = threadIdx.x;
+    const int b = blockIdx.y;
+    const int fa = blockIdx.x * a.fpw;
+    const int fb = min(a.F, fa + a.fpw);
+    MixTable<C, FR, true> t(a, lds, b, tab0, tab1);
+
+    auto load_obs = [&](int f, int c0, uint32_t (&o)[NO]) {
+        const uint32_t *op = reinterpret_cast<const uint32_t *>(a.obs_fm + (size_t)f * a.Np + c0);
+#pragma unroll
+        for (int k = 0; k < NO; k++) o[k] = op[(uint32_t)(lane + 64 * k)];
+    };
+
+    double m[4] = {1.0, 1.0, 1.0, 1.0};  // four independent product chains
+    int e = 0;
+    uint32_t base2[SPL / 2];  // per-site class row offsets (bytes, < DB_TAB_BYTES), two per register
+    MixParams<C, FR> P;       // parameters of the next table to build
+    uint32_t O[2][NO];        // observations of the feature being gathered / the next one
+
+    auto cell = [&](auto jc, uint32_t off) -> double {
+        constexpr int J = decltype(jc)::value;
+        const unsigned char *tb = reinterpret_cast<const unsigned char *>(J ? tab1 : tab0);
+        return *reinterpret_cast<const double *>(tb + off);
+    };
+    auto gather = [&](auto jc, const uint32_t (&ob)[NO], bool wide) {
+        if (SBZ_ABLATE & 1) return;
+        if (!wide) {
+            // launder the packed row offsets: otherwise LICM hoists each word's low half out of
+            // the feature loop and keeps 16 more VGPRs live (the SDWA add selects the half)
+            // Compiler memory barriers pin the reads here in groups of 8: LDS reads cannot fault
+            // and the static tables alias nothing else, so they would otherwise be speculated
+            // above earlier branches and all 32 results kept live.
+            asm volatile("" ::: "memory");
+#if SBZ_DB_LAUNDER
+#pragma unroll
+            for (int i = 0; i < SPL / 2; i++) asm volatile("" : "+v"(base2[i]));
+#endif
+#pragma unroll
+            for (int k = 0; k < NO; k++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const uint32_t bw = base2[2 * k + (j >> 1)];
+                    const uint32_t bs = (j & 1) ? (bw >> 16) : (bw & 0xffffu);
+                    m[k & 3] *= cell(jc, bs + ((ob[k] >> (8 * j)) & 0xffu));
+#if SBZ_DB_GBAR
+                    // <= 8 reads in flight: the group's products are inputs of the barrier, so
+                    // its multiplies complete before the next group's reads are issued
+                    if (j == 3 && (k & 1))
+                        asm volatile("" : "+v"(m[0]), "+v"(m[1]), "+v"(m[2]), "+v"(m[3])::"memory");
+#endif
+                }
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                if (q < NO) renorm(m[q], e);
+        } else {
+            // untamed inputs: renormalise after every factor (exact for any normal double).
+            // The base words pass through an empty asm so the compiler cannot treat this path's
+            // addresses as common with the fast path's and hoist all 32 above the branch.
+#pragma unroll
+            for (int k = 0; k < NO; k++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    uint32_t bw = base2[2 * k + (j >> 1)];
+                    asm volatile("" : "+v"(bw));
+                    const uint32_t bs = (j & 1) ? (bw >> 16) : (bw & 0xffffu);
+                    m[0] *= cell(jc, bs + ((ob[k] >> (8 * j)) & 0xffu));
+                    renorm(m[0], e);
+                }
+        }
+    };
+
+    for (int c0 = 0; c0 < a.Np; c0 += SPL * WAVE) {
+        // classes of this chunk's sites (cls = zc*RPZ + fc, padding -> the neutral row)
+        {
+            const uint8_t *zb = a.zone + (size_t)b * a.N;
+            uint32_t zs[SPL];
+            int4 pv[NO];
+            uint32_t fw[NO];
+#pragma unroll
+            for (int k = 0; k < NO; k++) {
+                const uint32_t p0 = (uint32_t)(c0 + 4 * lane + 256 * k);  // < Np (arrays padded)
+                pv[k] = *reinterpret_cast<const int4 *>(a.perm + p0);
+                fw[k] = *reinterpret_cast<const uint32_t *>(a.famc + p0);
+            }
+#pragma unroll
+            for (int k = 0; k < NO; k++) {
+                zs[4 * k + 0] = zb[(uint32_t)pv[k].x];
+                zs[4 * k + 1] = zb[(uint32_t)pv[k].y];
+                zs[4 * k + 2] = zb[(uint32_t)pv[k].z];
+                zs[4 * k + 3] = zb[(uint32_t)pv[k].w];
+            }
+#pragma unroll
+            for (int i = 0; i < SPL; i++) {
+                const int pos = c0 + 4 * lane + 256 * (i / 4) + (i % 4);
+                const int z = (int)zs[i];
+                const int fc = (int)((fw[i / 4] >> (8 * (i % 4))) & 0xffu);
+                const int cls = pos < a.N ? ((z < t.Z ? z + 1 : 0) * t.RPZ + fc) : t.ncls;
+                const uint32_t off = (uint32_t)(cls * t.row_bytes);
+                if (i & 1) base2[i >> 1] |= off << 16;
+                else base2[i >> 1] = off;
+            }
+        }
+        // prologue: feature fa's table into buffer 0, feature fa + 1's parameters
+        __builtin_amdgcn_sched_barrier(0);
+        t.load(fa, P);
+        load_obs(fa, c0, O[0]);
+        if (fa < t.nwf0 || fa >= t.nwf0 + NWC) t.prep(fa, fb);
+        bool wide = t.build(P, fa, tab0);
+        t.load(min(fa + 1, fb - 1), P);
+
+        // step J: gather feature f from buffer J; build feature f + 1 into buffer 1 - J
+        auto step = [&](auto jc, int f) {
+            constexpr int J = decltype(jc)::value;
+            const int fn = min(f + 1, fb - 1);
+            if (fn < t.nwf0 || fn >= t.nwf0 + NWC) t.prep(fn, fb);  // uniform, once per NWC
+            gather(jc, O[J], wide);
+            const bool wn = t.build(P, fn, J ? tab0 : tab1);
+            t.load(min(f + 2, fb - 1), P);
+            load_obs(fn, c0, O[1 - J]);
+            wide = wn;
+        };
+        int f = fa;
+        for (; f + 1 < fb; f += 2) {
+            step(std::integral_constant<int, 0>(), f);
+            step(std::integral_constant<int, 1>(), f + 1);
+        }
+        if (f < fb) gather(std::integral_constant<int, 0>(), O[0], wide);  // odd tail
+    }
+    double v = (log(m[0]) + log(m[1])) + (log(m[2]) + log(m[3]));
+    v = v + (double)e * LN2;
+    const double tot = wave_sum(v);
+    finish_chain(a, b, tot);
+}
+
+// ---------------------------------------------------------------------------------------
 // Zone-sparse mixture kernel.  A site outside every zone has class (0, fc), so over those
 // sites   sum log T0[fc][x] = sum_{fc,x} n_out[fc][x] * log T0[fc][x].
 // With n_all[f][fc][x] (all sites, counted once when the context opens) and the chain's list
@@ -454,7 +652,7 @@ __global__ __launch_bounds__(WAVE, SBZ_ZS_WAVES) void lik_zoned_kernel(LikArgs a
     const int b = blockIdx.y;
     const int fa = blockIdx.x * a.fpw;
     const int fb = min(a.F, fa + a.fpw);
-    const MixTable<C, FR> t(a, lds, b);
+    MixTable<C, FR> t(a, lds, b);
     const int NC = t.FamC * t.S1;
     const int nz = a.nzs[b];
     const uint32_t *zlb = a.zl + (size_t)b * a.N;
@@ -495,7 +693,9 @@ __global__ __launch_bounds__(WAVE, SBZ_ZS_WAVES) void lik_zoned_kernel(LikArgs a
     auto feature = [&](int f, bool live, bool first, int zb0, const MixParams<C, FR> &cur,
                        const uint32_t (&ob)[ZSPL], const int (&cc)[2], MixParams<C, FR> &fill,
                        uint32_t (&ofill)[ZSPL], int (&cfill)[2]) {
-        const bool wide = t.build(cur);
+        const int fk = min(f, fb - 1);
+        if (fk < t.nwf0 || fk >= t.nwf0 + NWC) t.prep(fk, fb);
+        const bool wide = t.build(cur, fk);
         __builtin_amdgcn_sched_barrier(0);
         t.load(min(f + NS - 1, fb - 1), fill);
         load_zobs(min(f + NS - 1, fb - 1), ofill);
@@ -806,6 +1006,21 @@ __global__ void repack_source_kernel(int B, int N, int F, int Np, const int *per
 }
 
 // The mixture table kernel for these template choices (dense or zone-sparse).
+template <int C, int FR>
+const void *mix_db_kernel_x(int spl) {
+    switch (spl) {
+        case 4: return reinterpret_cast<const void *>(&lik_mixture_db_kernel<C, 4, FR>);
+        case 8: return reinterpret_cast<const void *>(&lik_mixture_db_kernel<C, 8, FR>);
+        case 16: return reinterpret_cast<const void *>(&lik_mixture_db_kernel<C, 16, FR>);
+        default: return reinterpret_cast<const void *>(&lik_mixture_db_kernel<C, 32, FR>);
+    }
+}
+
+const void *mix_db_kernel(int C, int fr, int spl) {
+    if (C == 3) return fr == 4 ? mix_db_kernel_x<3, 4>(spl) : mix_db_kernel_x<3, 8>(spl);
+    return mix_db_kernel_x<2, 4>(spl);
+}
+
 template <int C, int FR, bool XS8>
 const void *mix_kernel_x(bool zoned, int spl, int zspl) {
     if (zoned) {
@@ -850,6 +1065,12 @@ void configure_mix_x(std::vector<const void *> &v) {
     v.push_back(reinterpret_cast<const void *>(&lik_mixture_kernel<C, 8, FR, XS8>));
     v.push_back(reinterpret_cast<const void *>(&lik_mixture_kernel<C, 16, FR, XS8>));
     v.push_back(reinterpret_cast<const void *>(&lik_mixture_kernel<C, 32, FR, XS8>));
+    if (XS8) {
+        v.push_back(reinterpret_cast<const void *>(&lik_mixture_db_kernel<C, 4, FR>));
+        v.push_back(reinterpret_cast<const void *>(&lik_mixture_db_kernel<C, 8, FR>));
+        v.push_back(reinterpret_cast<const void *>(&lik_mixture_db_kernel<C, 16, FR>));
+        v.push_back(reinterpret_cast<const void *>(&lik_mixture_db_kernel<C, 32, FR>));
+    }
 }
 
 template <int C>
@@ -874,16 +1095,20 @@ void configure_source(std::vector<const void *> &v) {
 // generic per-cell path (fr == 0).
 struct MixPlan {
     int fr = 0;
+    bool db = false;  // the double-buffered kernel applies (obs as x*8, table <= DB_TAB_BYTES)
 };
 
 size_t mix_lds_bytes(const sbz_dims &d, int C) {
     const size_t S1 = (size_t)d.n_states + 1;
     const size_t Fam = C == 3 ? (size_t)d.n_families : 0;
     const size_t ncls = (size_t)(d.n_zones + 1) * (Fam + 1);
-    return ((ncls + 1) * S1 + WAVE) * 8;
+    return ((ncls + 1) * S1 + WAVE + (size_t)NWC * NW_PER_F) * 8;
 }
 
-MixPlan plan_mixture(const sbz_dims &d, int C) {
+// dynamic LDS of lik_mixture_db_kernel (the two tables are static): junk + nwt
+size_t mix_db_lds_bytes() { return ((size_t)WAVE + (size_t)NWC * NW_PER_F) * 8; }
+
+MixPlan plan_mixture(const sbz_dims &d, int C, bool xs8 = false) {
     MixPlan p;
     const int S1 = d.n_states + 1;
     const int Fam = C == 3 ? d.n_families : 0;
@@ -894,6 +1119,11 @@ MixPlan plan_mixture(const sbz_dims &d, int C) {
     if (mix_lds_bytes(d, C) > 64 * 1024) return p;       // row offsets are 16-bit
     if (C == 2 || Fam <= 4) p.fr = 4;
     else if (Fam <= 8) p.fr = 8;
+    if (p.fr) {
+        const int rpz = C == 3 ? p.fr + 1 : 1;
+        const size_t tab = ((size_t)(d.n_zones + 1) * rpz + 1) * S1 * 8;
+        p.db = xs8 && tab <= (size_t)DB_TAB_BYTES;
+    }
     return p;
 }
 
@@ -970,9 +1200,12 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
     size_t lds = 0;
     int rc;
     if (!src_mode) {
-        plan = plan_mixture(d, ctx->C);
+        plan = plan_mixture(d, ctx->C, ctx->xs8 != 0);
         if (plan.fr) {
             zoned = ctx->d_cnt != nullptr && ctx->lik_kernel == 2;
+            // (the <C=3, SPL=32, FR=8> instantiation of the double-buffered kernel spills)
+            const bool db = plan.db && !zoned && ctx->lik_kernel == 3 &&
+                            !(ctx->C == 3 && plan.fr == 8 && ctx->spl == 32);
             if (zoned) {
                 rc = ensure(ctx, ctx->zl, (size_t)B * d.n_sites * sizeof(uint32_t));
                 if (rc) return rc;
@@ -985,8 +1218,9 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
                 a.nzs = static_cast<const int *>(ctx->nzs.ptr);
                 a.cnt = ctx->d_cnt;
             }
-            lds = mix_lds_bytes(d, ctx->C);
-            mix_fn = mix_kernel(ctx->C, plan.fr, ctx->xs8 != 0, zoned, ctx->spl, ctx->zspl);
+            lds = db ? mix_db_lds_bytes() : mix_lds_bytes(d, ctx->C);
+            mix_fn = db ? mix_db_kernel(ctx->C, plan.fr, ctx->spl)
+                        : mix_kernel(ctx->C, plan.fr, ctx->xs8 != 0, zoned, ctx->spl, ctx->zspl);
             // Long tasks: one resident round of single-wave tasks (occupancy x CUs) over the
             // launch, so every wave streams its features with no tail of late tasks.
             if (ctx->mix_occ == 0) {

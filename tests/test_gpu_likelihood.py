@@ -34,9 +34,10 @@ def _assert_close(got, ref, tol=REL_TOL):
     return 0.0 if rel.size == 0 else float(rel.max())
 
 
-# Mixture-mode kernels: "dense" = every site gathered from the table (default), "zoned" =
-# zone-sparse counts kernel (SBZ_LIK_KERNEL is read when a context opens).
-MODES = [("mixture", "dense"), ("mixture", "zoned"), ("source", "dense")]
+# Mixture-mode kernels: "dense" = every site gathered from the table (default), "db" = the
+# double-buffered dense kernel (where the table fits 4 KiB), "zoned" = zone-sparse counts kernel
+# (SBZ_LIK_KERNEL is read when a context opens).
+MODES = [("mixture", "dense"), ("mixture", "db"), ("mixture", "zoned"), ("source", "dense")]
 
 
 @pytest.fixture
