@@ -47,7 +47,8 @@ class sbz_chains(ctypes.Structure):
                 ("counter", ctypes.c_void_p), ("accepted", ctypes.c_void_p),
                 ("proposed", ctypes.c_void_p), ("status", ctypes.c_void_p),
                 ("trace_op", ctypes.c_void_p), ("trace_accept", ctypes.c_void_p),
-                ("trace_ll", ctypes.c_void_p), ("trace_zos", ctypes.c_void_p)]
+                ("trace_ll", ctypes.c_void_p), ("trace_zos", ctypes.c_void_p),
+                ("prior", ctypes.c_void_p)]
 
 
 # name -> (restype, argtypes); every symbol declared in include/sbz.h
@@ -69,6 +70,7 @@ SIGNATURES = {
     "sbz_memcpy_d2h": (_I, [_P, _P, _P, ctypes.c_uint64]),
     "sbz_lik_lds_bytes": (ctypes.c_uint64, [ctypes.POINTER(sbz_dims), _I]),
     "sbz_set_network": (_I, [_P, _P, ctypes.c_int32, _P, _P]),
+    "sbz_set_priors": (_I, [_P, _P, _P, ctypes.c_int32]),
     "sbz_mh_run_device": (_I, [_P, _I, _I, ctypes.POINTER(sbz_mh_config), ctypes.POINTER(sbz_chains)]),
     "sbz_mh_lds_bytes": (ctypes.c_uint64, [ctypes.POINTER(sbz_dims)]),
 }

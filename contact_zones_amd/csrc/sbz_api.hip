@@ -1,6 +1,7 @@
 // sbz_api.hip — C-ABI entry points of include/sbz.h (context, memory, likelihood).
 #include <algorithm>
 #include <cstdlib>
+#include <cmath>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -219,7 +220,8 @@ void sbz_close(sbz_ctx *ctx) {
     if (ctx->d_famc) (void)hipFree(ctx->d_famc);
     if (ctx->d_perm) (void)hipFree(ctx->d_perm);
     for (void *p : {(void *)ctx->d_obs_sm, (void *)ctx->d_fam_site, (void *)ctx->d_adj_ptr,
-                    (void *)ctx->d_adj_idx, (void *)ctx->d_app_list, (void *)ctx->d_app_cnt})
+                    (void *)ctx->d_adj_idx, (void *)ctx->d_app_list, (void *)ctx->d_app_cnt,
+                    (void *)ctx->d_alpha_g, (void *)ctx->d_alpha_f})
         if (p) (void)hipFree(p);
     if (ctx->d_cnt) (void)hipFree(ctx->d_cnt);
     free_buf(ctx->zl);
@@ -349,6 +351,34 @@ int sbz_set_network(sbz_ctx *ctx, const uint8_t *applicable, int32_t nnz, const 
     if (e == hipSuccess) e = hipMemcpy(ctx->d_app_list, list.data(), list.size() * 4, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(ctx->d_app_cnt, cnt.data(), cnt.size() * 4, hipMemcpyHostToDevice);
     return e == hipSuccess ? SBZ_OK : hip_fail(ctx, e, "network upload");
+}
+
+int sbz_set_priors(sbz_ctx *ctx, const double *alpha_global, const double *alpha_fam,
+                   int32_t size_prior) {
+    if (!ctx) return SBZ_EINVAL;
+    if (size_prior < 0 || size_prior > 2) return fail(ctx, SBZ_EINVAL, "size_prior must be 0, 1 or 2");
+    if (alpha_fam && (ctx->C != 3 || ctx->d.n_families == 0))
+        return fail(ctx, SBZ_EINVAL, "alpha_fam needs inheritance with families");
+    const size_t fs = (size_t)ctx->d.n_features * ctx->d.n_states;
+    (void)hipSetDevice(ctx->device);
+    for (double **pp : {&ctx->d_alpha_g, &ctx->d_alpha_f}) {
+        if (*pp) (void)hipFree(*pp);
+        *pp = nullptr;
+    }
+    auto upload = [&](const double *src, size_t n, double **dst) -> int {
+        if (!src) return SBZ_OK;
+        for (size_t i = 0; i < n; i++)
+            if (!(src[i] >= 0.0) || std::isinf(src[i]))
+                return fail(ctx, SBZ_EINVAL, "prior concentrations must be finite and >= 0");
+        if (hipMalloc(dst, n * sizeof(double)) != hipSuccess)
+            return fail(ctx, SBZ_ENOMEM, "prior allocation failed");
+        hipError_t e = hipMemcpy(*dst, src, n * sizeof(double), hipMemcpyHostToDevice);
+        return e == hipSuccess ? SBZ_OK : hip_fail(ctx, e, "prior upload");
+    };
+    int rc = upload(alpha_global, fs, &ctx->d_alpha_g);
+    if (rc == SBZ_OK) rc = upload(alpha_fam, (size_t)ctx->d.n_families * fs, &ctx->d_alpha_f);
+    if (rc == SBZ_OK) ctx->size_prior = size_prior;
+    return rc;
 }
 
 int sbz_mh_run_device(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg,

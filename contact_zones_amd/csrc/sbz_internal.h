@@ -60,6 +60,9 @@ struct sbz_ctx {
     int *d_adj_ptr = nullptr, *d_adj_idx = nullptr;  // CSR network
     int adj_nnz = 0;
     int *d_app_list = nullptr, *d_app_cnt = nullptr; // [F][S] applicable states, [F] counts
+    double *d_alpha_g = nullptr;  // [F][S] 'counts' prior on p_global (sbz_set_priors) or null
+    double *d_alpha_f = nullptr;  // [Fam][F][S] 'counts' prior on p_families or null
+    int size_prior = 0;           // 0 none, 1 uniform, 2 quadratic
     int zspl = 8;          // zoned sites per lane and chunk of the zone-sparse kernel
     int lik_kernel = 1;    // SBZ_LIK_KERNEL: 1 dense (default), 2 zone-sparse ("zoned"),
                            // 3 dense double-buffered ("db", where the table fits 4 KiB)

@@ -2,8 +2,8 @@
 //
 // One wave (64 lanes) runs one chain for n_steps without leaving the kernel:
 // MCMCGenerative.step (sbayes/sampling/mcmc_generative.py:282-351) with the operators of
-// ZoneMCMC / ZoneMCMCWarmup (sbayes/sampling/zone_sampling.py) for SAMPLE_SOURCE = false and
-// uniform priors (log prior 0; model.py:596-623, 930-960, 1020-1035):
+// ZoneMCMC / ZoneMCMCWarmup (sbayes/sampling/zone_sampling.py) for SAMPLE_SOURCE = false; priors
+// zero, 'counts' on p_global / p_families and 'uniform' / 'quadratic' zone size (sbz_set_priors):
 //   shrink_zone :866-933 (warm-up :1498-1574)   grow_zone :788-864 (:1418-1496)
 //   swap_zone :704-786 (:1328-1416)             alter_weights :408-452
 //   alter_p_global :454-493   alter_p_zones :495-535   alter_p_families :571-612
@@ -178,7 +178,8 @@ struct Rng {
     __device__ double normal() {  // Box-Muller (Philox mode only)
         const double u1 = 1.0 - uniform53();  // (0, 1]
         const double u2 = uniform53();
-        return sqrt(-2.0 * log(u1)) * cos(6.283185307179586476925286766559 * u2);
+        // cos(2 pi u2) as cospi(2 u2): no large-argument reduction (u2 in [0, 1))
+        return sqrt(-2.0 * log(u1)) * cospi(2.0 * u2);
     }
     // Marsaglia-Tsang, alpha >= 1.  Each round accepts with probability > 0.95 (alpha >= 1);
     // the loop is bounded at 64 rounds (probability of reaching it < 1e-80).
@@ -234,6 +235,22 @@ __device__ __forceinline__ void dirichlet_proposal2(Rng &rng, double w0, double 
     log_q_back = uni(log(qb));
 }
 
+// scipy.special.xlogy(a, x): 0 where a == 0, else a * log(x)
+__device__ __forceinline__ double xlogy(double a, double x) { return a == 0.0 ? 0.0 : a * log(x); }
+
+// Change of the zone-size prior (ZoneSizePrior, model.py:932-971) when one zone goes from size
+// s to s1 = s +- 1: 'uniform' is -sum log C(N, size) (log_binom, util.py:1202-1217), and
+// C(N, k+1) / C(N, k) = (N-k) / (k+1), so the change is one log of that ratio; 'quadratic' is
+// -sum log(size^2).
+__device__ __forceinline__ double size_prior_delta(int kind, int N, int s, int s1) {
+    if (kind == 1) {
+        return s1 > s ? -log((double)(N - s) / (double)(s + 1))   // grow
+                      : -log((double)s / (double)(N - s + 1));    // shrink
+    }
+    if (kind == 2) return log((double)s * (double)s) - log((double)s1 * (double)s1);
+    return 0.0;
+}
+
 // The reference cell for one (site, feature): normalize_weights (model.py:436-452) then
 // (n0*l0 + n1*l1) + n2*l2 with NA -> every lh 1 and absent components -> lh 0.
 template <int C>
@@ -278,6 +295,9 @@ struct MhArgs {
     int nnz;
     const int *app_list;        // [F][S] applicable states of each feature (ascending)
     const int *app_cnt;         // [F]
+    const double *alpha_g;      // [F][S] 'counts' prior on p_global, or null (sbz_set_priors)
+    const double *alpha_f;      // [Fam][F][S] 'counts' prior on p_families, or null
+    int size_prior;             // 0 none, 1 uniform, 2 quadratic
     sbz_chains ch;
 };
 
@@ -336,6 +356,7 @@ __global__ __launch_bounds__(WAVE) void mh_kernel(MhArgs a) {
     rng.bad = 0;
 
     double ll = ch.ll[b];
+    double prior = ch.prior ? ch.prior[b] : 0.0;  // carried log prior (sbz_set_priors)
     int err = 0;             // first range-check failure (MH_IDX)
     long long err_val = 0;
     const long long nFS = (long long)F * S, nZFS = (long long)Z * F * S, nFamFS = (long long)Fam * F * S;
@@ -506,10 +527,12 @@ __global__ __launch_bounds__(WAVE) void mh_kernel(MhArgs a) {
             break;
         }
         double log_q = 0.0, log_q_back = -INFINITY;
+        double dprior = 0.0;  // prior_new - prior_prev of the proposal
         // zone move: site sa goes zoa -> zna, site sb (swap) zob -> znb
         int sa = -1, zoa = NONE, zna = NONE, sb = -1;
         // parameter move
         int comp = -1, row = 0, f = 0, ia = 0, ib = 0;
+        long long poff = 0;  // offset of the altered row (parameters and prior concentrations)
         double prec = 0.0;
         double *base = nullptr;
         const int n_free = N - occupied;
@@ -549,6 +572,7 @@ __global__ __launch_bounds__(WAVE) void mh_kernel(MhArgs a) {
                         }
                         log_q = uni(log(q));
                         log_q_back = uni(log(q_back));
+                        if (op == GROW) dprior = uni(size_prior_delta(a.size_prior, N, size, size + 1));
                         sa = site;
                         zoa = NONE;
                         zna = z;
@@ -574,6 +598,7 @@ __global__ __launch_bounds__(WAVE) void mh_kernel(MhArgs a) {
                 wsync();
                 log_q = uni(log(1.0 / (double)size));
                 log_q_back = uni(log(q_back));
+                dprior = uni(size_prior_delta(a.size_prior, N, size, size - 1));
                 sa = site;
                 zoa = z;
                 zna = NONE;
@@ -612,6 +637,7 @@ __global__ __launch_bounds__(WAVE) void mh_kernel(MhArgs a) {
                 break;
             }
             base = arr + off;
+            poff = off;
         }
 
         // ---- 2. Dirichlet proposal of the pair (zone_sampling.py:421-438, :537-569)
@@ -626,6 +652,16 @@ __global__ __launch_bounds__(WAVE) void mh_kernel(MhArgs a) {
             dirichlet_proposal2(rng, t0, t1, prec, u0, u1, log_q, log_q_back);
             nv0 = raw ? u0 : u0 * sum;
             nv1 = raw ? u1 : u1 * sum;
+            // 'counts' priors: dirichlet_logpdf(p[f, states], alpha) changes only in the two
+            // altered states' xlogy(alpha - 1, p) terms (prior_p_global_dirichlet
+            // model.py:1142-1170, prior_p_families_dirichlet :1173-1219)
+            if ((comp == 0 && a.alpha_g) || (C == 3 && comp == 2 && a.alpha_f)) {
+                // the concentrations sit at the same offset as the altered pair (off + ia / ib)
+                const double *al = comp == 0 ? a.alpha_g : a.alpha_f;
+                const double a0 = uni(al[poff + ia]) - 1.0;
+                const double a1 = uni(al[poff + ib]) - 1.0;
+                dprior = uni((xlogy(a0, nv0) - xlogy(a0, c0)) + (xlogy(a1, nv1) - xlogy(a1, c1)));
+            }
         }
 
         // ---- 3. delta log-likelihood
@@ -649,13 +685,14 @@ __global__ __launch_bounds__(WAVE) void mh_kernel(MhArgs a) {
         } else if (log_q == -INFINITY) {
             accept = true;
         } else {
-            const double mh = (delta * 1.0) - (log_q - log_q_back) + 0.0;
+            const double mh = (delta * 1.0) - (log_q - log_q_back) + dprior;
             accept = log(rng.real()) < mh;
         }
         if (lane == 0) stat[op]++;
         if (accept) {
             if (lane == 0) stat[8 + op]++;
             ll = ll + delta;
+            prior = prior + dprior;
             wsync();
             if (sa >= 0) {
                 if (lane == 0) {
@@ -690,6 +727,7 @@ __global__ __launch_bounds__(WAVE) void mh_kernel(MhArgs a) {
     for (int s = lane; s < N; s += WAVE) gzos[s] = zos[s];
     if (lane == 0) {
         ch.ll[b] = ll;
+        if (ch.prior) ch.prior[b] = prior;
         if (ch.tape_pos) ch.tape_pos[b] = rng.pos;
         if (ch.counter) ch.counter[b] = rng.ctr;
         if (ch.accepted)
@@ -763,6 +801,9 @@ int launch_mh(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg, const 
     a.nnz = ctx->adj_nnz;
     a.app_list = ctx->d_app_list;
     a.app_cnt = ctx->d_app_cnt;
+    a.alpha_g = ctx->d_alpha_g;
+    a.alpha_f = ctx->C == 3 ? ctx->d_alpha_f : nullptr;
+    a.size_prior = ctx->size_prior;
     a.ch = *chains;
     if (!a.ch.zone_of_site || !a.ch.w || !a.ch.p_global || !a.ch.ll || !a.ch.max_size ||
         !a.ch.p_grow_connected || (d.n_zones > 0 && !a.ch.p_zones) ||

@@ -18,9 +18,10 @@ zones come from the same python ``random`` calls (``random.sample`` of the free-
 to the reference's; weights are uniform and p_* the smoothed MLE.  The MH draws themselves come
 from Philox4x32-10 keyed by (seed, global chain id) — results do not depend on the GPU count.
 
-Supported model (checked, NotImplementedError otherwise): SAMPLE_SOURCE = false and the uniform
-priors of config/default_config.json:33-40 (every prior term is 0, so the MH ratio needs no
-prior).  MC3 (``mc3=True``) and ``sample_from_prior`` are not part of the batched path.
+Supported model (checked, NotImplementedError otherwise): SAMPLE_SOURCE = false; the priors of
+contact_zones_amd/priors.py (zero / uniform terms, 'counts' on universal and inheritance,
+'uniform' / 'quadratic' zone size), read from the reference Model's Prior or given as
+``priors=``.  MC3 (``mc3=True``) and ``sample_from_prior`` are not part of the batched path.
 
 Multi-GPU: one process per GPU.  With ``torch.distributed`` initialised, chains are sharded
 contiguously by rank; the only collectives are the per-operator counter sum at the end of a run,
@@ -34,6 +35,7 @@ from collections import defaultdict
 import numpy as np
 
 from . import packing
+from .priors import PriorSpec
 from .sampler import OPS, op_probabilities, precisions
 
 Q_REJECT = 0
@@ -94,24 +96,10 @@ def adjacency_csr(adj_mat, n_sites):
 
 
 def check_model(model):
-    """The batched sampler implements SAMPLE_SOURCE = false with uniform priors (log prior 0)."""
+    """The batched sampler implements SAMPLE_SOURCE = false (priors: contact_zones_amd/priors.py)."""
     if getattr(model, "sample_source", False):
         raise NotImplementedError("SAMPLE_SOURCE = true (source Gibbs sampling) is not supported "
                                   "by the batched sampler")
-    cfg = getattr(getattr(model, "prior", None), "config", None)
-    if cfg is None:
-        cfg = (getattr(model, "config", None) or {}).get("PRIOR")
-    if cfg is None:
-        return
-    zero = {"area_size": ("none",), "geo": ("uniform",), "weights": ("uniform",),
-            "universal": ("uniform",), "contact": ("uniform",), "inheritance": ("uniform",)}
-    for k, ok in zero.items():
-        if k == "inheritance" and not getattr(model, "inheritance", False):
-            continue
-        t = cfg.get(k, {}).get("type", ok[0]) if isinstance(cfg.get(k, {}), dict) else ok[0]
-        if t not in ok:
-            raise NotImplementedError(f"prior '{k}' of type '{t}': the batched sampler supports "
-                                      f"only the zero-valued priors ({k}: {ok[0]})")
 
 
 class InitialSamples:
@@ -267,7 +255,8 @@ class BatchedZoneMCMC:
     def __init__(self, model, data, operators, n_chains, var_proposal, p_grow_connected,
                  initial_size, initial_sample=None, mc3=False, swap_period=None, chain_swaps=None,
                  sample_from_prior=False, show_screen_log=False, logger=None, *, seed=None,
-                 rng=None, device=None, group=None, refresh_every_launch=True, **kwargs):
+                 rng=None, device=None, group=None, refresh_every_launch=True, priors=None,
+                 **kwargs):
         if mc3:
             raise NotImplementedError("MC3 chain swaps are not part of the batched sampler")
         if sample_from_prior:
@@ -306,6 +295,9 @@ class BatchedZoneMCMC:
         self.fn_operators = [k for k in self.operators]
         self.precision = precisions(var_proposal)
         self.refresh_every_launch = refresh_every_launch
+        # the prior terms of the MH ratio: from the reference Model's Prior (model.py:455-505)
+        # unless given; unsupported prior types raise NotImplementedError
+        self.priors = priors if priors is not None else PriorSpec.from_model(model, self.applicable_states)
 
         self.statistics = {'sample_id': [], 'sample_likelihood': [], 'sample_prior': [],
                            'sample_zones': [], 'sample_weights': [], 'sample_p_global': [],
@@ -340,7 +332,11 @@ class BatchedZoneMCMC:
         return list(operators.keys()), list(operators.values())
 
     def prior(self, sample, chain):
-        return 0.0  # uniform priors (check_model)
+        """Log prior of `sample` (Prior.__call__, model.py:484-505, for the supported types)."""
+        zos, w, pg, pz, pf, _ = self._pack(sample)
+        return float(self.priors.log_prior(zos[None], pg[None], None if pf is None else pf[None],
+                                           self.applicable_states, self.n_zones,
+                                           self.inheritance)[0])
 
     def likelihood(self, sample, chain):
         """Full log-likelihood of `sample` on the GPU (MCMCGenerative.likelihood, :106-127)."""
@@ -365,7 +361,7 @@ class BatchedZoneMCMC:
                                             self.inheritance, device=dev)
             self._sampler = Sampler(self._engine, self.applicable_states, self.adj_indptr,
                                     self.adj_indices, self.p_operators, self.precision,
-                                    self.min_size, warmup=self.IS_WARMUP)
+                                    self.min_size, warmup=self.IS_WARMUP, priors=self.priors)
         return self._engine
 
     def _pack(self, s):
@@ -406,8 +402,10 @@ class BatchedZoneMCMC:
         mine = samples[self.lo:self.hi]
         packed = [self._pack(s) for s in mine]
         stack = lambda k: np.stack([p[k] for p in packed]) if packed else None  # noqa: E731
-        self._state = ChainState(eng, stack(0), stack(1), stack(2), stack(3),
-                                 stack(4) if self.inheritance else None)
+        pf = stack(4) if self.inheritance else None
+        prior0 = self.priors.log_prior(stack(0), stack(2), pf, self.applicable_states,
+                                       self.n_zones, self.inheritance)
+        self._state = ChainState(eng, stack(0), stack(1), stack(2), stack(3), pf, prior=prior0)
         self._acc0 = self._state.accepted.clone()
         self._prop0 = self._state.proposed.clone()
         self._tape_pos = None
@@ -422,7 +420,8 @@ class BatchedZoneMCMC:
         ll = self._state.ll.cpu().numpy()
         self._ll[:] = -np.inf
         self._ll[self.lo:self.hi] = ll
-        self._prior[self.lo:self.hi] = 0.0
+        self._prior[:] = -np.inf
+        self._prior[self.lo:self.hi] = self._state.prior.cpu().numpy()
 
     def _advance(self, n):
         """n MH steps on every chain of this rank (one launch)."""
@@ -515,6 +514,9 @@ class BatchedZoneMCMC:
             if i_step % steps_per_sample == 0:
                 s0 = self._chain0_sample()
                 if self.rank == 0:
+                    # the logged sample's prior evaluated in full (the carried value differs by
+                    # rounding only): the reference logs Prior.__call__ of the sample
+                    self._prior[self.chain_idx[0]] = self.prior(s0, self.chain_idx[0])
                     self.log_sample_statistics(s0, c=self.chain_idx[0],
                                                sample_id=int(i_step / steps_per_sample))
             if (i_step + 1) % 1000 == 0 and self.rank == 0:

@@ -7,8 +7,8 @@ with the ZoneMCMC / ZoneMCMCWarmup operators (sbayes/sampling/zone_sampling.py:4
 ``ChainState`` holds it.  Draws come from Philox (production) or from a replay tape of the
 reference's own decisions (parity tests).
 
-Supported model: SAMPLE_SOURCE = false, uniform priors (the reference default priors,
-config/default_config.json:35-42).  Operator names and their canonical order follow
+Supported model: SAMPLE_SOURCE = false; zero (uniform) priors, 'counts' priors on p_global /
+p_families and 'uniform' / 'quadratic' zone-size priors (contact_zones_amd/priors.py).  Operator names and their canonical order follow
 ``include/sbz.h`` (sbz_op).
 """
 import ctypes
@@ -51,7 +51,7 @@ def precisions(var_proposal):
 class ChainState:
     """Device-resident state of B chains (torch tensors on the engine's GPU)."""
 
-    def __init__(self, engine, zone_of_site, w, p_global, p_zones, p_fam=None):
+    def __init__(self, engine, zone_of_site, w, p_global, p_zones, p_fam=None, prior=None):
         torch = _torch()
         dev = torch.device("cuda", engine.device)
         self.engine = engine
@@ -66,6 +66,10 @@ class ChainState:
         engine._check_shapes(self.B, self.zone_of_site, self.w, self.p_global, self.p_zones,
                              self.p_fam, None)
         self.ll = torch.empty(self.B, dtype=f64, device=dev)
+        # log prior of each chain (carried by the sampler; 0 when every prior term is zero)
+        self.prior = (torch.zeros(self.B, dtype=f64, device=dev) if prior is None else
+                      torch.as_tensor(np.broadcast_to(np.asarray(prior, np.float64), (self.B,)).copy(),
+                                      device=dev))
         self.accepted = torch.zeros((self.B, 8), dtype=torch.int64, device=dev)
         self.proposed = torch.zeros((self.B, 8), dtype=torch.int64, device=dev)
         self.counter = torch.zeros(self.B, dtype=torch.int64, device=dev)
@@ -85,7 +89,7 @@ class ChainState:
     def to_numpy(self):
         out = {"zone_of_site": self.zone_of_site.cpu().numpy(), "w": self.w.cpu().numpy(),
                "p_global": self.p_global.cpu().numpy(), "p_zones": self.p_zones.cpu().numpy(),
-               "ll": self.ll.cpu().numpy()}
+               "ll": self.ll.cpu().numpy(), "prior": self.prior.cpu().numpy()}
         if self.p_fam is not None:
             out["p_fam"] = self.p_fam.cpu().numpy()
         return out
@@ -95,7 +99,7 @@ class Sampler:
     """MH sampler over a LikelihoodEngine's context (same data, same GPU)."""
 
     def __init__(self, engine, applicable_states, adj_indptr, adj_indices, operators, var_proposal,
-                 min_size, warmup=False):
+                 min_size, warmup=False, priors=None):
         self.engine = engine
         states = np.ascontiguousarray(applicable_states, dtype=np.uint8)
         if states.shape != (engine.n_features, engine.n_states):
@@ -117,6 +121,28 @@ class Sampler:
             self.cfg.precision[i] = float(prec[i])
         self.cfg.min_size = int(min_size)
         self.cfg.warmup = int(bool(warmup))
+        self.set_priors(priors)
+
+    def set_priors(self, priors):
+        """The prior terms of the MH ratio (contact_zones_amd.priors.PriorSpec; None = zero)."""
+        from .priors import PriorSpec
+        p = priors if priors is not None else PriorSpec()
+        eng = self.engine
+        F, S = eng.n_features, eng.n_states
+        ag = af = None
+        if p.alpha_global is not None:
+            ag = np.ascontiguousarray(p.alpha_global, np.float64)
+            if ag.shape != (F, S):
+                raise ValueError(f"alpha_global: expected {(F, S)}, got {ag.shape}")
+        if p.alpha_fam is not None:
+            af = np.ascontiguousarray(p.alpha_fam, np.float64)
+            if af.shape != (eng.n_families, F, S):
+                raise ValueError(f"alpha_fam: expected {(eng.n_families, F, S)}, got {af.shape}")
+        vp = ctypes.c_void_p
+        check(eng._lib.sbz_set_priors(eng.ctx, vp(ag.ctypes.data) if ag is not None else None,
+                                      vp(af.ctypes.data) if af is not None else None,
+                                      int(p.size_prior)), eng.ctx)
+        self.priors = p
 
     def run(self, state, n_steps, max_size, p_grow_connected, seed=0, chain_id0=0, tape=None,
             tape_len=None, tape_pos=None, trace=False, trace_zones=False):
@@ -140,6 +166,7 @@ class Sampler:
         ch.p_zones = state.p_zones.data_ptr()
         ch.p_fam = state.p_fam.data_ptr() if state.p_fam is not None else None
         ch.ll = state.ll.data_ptr()
+        ch.prior = state.prior.data_ptr()
         ch.max_size = ms.data_ptr()
         ch.p_grow_connected = pg.data_ptr()
         out = {"status": torch.zeros(B, dtype=torch.int32, device=dev)}

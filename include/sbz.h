@@ -116,7 +116,8 @@ uint64_t sbz_lik_lds_bytes(const sbz_dims *dims, int source_mode);
 /* ------------------------------------------------------------------------------------------
  * Metropolis-Hastings sampler  (MCMCGenerative.step, sbayes/sampling/mcmc_generative.py:282-351,
  * operators of ZoneMCMC / ZoneMCMCWarmup, sbayes/sampling/zone_sampling.py:408-933, 1272-1577;
- * SAMPLE_SOURCE = false, uniform priors).  One wave runs one chain for n_steps in one launch.
+ * SAMPLE_SOURCE = false; zero, 'counts' and zone-size priors).  One wave runs one chain for
+ * n_steps in one launch.
  * ------------------------------------------------------------------------------------------ */
 
 /* Canonical operator order of sbz_mh_config.op_prob. */
@@ -155,12 +156,28 @@ typedef struct sbz_chains {
     uint8_t *trace_accept;            /* [B][n_steps] (with trace_op) */
     double *trace_ll;                 /* [B][n_steps] (with trace_op) */
     uint8_t *trace_zos;               /* [B][n_steps][N] or NULL (tests) */
+    double *prior;                    /* [B] in/out: the chain's log prior (sbz_set_priors), or NULL
+                                         when every prior term is 0 */
 } sbz_chains;
 
 /* Sampler-only data: applicable states (uint8 [F][S], data.states) and the site network as CSR
  * (data.network['adj_mat'], sbayes/util.py:139-155; rows sorted).  Call once after sbz_open. */
 int sbz_set_network(sbz_ctx *ctx, const uint8_t *applicable, int32_t nnz, const int32_t *adj_indptr,
                     const int32_t *adj_indices);
+
+/* Priors of the MH ratio (Prior.__call__, sbayes/model.py:484-505).  Default: all zero (the
+ * uniform priors of config/default_config.json:33-40).
+ *   alpha_global  double [F][S] or NULL: 'counts' prior on p_global — the Dirichlet
+ *                 concentration of each applicable state (PGlobalPrior.dirichlet,
+ *                 model.py:571-597, util.counts_to_dirichlet); other entries ignored.
+ *   alpha_fam     double [Fam][F][S] or NULL: 'counts' prior on p_families (PFamiliesPrior,
+ *                 model.py:631-672, util.inheritance_counts_to_dirichlet).
+ *   size_prior    0 'none', 1 'uniform' (-sum log C(N, size)), 2 'quadratic' (-sum log size^2)
+ *                 (ZoneSizePrior, model.py:893-976).
+ * The kernel adds the prior difference of each proposal (dirichlet_logpdf terms of the two
+ * altered states, or the changed zone size) to the MH ratio and carries sbz_chains.prior. */
+int sbz_set_priors(sbz_ctx *ctx, const double *alpha_global, const double *alpha_fam,
+                   int32_t size_prior);
 
 /* Run n_steps MH steps on B device-resident chains; asynchronous on ctx's stream. */
 int sbz_mh_run_device(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg,

@@ -6,7 +6,8 @@ CPU-baseline leg may import it, and only as the checker.  The product path never
 
 It replays a *decision tape* (tests/golden/make_golden_mh.py) through a restatement of
 ``MCMCGenerative.step`` (sbayes/sampling/mcmc_generative.py:282-351) and the operators of
-``ZoneMCMC`` / ``ZoneMCMCWarmup`` with SAMPLE_SOURCE = false and uniform priors (log prior 0):
+``ZoneMCMC`` / ``ZoneMCMCWarmup`` with SAMPLE_SOURCE = false; priors zero (uniform), 'counts'
+on p_global / p_families and 'uniform' / 'quadratic' on zone sizes (``Model.log_prior``):
 
   shrink_zone   zone_sampling.py:866-933      (warm-up :1498-1574: q_back = 1/(size+1))
   grow_zone     zone_sampling.py:788-864      (warm-up :1418-1496)
@@ -23,7 +24,7 @@ oracle/lik_numpy.py, bit-exact with the reference's Likelihood.__call__.
 import math
 
 import numpy as np
-from scipy.special import gammaln, xlogy
+from scipy.special import betaln, gammaln, xlogy
 
 from . import lik_numpy
 
@@ -79,6 +80,49 @@ class Model:
         N = self.obs.shape[0]
         indptr, indices = fx["adj_indptr"], fx["adj_indices"]
         self.adj = [indices[indptr[s]:indptr[s + 1]] for s in range(N)]
+        self.n_zones = int(fx["n_zones"])
+        self.size_prior = int(fx["prior_size"]) if "prior_size" in fx else 0
+        self.alpha_global = fx.get("prior_alpha_global")
+        self.alpha_fam = fx.get("prior_alpha_fam")
+
+    def log_prior(self, st):
+        """Prior.__call__ (model.py:484-505) for the supported types: zone size 'none' /
+        'uniform' / 'quadratic' (model.py:932-971), geo / weights / p_zones uniform (0),
+        'counts' on p_global and p_families (prior_p_global_dirichlet model.py:1142-1170,
+        prior_p_families_dirichlet :1173-1219, util.dirichlet_logpdf = scipy _logpdf)."""
+        zos = st["zos"]
+        N = zos.shape[0]
+        log_prior = 0
+        sizes = np.array([np.count_nonzero(zos == z) for z in range(self.n_zones)], dtype=np.int64)
+        if self.size_prior == 1:
+            log_prior += -np.sum(-betaln(1 + N - sizes, 1 + sizes) - np.log(N + 1))
+        elif self.size_prior == 2:
+            log_prior += -np.sum(np.log(sizes ** 2))
+        else:
+            log_prior += 0.
+        log_prior += 0.  # geo
+        log_prior += 0.  # weights
+        if self.alpha_global is not None:
+            lp = np.zeros(self.states.shape[0])
+            for f in range(self.states.shape[0]):
+                idx = np.flatnonzero(self.states[f])
+                lp[f] = dirichlet_logpdf(st["pg"][f, idx], self.alpha_global[f, idx])
+            log_prior += np.sum(lp)
+        else:
+            log_prior += 0
+        log_prior += 0.  # p_zones
+        if self.inheritance:
+            if self.alpha_fam is not None:
+                n_fam = self.alpha_fam.shape[0]
+                lp = np.zeros((n_fam, self.states.shape[0]))
+                for fam in range(n_fam):
+                    for f in range(self.states.shape[0]):
+                        idx = np.flatnonzero(self.states[f])
+                        lp[fam, f] = dirichlet_logpdf(st["pf"][fam, f, idx], self.alpha_fam[fam, f, idx])
+                log_prior += np.sum(lp)
+            else:
+                log_prior += 0.
+        return log_prior
 
     def neighbours(self, zone, occupied):
         """get_neighbours: sites adjacent to the zone that are in no zone (util.py:152-155)."""
@@ -227,22 +271,23 @@ OPERATORS = {SHRINK: op_shrink, GROW: op_grow, SWAP: op_swap, WEIGHTS: op_weight
              P_GLOBAL: op_p_global, P_ZONES: op_p_zones, P_FAMILIES: op_p_families}
 
 
-def step(m, st, ll, c, tape):
-    """MCMCGenerative.step (mcmc_generative.py:282-329) with uniform priors.
-    Returns (state, ll, op, accepted)."""
+def step(m, st, ll, prior, c, tape):
+    """MCMCGenerative.step (mcmc_generative.py:282-329).  Returns (state, ll, prior, op,
+    accepted)."""
     op = tape.int()
     cand, log_q, log_q_back = OPERATORS[op](m, st, c, tape)
     if log_q_back == -np.inf:
-        return st, ll, op, False
+        return st, ll, prior, op, False
     ll_cand = m.loglik(cand)
+    prior_cand = m.log_prior(cand)
     if log_q == -np.inf:
         accept = True
     else:
-        mh = ((ll_cand - ll) * 1.0) - (log_q - log_q_back) + (0.0 - 0.0)
+        mh = ((ll_cand - ll) * 1.0) - (log_q - log_q_back) + (prior_cand - prior)
         accept = math.log(tape.real()) < mh
     if accept:
-        return cand, ll_cand, op, True
-    return st, ll, op, False
+        return cand, ll_cand, prior_cand, op, True
+    return st, ll, prior, op, False
 
 
 def initial_state(fx, c):
@@ -259,14 +304,17 @@ def replay(fx, chain, n_steps=None):
     m = Model(fx)
     st = initial_state(fx, chain)
     ll = m.loglik(st)
+    prior = m.log_prior(st)
+    init_prior = prior
     tape = TapeReader(fx["tape"][chain, :int(fx["tape_len"][chain])])
     steps = fx["step_op"].shape[1] if n_steps is None else n_steps
-    ops, acc, lls, zos = [], [], [], []
+    ops, acc, lls, priors, zos = [], [], [], [], []
     for _ in range(steps):
-        st, ll, op, a = step(m, st, ll, chain, tape)
+        st, ll, prior, op, a = step(m, st, ll, prior, chain, tape)
         ops.append(op)
         acc.append(a)
         lls.append(ll)
+        priors.append(prior)
         zos.append(st["zos"].copy())
-    return dict(op=np.array(ops), accept=np.array(acc), ll=np.array(lls), zos=np.array(zos),
-                state=st, tape_used=tape.pos)
+    return dict(op=np.array(ops), accept=np.array(acc), ll=np.array(lls), prior=np.array(priors),
+                init_prior=init_prior, zos=np.array(zos), state=st, tape_used=tape.pos)

@@ -147,7 +147,10 @@ def run_case(name, data, model_cfg, mcmc_cfg, steps, seed, warmup, n_chains):
             init[c] = s.copy()
             return s
 
+        init_prior = {}
+
         def step(sample, c):
+            init_prior.setdefault(c, float(sampler._prior[c]))  # the chain's prior at its start
             TAPE.chain = c
             acc0 = sampler.statistics["accepted_steps"]
             n0 = len(TAPE.items.get(c, []))
@@ -156,7 +159,8 @@ def run_case(name, data, model_cfg, mcmc_cfg, steps, seed, warmup, n_chains):
             op = int(TAPE.items[c][n0])
             steps_out[c].append((op, sampler.statistics["accepted_steps"] > acc0,
                                  float(sampler._ll[c]),
-                                 packing.zones_to_zone_of_site(new.zones, N)))
+                                 packing.zones_to_zone_of_site(new.zones, N),
+                                 float(sampler._prior[c])))
             return new
 
         sampler.step = step
@@ -214,6 +218,35 @@ def run_case(name, data, model_cfg, mcmc_cfg, steps, seed, warmup, n_chains):
     out["step_ll"] = np.array([[s[2] for s in steps_out[c]] for c in range(n_chains)])
     out["step_zone_of_site"] = np.array([[s[3] for s in steps_out[c]] for c in range(n_chains)],
                                         np.uint8)
+    out["step_prior"] = np.array([[s[4] for s in steps_out[c]] for c in range(n_chains)])
+    # priors as the chains used them (Prior, model.py:455-505): Dirichlet concentrations of the
+    # 'counts' priors scattered to [F][S] / [Fam][F][S] (0 at inapplicable states), size prior.
+    # Taken from a chain's model copy (mcmc_generative.py:80): every copy re-parses the config and
+    # rescales data.prior_inheritance['counts'] in place (model.py:654-660), which moves the
+    # family concentrations by an ulp from the first model's.
+    pr = sampler.posterior_per_chain[0].prior
+    if model_cfg["INHERITANCE"] and pr.prior_p_families.prior_type.value == "counts":
+        for c in range(1, n_chains):  # every copy after the first carries the same values
+            other = sampler.posterior_per_chain[c].prior.prior_p_families.dirichlet
+            for fam_a, fam_b in zip(pr.prior_p_families.dirichlet, other):
+                assert all(np.array_equal(x, y) for x, y in zip(fam_a, fam_b))
+    states = np.asarray(data.states, bool)
+    F, S = states.shape
+    out["prior_size"] = np.array({"none": 0, "uniform": 1, "quadratic": 2}[
+        model_cfg["PRIOR"]["area_size"]["type"]])
+    if pr.prior_p_global.prior_type.value == "counts":
+        ag = np.zeros((F, S))
+        for f in range(F):
+            ag[f, states[f]] = pr.prior_p_global.dirichlet[f]
+        out["prior_alpha_global"] = ag
+    if model_cfg["INHERITANCE"] and pr.prior_p_families.prior_type.value == "counts":
+        n_fam = len(pr.prior_p_families.dirichlet)
+        af = np.zeros((n_fam, F, S))
+        for fam in range(n_fam):
+            for f in range(F):
+                af[fam, f, states[f]] = pr.prior_p_families.dirichlet[fam][f]
+        out["prior_alpha_fam"] = af
+    out["init_prior"] = np.array([init_prior[c] for c in range(n_chains)])
     if warmup:
         out["best_zone_of_site"] = packing.zones_to_zone_of_site(best.zones, N)
         out["best_w"] = np.asarray(best.weights)
@@ -298,12 +331,28 @@ def small_data(seed=7, N=40, F=12, S=4, fam=2):
     return types.SimpleNamespace(features=x, states=states, network=net, families=fams)
 
 
-def model_cfg(Z, inheritance, min_m=3, max_m=50):
+def model_cfg(Z, inheritance, min_m=3, max_m=50, counts=False, size="none"):
+    prior = {"geo": {"type": "uniform"}, "area_size": {"type": size},
+             "weights": {"type": "uniform"}, "universal": {"type": "uniform"},
+             "inheritance": {"type": "uniform"}, "contact": {"type": "uniform"}}
+    if counts:  # as experiments/balkan/config.json:34-50
+        prior["universal"] = {"type": "counts", "scale_counts": None}
+        prior["inheritance"] = {"type": "counts", "scale_counts": 10}
     return {"N_AREAS": Z, "MIN_M": min_m, "MAX_M": max_m, "INHERITANCE": inheritance,
-            "SAMPLE_SOURCE": False,
-            "PRIOR": {"geo": {"type": "uniform"}, "area_size": {"type": "none"},
-                      "weights": {"type": "uniform"}, "universal": {"type": "uniform"},
-                      "inheritance": {"type": "uniform"}, "contact": {"type": "uniform"}}}
+            "SAMPLE_SOURCE": False, "PRIOR": prior}
+
+
+def with_counts(d, seed=11):
+    """Attach prior counts (load_data.py:86, 113 layouts: 'counts' [F][S], [Fam][F][S]) drawn for
+    the applicable states."""
+    rng = np.random.default_rng(seed)
+    st = np.asarray(d.states, bool)
+    cu = np.where(st, rng.integers(0, 40, size=st.shape), 0).astype(float)
+    n_fam = d.families.shape[0]
+    ci = np.where(st[None], rng.integers(0, 25, size=(n_fam,) + st.shape), 0).astype(float)
+    return types.SimpleNamespace(features=d.features, states=d.states, network=d.network,
+                                 families=d.families, prior_universal={"counts": cu},
+                                 prior_inheritance={"counts": ci})
 
 
 def mcmc_cfg(area=0.4, m_initial=5, p_grow=0.85, inheritance=0.1):
@@ -327,6 +376,12 @@ def main():
              steps=400, seed=6, warmup=False, n_chains=3)
     run_case("small_warmup", s, model_cfg(2, True, min_m=3, max_m=8), mcmc_cfg(area=0.8, m_initial=4),
              steps=300, seed=8, warmup=True, n_chains=4)
+    sc = with_counts(s)
+    run_case("small_priors", sc, model_cfg(3, True, min_m=3, max_m=6, counts=True, size="uniform"),
+             mcmc_cfg(area=0.6, m_initial=4), steps=400, seed=9, warmup=False, n_chains=3)
+    run_case("small_priors_warmup", sc,
+             model_cfg(2, True, min_m=3, max_m=8, counts=True, size="quadratic"),
+             mcmc_cfg(area=0.6, m_initial=4), steps=300, seed=10, warmup=True, n_chains=4)
 
 
 if __name__ == "__main__":

@@ -30,7 +30,7 @@ def test_generate_samples_statistics_match_reference(case, gpu_available):
     st = smp.statistics
     assert st["sample_id"] == fx["stat_sample_id"].tolist()
     np.testing.assert_allclose(st["sample_likelihood"], fx["stat_sample_likelihood"], rtol=RTOL)
-    assert st["sample_prior"] == fx["stat_sample_prior"].tolist()
+    assert st["sample_prior"] == fx["stat_sample_prior"].tolist()  # bit-exact (host Prior)
     np.testing.assert_array_equal(np.array(st["sample_zones"]), fx["stat_sample_zones"])
     np.testing.assert_array_equal(np.array(st["sample_weights"]), fx["stat_sample_weights"])
     np.testing.assert_array_equal(np.array(st["sample_p_global"]), fx["stat_sample_p_global"])

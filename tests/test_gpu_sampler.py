@@ -21,10 +21,12 @@ def _setup(fx):
     Z = int(fx["n_zones"])
     Fam = fx["init_p_fam"].shape[1] if inh else 0
     eng = LikelihoodEngine(fx["obs"], fx["fam_of_site"], S, Z, Fam, inh)
+    from contact_zones_amd.priors import PriorSpec
+    priors = PriorSpec(fx.get("prior_alpha_global"), fx.get("prior_alpha_fam"), int(fx["prior_size"]))
     smp = Sampler(eng, fx["states"], fx["adj_indptr"], fx["adj_indices"], fx["op_probs"],
-                  fx["precision"], int(fx["min_size"]), warmup=bool(fx["warmup"]))
+                  fx["precision"], int(fx["min_size"]), warmup=bool(fx["warmup"]), priors=priors)
     st = ChainState(eng, fx["init_zone_of_site"], fx["init_w"], fx["init_p_global"],
-                    fx["init_p_zones"], fx["init_p_fam"] if inh else None)
+                    fx["init_p_zones"], fx["init_p_fam"] if inh else None, prior=fx["init_prior"])
     return eng, smp, st
 
 
@@ -45,6 +47,8 @@ def test_tape_replay_matches_reference(gpu_available, case):
     ll = out["ll"].cpu().numpy()
     rel = np.abs(ll - fx["step_ll"]) / np.abs(fx["step_ll"])
     assert rel.max() <= REL_TOL, rel.max()
+    # the carried log prior (prior += proposal difference) ends at the reference's value
+    np.testing.assert_allclose(st.prior.cpu().numpy(), fx["step_prior"][:, -1], rtol=1e-12, atol=1e-12)
     # the incrementally tracked ll equals a fresh full evaluation of the final state
     final = st.ll.cpu().numpy().copy()
     fresh = st.refresh_ll().cpu().numpy()
@@ -105,3 +109,21 @@ def test_philox_chains_are_valid_and_reproducible(gpu_available):
     torch.cuda.synchronize()
     np.testing.assert_array_equal(st2_one.zone_of_site.cpu().numpy()[0], s["zone_of_site"][1])
     np.testing.assert_array_equal(st2_one.w.cpu().numpy()[0], s["w"][1])
+
+
+def test_philox_carried_prior_matches_full_prior(gpu_available):
+    """'counts' + zone-size priors under Philox draws: after 3000 steps the prior the kernel
+    carries (prior += proposal difference) equals the full Prior of the final states."""
+    import torch
+    from contact_zones_amd.priors import PriorSpec
+    fx = load_golden("mh_small_priors")
+    eng, smp, st = _setup(fx)
+    out = smp.run(st, 3000, fx["max_size"], fx["p_grow_connected"], seed=99)
+    torch.cuda.synchronize()
+    assert out["status"].cpu().numpy().tolist() == [0] * st.B
+    s = st.to_numpy()
+    spec = PriorSpec(fx["prior_alpha_global"], fx["prior_alpha_fam"], int(fx["prior_size"]))
+    full = spec.log_prior(s["zone_of_site"], s["p_global"], s["p_fam"], fx["states"],
+                          int(fx["n_zones"]), True)
+    np.testing.assert_allclose(s["prior"], full, rtol=1e-12)
+    assert np.any(s["prior"] != fx["init_prior"])  # the prior moved

@@ -11,6 +11,7 @@ from conftest import golden_cases, load_golden
 from contact_zones_amd import packing
 from contact_zones_amd.mcmc import (BatchedZoneMCMC, BatchedZoneMCMCWarmup, InitialSamples,
                                     check_model, get_max_size_list)
+from contact_zones_amd.priors import PriorSpec
 from contact_zones_amd.sampler import OPS
 
 MH_CASES = golden_cases("mh_", exclude=())
@@ -36,7 +37,9 @@ def objects_from_fixture(fx):
                     "inheritance": prec[3] if inh else None}
     kw = dict(model=model, data=data, operators=ops, n_chains=fx["init_w"].shape[0],
               var_proposal=var_proposal, p_grow_connected=float(fx["p_grow_base"]),
-              initial_size=int(fx["initial_size"]))
+              initial_size=int(fx["initial_size"]),
+              priors=PriorSpec(fx.get("prior_alpha_global"), fx.get("prior_alpha_fam"),
+                               int(fx["prior_size"])))
     return kw
 
 
@@ -93,20 +96,9 @@ def test_initial_sample_reuses_previous_sample():
 
 
 def test_model_checks():
-    ok = types.SimpleNamespace(sample_source=False, inheritance=True, prior=types.SimpleNamespace(
-        config={"geo": {"type": "uniform"}, "area_size": {"type": "none"},
-                "weights": {"type": "uniform"}, "universal": {"type": "uniform"},
-                "inheritance": {"type": "uniform"}, "contact": {"type": "uniform"}}))
-    check_model(ok)
+    check_model(types.SimpleNamespace(sample_source=False, inheritance=True))
     with pytest.raises(NotImplementedError):
         check_model(types.SimpleNamespace(sample_source=True, inheritance=False))
-    bad = types.SimpleNamespace(**vars(ok))
-    bad.prior = types.SimpleNamespace(config=dict(ok.prior.config, universal={"type": "counts"}))
-    with pytest.raises(NotImplementedError):
-        check_model(bad)
-    bad.prior = types.SimpleNamespace(config=dict(ok.prior.config, area_size={"type": "uniform"}))
-    with pytest.raises(NotImplementedError):
-        check_model(bad)
 
 
 def test_unsupported_options_raise():

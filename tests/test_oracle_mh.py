@@ -19,8 +19,11 @@ def test_oracle_replays_reference_trajectory(case):
         np.testing.assert_array_equal(r["accept"], fx["step_accept"][c])
         np.testing.assert_array_equal(r["zos"], fx["step_zone_of_site"][c])
         np.testing.assert_array_equal(r["ll"], fx["step_ll"][c])
+        # log prior (Prior.__call__): bit-exact at the start and after every step
+        assert r["init_prior"] == fx["init_prior"][c]
+        np.testing.assert_array_equal(r["prior"], fx["step_prior"][c])
         assert r["tape_used"] == int(fx["tape_len"][c])
-        lls.append(r["ll"][-1])
+        lls.append(r["ll"][-1] + r["prior"][-1])
     if bool(fx["warmup"]):
         # best chain = argmax(ll + prior) after the warm-up (mcmc_generative.py:195-200)
         best = int(np.argmax(lls))
@@ -37,3 +40,14 @@ def test_fixtures_cover_every_operator_and_rejection_kind():
         rejected_zone_moves += int(np.sum(zone & ~fx["step_accept"]))
     assert np.all(ops > 50), ops
     assert rejected_zone_moves > 50
+
+
+def test_fixtures_cover_the_prior_types():
+    """'counts' priors on p_global / p_families, and both non-trivial zone-size priors."""
+    sizes, counts_g, counts_f = set(), 0, 0
+    for case in MH_CASES:
+        fx = load_golden(case)
+        sizes.add(int(fx["prior_size"]))
+        counts_g += "prior_alpha_global" in fx
+        counts_f += "prior_alpha_fam" in fx
+    assert sizes == {0, 1, 2} and counts_g >= 2 and counts_f >= 2
