@@ -273,6 +273,11 @@ def run_case(name, data, model_cfg, mcmc_cfg, steps, seed, warmup, n_chains):
         out["stat_reject_operator"] = np.array([st["reject_operator"].get(k, 0) for k in OPS])
         out["stat_last_zones"] = np.asarray(st["last_sample"].zones, bool)
         out["stat_last_weights"] = np.asarray(st["last_sample"].weights, np.float64)
+        # the reference's per-zone contributions of every logged sample (postprocessing.py:271-313)
+        from sbayes.postprocessing import contribution_per_area
+        contribution_per_area(sampler)
+        out["stat_lh_single_zones"] = np.asarray(sampler.statistics["sample_lh_single_zones"])
+        out["stat_prior_single_zones"] = np.asarray(sampler.statistics["sample_prior_single_zones"])
     # run metadata (for the host-side drop-in tests: initial samples, warm-up lists)
     out["seed"] = np.array(seed)
     out["initial_size"] = np.array(mcmc_cfg["M_INITIAL"])
