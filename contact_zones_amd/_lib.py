@@ -31,8 +31,9 @@ _D = ctypes.c_double
 
 
 class sbz_mh_config(ctypes.Structure):
-    _fields_ = [("op_prob", _D * 8), ("precision", _D * 4), ("min_size", ctypes.c_int32),
-                ("warmup", ctypes.c_int32)]
+    _fields_ = [("op_prob", ctypes.c_double * 16), ("precision", ctypes.c_double * 4),
+                ("min_size", ctypes.c_int32), ("warmup", ctypes.c_int32),
+                ("sample_source", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 class sbz_chains(ctypes.Structure):
@@ -48,7 +49,9 @@ class sbz_chains(ctypes.Structure):
                 ("proposed", ctypes.c_void_p), ("status", ctypes.c_void_p),
                 ("trace_op", ctypes.c_void_p), ("trace_accept", ctypes.c_void_p),
                 ("trace_ll", ctypes.c_void_p), ("trace_zos", ctypes.c_void_p),
-                ("prior", ctypes.c_void_p)]
+                ("prior", ctypes.c_void_p), ("source", ctypes.c_void_p),
+                ("alias_pending", ctypes.c_void_p), ("alias_p_global", ctypes.c_void_p),
+                ("alias_p_zones", ctypes.c_void_p), ("alias_p_fam", ctypes.c_void_p)]
 
 
 # name -> (restype, argtypes); every symbol declared in include/sbz.h
@@ -71,6 +74,7 @@ SIGNATURES = {
     "sbz_lik_lds_bytes": (ctypes.c_uint64, [ctypes.POINTER(sbz_dims), _I]),
     "sbz_set_network": (_I, [_P, _P, ctypes.c_int32, _P, _P]),
     "sbz_set_priors": (_I, [_P, _P, _P, ctypes.c_int32]),
+    "sbz_set_gibbs_counts": (_I, [_P, _P, _P]),
     "sbz_mh_run_device": (_I, [_P, _I, _I, ctypes.POINTER(sbz_mh_config), ctypes.POINTER(sbz_chains)]),
     "sbz_mh_lds_bytes": (ctypes.c_uint64, [ctypes.POINTER(sbz_dims)]),
 }

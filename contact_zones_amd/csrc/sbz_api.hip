@@ -221,7 +221,8 @@ void sbz_close(sbz_ctx *ctx) {
     if (ctx->d_perm) (void)hipFree(ctx->d_perm);
     for (void *p : {(void *)ctx->d_obs_sm, (void *)ctx->d_fam_site, (void *)ctx->d_adj_ptr,
                     (void *)ctx->d_adj_idx, (void *)ctx->d_app_list, (void *)ctx->d_app_cnt,
-                    (void *)ctx->d_alpha_g, (void *)ctx->d_alpha_f})
+                    (void *)ctx->d_alpha_g, (void *)ctx->d_alpha_f, (void *)ctx->d_gc_g,
+                    (void *)ctx->d_gc_f})
         if (p) (void)hipFree(p);
     if (ctx->d_cnt) (void)hipFree(ctx->d_cnt);
     free_buf(ctx->zl);
@@ -378,6 +379,31 @@ int sbz_set_priors(sbz_ctx *ctx, const double *alpha_global, const double *alpha
     int rc = upload(alpha_global, fs, &ctx->d_alpha_g);
     if (rc == SBZ_OK) rc = upload(alpha_fam, (size_t)ctx->d.n_families * fs, &ctx->d_alpha_f);
     if (rc == SBZ_OK) ctx->size_prior = size_prior;
+    return rc;
+}
+
+int sbz_set_gibbs_counts(sbz_ctx *ctx, const double *counts_global, const double *counts_fam) {
+    if (!ctx) return SBZ_EINVAL;
+    if (counts_fam && (ctx->C != 3 || ctx->d.n_families == 0))
+        return fail(ctx, SBZ_EINVAL, "counts_fam needs inheritance with families");
+    const size_t fs = (size_t)ctx->d.n_features * ctx->d.n_states;
+    (void)hipSetDevice(ctx->device);
+    for (double **pp : {&ctx->d_gc_g, &ctx->d_gc_f}) {
+        if (*pp) (void)hipFree(*pp);
+        *pp = nullptr;
+    }
+    auto upload = [&](const double *src, size_t n, double **dst) -> int {
+        if (!src) return SBZ_OK;
+        for (size_t i = 0; i < n; i++)
+            if (!(src[i] >= 0.0) || std::isinf(src[i]))
+                return fail(ctx, SBZ_EINVAL, "Gibbs prior counts must be finite and >= 0");
+        if (hipMalloc(dst, n * sizeof(double)) != hipSuccess)
+            return fail(ctx, SBZ_ENOMEM, "Gibbs counts allocation failed");
+        hipError_t e = hipMemcpy(*dst, src, n * sizeof(double), hipMemcpyHostToDevice);
+        return e == hipSuccess ? SBZ_OK : hip_fail(ctx, e, "Gibbs counts upload");
+    };
+    int rc = upload(counts_global, fs, &ctx->d_gc_g);
+    if (rc == SBZ_OK) rc = upload(counts_fam, (size_t)ctx->d.n_families * fs, &ctx->d_gc_f);
     return rc;
 }
 

@@ -63,6 +63,8 @@ struct sbz_ctx {
     double *d_alpha_g = nullptr;  // [F][S] 'counts' prior on p_global (sbz_set_priors) or null
     double *d_alpha_f = nullptr;  // [Fam][F][S] 'counts' prior on p_families or null
     int size_prior = 0;           // 0 none, 1 uniform, 2 quadratic
+    double *d_gc_g = nullptr;     // [F][S] Gibbs prior counts of p_global (sbz_set_gibbs_counts)
+    double *d_gc_f = nullptr;     // [Fam][F][S] of p_families
     int zspl = 8;          // zoned sites per lane and chunk of the zone-sparse kernel
     int lik_kernel = 1;    // SBZ_LIK_KERNEL: 1 dense (default), 2 zone-sparse ("zoned"),
                            // 3 dense double-buffered ("db", where the table fits 4 KiB)

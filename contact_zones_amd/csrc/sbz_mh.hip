@@ -22,284 +22,13 @@
 // bit-exact trajectories; otherwise Philox4x32-10 keyed by (seed, global chain id).
 #include <cmath>
 #include <cstdint>
+#include <string>
 
-#include "sbz_internal.h"
+#include "sbz_mh_common.h"
 
 namespace sbz {
 
-namespace {
 
-constexpr int WAVE = 64;
-constexpr int NONE = 255;
-constexpr double LN2 = 0.69314718055994530941723212145818;
-enum Op { SHRINK = 0, GROW = 1, SWAP = 2, WEIGHTS = 3, P_GLOBAL = 4, P_ZONES = 5, P_FAMILIES = 6 };
-
-__device__ __forceinline__ void wsync() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-}
-
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
-}
-
-__device__ __forceinline__ int wave_sum_i(int v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
-}
-
-__device__ __forceinline__ int lane_prefix(uint64_t mask) {
-    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
-                                          __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-}
-
-// Range-checked index: an index outside [0, lim) is recorded (the first one, as `code`, with its
-// value) and replaced by 0, so no access ever leaves its allocation; the chain then stops with
-// status 16 + code (a replay mismatch or corrupt input, never silently).
-#define MH_IDX(i, lim, code) sbz_mh_idx((long long)(i), (long long)(lim), (code), err, err_val)
-__device__ __forceinline__ size_t sbz_mh_idx(long long i, long long lim, int code, int &err,
-                                             long long &err_val) {
-    if (i >= 0 && i < lim) return (size_t)i;
-    if (!err) {
-        err = code;
-        err_val = i;
-    }
-    return 0;
-}
-
-// The chain's parameters are rewritten inside the kernel (lane 0, on acceptance) and re-read by
-// every lane in later steps.  A plain load can hit a line the CU's vector L1 cached before the
-// store, so parameter loads bypass L1 (sc1) and parameter stores are sc1 stores followed by
-// vmcnt(0) (MI355X_MICROARCH.md, the sc1 rows of the hand-off table).
-__device__ __forceinline__ double ldp(const double *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void stp(double *p, double v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ void renorm(double &m, int &e) {
-    e += __builtin_amdgcn_frexp_exp(m);
-    m = __builtin_amdgcn_frexp_mant(m);
-}
-
-// ---------------------------------------------------------------------------------------
-// Random draws (wave-uniform).
-// ---------------------------------------------------------------------------------------
-__device__ __forceinline__ void philox_round(uint32_t (&c)[4], const uint32_t (&k)[2]) {
-    const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
-    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
-    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k[0];
-    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k[1];
-    c[0] = n0;
-    c[1] = (uint32_t)p1;
-    c[2] = n2;
-    c[3] = (uint32_t)p0;
-}
-
-__device__ void philox4x32_10(uint32_t (&c)[4], uint32_t k0, uint32_t k1) {
-    uint32_t k[2] = {k0, k1};
-#pragma unroll
-    for (int i = 0; i < 10; i++) {
-        philox_round(c, k);
-        k[0] += 0x9E3779B9u;
-        k[1] += 0xBB67AE85u;
-    }
-}
-
-// Wave-uniform scalars: every decision of the step loop is forced through readfirstlane, so the
-// lanes can never disagree on the control flow (and the values live in SGPRs).
-__device__ __forceinline__ int uni(int v) { return (int)__builtin_amdgcn_readfirstlane((uint32_t)v); }
-__device__ __forceinline__ int64_t uni64(int64_t v) {
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
-    return (int64_t)(((uint64_t)hi << 32) | lo);
-}
-__device__ __forceinline__ double uni(double v) {
-    return __longlong_as_double((long long)uni64((int64_t)__double_as_longlong(v)));
-}
-
-// The draw source: a replay tape (read straight from HBM, one item per draw, broadcast to the
-// wave) or Philox4x32-10.  Plain scalar members only: nothing of it lives in per-lane scratch.
-struct Rng {
-    const double *tape;  // this chain's tape, or null (Philox)
-    int64_t pos, len;    // tape cursor / length
-    uint32_t key0, key1;
-    uint64_t chain, ctr; // Philox stream (global chain id) and counter (one block per uniform)
-    int bad;             // tape exhausted
-
-    __device__ double tape_item() {
-        if (pos >= len) {
-            bad = 1;
-            return 0.0;
-        }
-        const double v = tape[pos];
-        pos = uni64(pos + 1);
-        return uni(v);
-    }
-    __device__ double uniform53() {  // [0, 1) with 53 random bits, one Philox block per call
-        uint32_t c[4] = {(uint32_t)ctr, (uint32_t)(ctr >> 32), (uint32_t)chain,
-                         (uint32_t)(chain >> 32)};
-        philox4x32_10(c, key0, key1);
-        ctr++;
-        const uint64_t bits = ((uint64_t)c[0] << 32) | c[1];
-        return uni((double)(bits >> 11) * 0x1p-53);
-    }
-    // a real in [0, 1): python random.random() / the acceptance and connected-step uniforms
-    __device__ double real() { return tape ? tape_item() : uniform53(); }
-    // an index in [0, n): np.random.choice(range(n)) / random.choice(seq) -> seq[k]
-    __device__ int below(int n) {
-        if (tape) return uni((int)tape_item());
-        return uni(min((int)(uniform53() * (double)n), n - 1));
-    }
-    __device__ int op(const double *cdf, int nops) {
-        if (tape) return uni((int)tape_item());
-        const double u = uniform53();  // numpy choice(p): first cdf entry > u
-        int i = 0;
-        while (i < nops - 1 && !(u < cdf[i])) i++;
-        return uni(i);
-    }
-    // random.sample(population, 2): two distinct values in draw order (pop == null: 0..n-1)
-    __device__ void pair(const int *pop, int n, int &a, int &b) {
-        if (tape) {
-            a = uni((int)tape_item());
-            b = uni((int)tape_item());
-            return;
-        }
-        const int i = below(n);
-        int j = below(n - 1);
-        if (j >= i) j++;
-        a = uni(pop ? pop[i] : i);
-        b = uni(pop ? pop[j] : j);
-    }
-    __device__ double normal() {  // Box-Muller (Philox mode only)
-        const double u1 = 1.0 - uniform53();  // (0, 1]
-        const double u2 = uniform53();
-        // cos(2 pi u2) as cospi(2 u2): no large-argument reduction (u2 in [0, 1))
-        return sqrt(-2.0 * log(u1)) * cospi(2.0 * u2);
-    }
-    // Marsaglia-Tsang, alpha >= 1.  Each round accepts with probability > 0.95 (alpha >= 1);
-    // the loop is bounded at 64 rounds (probability of reaching it < 1e-80).
-    __device__ double gamma(double alpha) {
-        const double d = alpha - 1.0 / 3.0, c = 1.0 / sqrt(9.0 * d);
-        double r = d;
-        for (int it = 0; it < 64; it++) {
-            const double x = normal();
-            double v = 1.0 + c * x;
-            if (v <= 0.0) continue;
-            v = v * v * v;
-            const double u = uniform53();
-            if (u < 1.0 - 0.0331 * (x * x) * (x * x) ||
-                log(u) < 0.5 * x * x + d * (1.0 - v + log(v))) {
-                r = d * v;
-                break;
-            }
-        }
-        return uni(r);
-    }
-    // np.random.dirichlet(alpha) for 2 components
-    __device__ void dirichlet2(double a0, double a1, double &x0, double &x1) {
-        if (tape) {
-            x0 = tape_item();
-            x1 = tape_item();
-            return;
-        }
-        const double g0 = gamma(a0), g1 = gamma(a1);
-        const double s = g0 + g1;
-        x0 = g0 / s;
-        x1 = g1 / s;
-    }
-};
-
-// scipy.stats.dirichlet._logpdf for 2 components:
-//   -(sum gammaln(a) - gammaln(sum a)) + sum xlogy(a - 1, x)
-__device__ __forceinline__ double dirichlet_logpdf2(double x0, double x1, double a0, double a1) {
-    const double lnB = (lgamma(a0) + lgamma(a1)) - lgamma(a0 + a1);
-    const double t0 = (a0 - 1.0) == 0.0 ? 0.0 : (a0 - 1.0) * log(x0);
-    const double t1 = (a1 - 1.0) == 0.0 ? 0.0 : (a1 - 1.0) * log(x1);
-    return -lnB + (t0 + t1);
-}
-
-// dirichlet_proposal on a pair w (sums to 1): new pair, log q, log q_back
-__device__ __forceinline__ void dirichlet_proposal2(Rng &rng, double w0, double w1, double prec, double &n0,
-                                    double &n1, double &log_q, double &log_q_back) {
-    const double a0 = 1.0 + prec * w0, a1 = 1.0 + prec * w1;
-    rng.dirichlet2(a0, a1, n0, n1);
-    const double q = exp(dirichlet_logpdf2(n0, n1, a0, a1));
-    const double b0 = 1.0 + prec * n0, b1 = 1.0 + prec * n1;
-    const double qb = exp(dirichlet_logpdf2(w0, w1, b0, b1));
-    log_q = uni(log(q));
-    log_q_back = uni(log(qb));
-}
-
-// scipy.special.xlogy(a, x): 0 where a == 0, else a * log(x)
-__device__ __forceinline__ double xlogy(double a, double x) { return a == 0.0 ? 0.0 : a * log(x); }
-
-// Change of the zone-size prior (ZoneSizePrior, model.py:932-971) when one zone goes from size
-// s to s1 = s +- 1: 'uniform' is -sum log C(N, size) (log_binom, util.py:1202-1217), and
-// C(N, k+1) / C(N, k) = (N-k) / (k+1), so the change is one log of that ratio; 'quadratic' is
-// -sum log(size^2).
-__device__ __forceinline__ double size_prior_delta(int kind, int N, int s, int s1) {
-    if (kind == 1) {
-        return s1 > s ? -log((double)(N - s) / (double)(s + 1))   // grow
-                      : -log((double)s / (double)(N - s + 1));    // shrink
-    }
-    if (kind == 2) return log((double)s * (double)s) - log((double)s1 * (double)s1);
-    return 0.0;
-}
-
-// The reference cell for one (site, feature): normalize_weights (model.py:436-452) then
-// (n0*l0 + n1*l1) + n2*l2 with NA -> every lh 1 and absent components -> lh 0.
-template <int C>
-__device__ __forceinline__ double cell(const double (&w)[3], bool hz, bool hf, bool na, double l0,
-                                       double l1, double l2) {
-    const double w0 = w[0] * 1.0, w1 = w[1] * (hz ? 1.0 : 0.0);
-    double sum = w0 + w1, w2 = 0.0;
-    if (C == 3) {
-        w2 = w[2] * (hf ? 1.0 : 0.0);
-        sum = sum + w2;
-    }
-    const double L0 = na ? 1.0 : l0;
-    const double L1 = na ? 1.0 : (hz ? l1 : 0.0);
-    double v = (w0 / sum) * L0 + (w1 / sum) * L1;
-    if (C == 3) v = v + (w2 / sum) * (na ? 1.0 : (hf ? l2 : 0.0));
-    return v;
-}
-
-struct Chain {
-    // LDS
-    uint8_t *zos;       // [N] zone of site
-    uint16_t *nb;       // [N] neighbour stamps
-    int *zsize;         // [Z]
-    double *col;        // staged parameter column (old values)
-    uint16_t stamp;
-    int occupied;       // sites in any zone
-};
-
-}  // namespace
-
-struct MhArgs {
-    int N, F, S, Z, Fam, C, FamC, Np, xs8;
-    int n_steps, nops, min_size, warmup;
-    double op_cdf[8];
-    double prec[4];
-    const uint8_t *obs_fm;      // [F][Np] by position
-    const uint8_t *famc;        // [Np] by position
-    const int *perm;            // [Np] site of position
-    const uint8_t *obs_sm;      // [N][F] x by site (S = NA)
-    const uint8_t *fam_site;    // [N] family class by site
-    const int *adj_ptr, *adj_idx;
-    int nnz;
-    const int *app_list;        // [F][S] applicable states of each feature (ascending)
-    const int *app_cnt;         // [F]
-    const double *alpha_g;      // [F][S] 'counts' prior on p_global, or null (sbz_set_priors)
-    const double *alpha_f;      // [Fam][F][S] 'counts' prior on p_families, or null
-    int size_prior;             // 0 none, 1 uniform, 2 quadratic
-    sbz_chains ch;
-};
 
 namespace {
 
@@ -317,7 +46,7 @@ __global__ __launch_bounds__(WAVE) void mh_kernel(MhArgs a) {
     int *zsize = reinterpret_cast<int *>(col + ((ncol + 1) & ~1));  // [Z]
     uint16_t *nb = reinterpret_cast<uint16_t *>(zsize + ((Z + 1) & ~1));  // [N]
     uint8_t *zos = reinterpret_cast<uint8_t *>(nb + ((N + 1) & ~1));      // [N]
-    int *stat = reinterpret_cast<int *>(zos + ((N + 3) & ~3));               // [16] proposed | accepted
+    int *stat = reinterpret_cast<int *>(zos + ((N + 3) & ~3));  // [MH_STAT_INTS] proposed | accepted
 
     uint8_t *gzos = ch.zone_of_site + (size_t)b * N;
     double *w = ch.w + (size_t)b * F * C;
@@ -330,7 +59,7 @@ __global__ __launch_bounds__(WAVE) void mh_kernel(MhArgs a) {
 
     // load the zone assignment; sizes
     for (int z = lane; z < Z; z += WAVE) zsize[z] = 0;
-    if (lane < 16) stat[lane] = 0;
+    if (lane < MH_STAT_INTS) stat[lane] = 0;
     for (int s = lane; s < N; s += WAVE) nb[s] = 0;
     wsync();
     int occ = 0;
@@ -690,7 +419,7 @@ __global__ __launch_bounds__(WAVE) void mh_kernel(MhArgs a) {
         }
         if (lane == 0) stat[op]++;
         if (accept) {
-            if (lane == 0) stat[8 + op]++;
+            if (lane == 0) stat[SBZ_N_OPS + op]++;
             ll = ll + delta;
             prior = prior + dprior;
             wsync();
@@ -730,11 +459,11 @@ __global__ __launch_bounds__(WAVE) void mh_kernel(MhArgs a) {
         if (ch.prior) ch.prior[b] = prior;
         if (ch.tape_pos) ch.tape_pos[b] = rng.pos;
         if (ch.counter) ch.counter[b] = rng.ctr;
-        if (ch.accepted)
-            for (int i = 0; i < 7; i++) ch.accepted[(size_t)b * 8 + i] += stat[8 + i];
-        if (ch.proposed)
-            for (int i = 0; i < 7; i++) ch.proposed[(size_t)b * 8 + i] += stat[i];
         if (ch.status) ch.status[b] = broken ? 2 : (rng.bad ? 1 : 0);
+    }
+    if (lane < SBZ_N_OPS) {  // per-operator counters, one lane each
+        if (ch.accepted) ch.accepted[(size_t)b * SBZ_N_OPS + lane] += stat[SBZ_N_OPS + lane];
+        if (ch.proposed) ch.proposed[(size_t)b * SBZ_N_OPS + lane] += stat[lane];
     }
     {
         const uint64_t bad = __ballot(err != 0);
@@ -751,15 +480,15 @@ size_t mh_lds_bytes(const sbz_dims &d, int C) {
     const size_t Fam = C == 3 ? (size_t)d.n_families : 0;
     const size_t ncol = (1 + (size_t)d.n_zones + Fam) * d.n_states + C;
     return ((ncol + 1) & ~(size_t)1) * 8 + (((size_t)d.n_zones + 1) & ~(size_t)1) * 4 +
-           (((size_t)d.n_sites + 1) & ~(size_t)1) * 2 + (((size_t)d.n_sites + 3) & ~(size_t)3) + 16 * 4;
+           (((size_t)d.n_sites + 1) & ~(size_t)1) * 2 + (((size_t)d.n_sites + 3) & ~(size_t)3) +
+           MH_STAT_INTS * 4;
 }
 
 int launch_mh(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg, const sbz_chains *chains) {
     const sbz_dims &d = ctx->d;
     if (!ctx->d_adj_ptr) return fail(ctx, SBZ_ESTATE, "sbz_set_network must be called before sbz_mh_run_device");
     if (B <= 0 || n_steps <= 0) return SBZ_OK;
-    const size_t lds = mh_lds_bytes(d, ctx->C);
-    if (lds > 64 * 1024) return fail(ctx, SBZ_EINVAL, "sampler state exceeds 64 KiB of LDS (too many sites)");
+    const bool src = cfg->sample_source != 0;
     MhArgs a{};
     a.N = d.n_sites;
     a.F = d.n_features;
@@ -773,23 +502,39 @@ int launch_mh(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg, const 
     a.n_steps = n_steps;
     a.min_size = cfg->min_size;
     a.warmup = cfg->warmup;
+    // operators of the mode: zone moves + alter_* (mixture) or + Gibbs operators (source mode)
+    bool allowed[SBZ_N_OPS] = {};
+    allowed[SHRINK] = allowed[GROW] = allowed[SWAP] = true;
+    if (src) {
+        for (int i = G_SOURCES; i <= G_P_FAMILIES; i++) allowed[i] = true;
+    } else {
+        for (int i = WEIGHTS; i <= P_FAMILIES; i++) allowed[i] = true;
+    }
     double tot = 0.0;
-    for (int i = 0; i < 7; i++) {
-        if (cfg->op_prob[i] < 0.0) return fail(ctx, SBZ_EINVAL, "negative operator probability");
-        tot += cfg->op_prob[i];
+    int last = -1;
+    for (int i = 0; i < SBZ_N_OPS; i++) {
+        const double p = cfg->op_prob[i];
+        if (p < 0.0 || std::isnan(p)) return fail(ctx, SBZ_EINVAL, "negative operator probability");
+        if (p > 0.0 && !allowed[i])
+            return fail(ctx, SBZ_EINVAL, std::string("operator ") + std::to_string(i) +
+                                             (i == 7 ? " (gibbsish_sample_zones) is not supported"
+                                                     : " is not available in this mode (sample_source)"));
+        if (p > 0.0) last = i;
+        tot += p;
     }
     if (!(tot > 0.0)) return fail(ctx, SBZ_EINVAL, "operator probabilities sum to 0");
-    if (cfg->op_prob[7] != 0.0) return fail(ctx, SBZ_EINVAL, "gibbsish_sample_zones is not supported (weight must be 0)");
-    if (d.n_zones == 0 && (cfg->op_prob[0] + cfg->op_prob[1] + cfg->op_prob[2] + cfg->op_prob[5]) > 0)
-        return fail(ctx, SBZ_EINVAL, "zone operators need n_zones > 0");
-    if (ctx->C == 2 && cfg->op_prob[6] > 0) return fail(ctx, SBZ_EINVAL, "alter_p_families needs inheritance");
+    const double zone_ops = cfg->op_prob[SHRINK] + cfg->op_prob[GROW] + cfg->op_prob[SWAP] +
+                            cfg->op_prob[P_ZONES] + cfg->op_prob[G_P_ZONES];
+    if (d.n_zones == 0 && zone_ops > 0) return fail(ctx, SBZ_EINVAL, "zone operators need n_zones > 0");
+    if ((ctx->C == 2 || d.n_families == 0) && (cfg->op_prob[P_FAMILIES] + cfg->op_prob[G_P_FAMILIES]) > 0)
+        return fail(ctx, SBZ_EINVAL, "family operators need inheritance with families");
     double acc = 0.0;
-    a.nops = 7;
-    for (int i = 0; i < 7; i++) {
+    a.nops = last + 1;
+    for (int i = 0; i < a.nops; i++) {
         acc += cfg->op_prob[i] / tot;
         a.op_cdf[i] = acc;
     }
-    a.op_cdf[6] = 1.0;
+    a.op_cdf[a.nops - 1] = 1.0;
     for (int i = 0; i < 4; i++) a.prec[i] = cfg->precision[i];
     a.obs_fm = ctx->d_obs_fm;
     a.famc = ctx->d_famc;
@@ -804,13 +549,22 @@ int launch_mh(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg, const 
     a.alpha_g = ctx->d_alpha_g;
     a.alpha_f = ctx->C == 3 ? ctx->d_alpha_f : nullptr;
     a.size_prior = ctx->size_prior;
+    a.gc_g = ctx->d_gc_g;
+    a.gc_f = ctx->C == 3 ? ctx->d_gc_f : nullptr;
     a.ch = *chains;
     if (!a.ch.zone_of_site || !a.ch.w || !a.ch.p_global || !a.ch.ll || !a.ch.max_size ||
         !a.ch.p_grow_connected || (d.n_zones > 0 && !a.ch.p_zones) ||
-        (ctx->C == 3 && d.n_families > 0 && !a.ch.p_fam))
+        (ctx->C == 3 && d.n_families > 0 && !a.ch.p_fam) || (src && !a.ch.source))
         return fail(ctx, SBZ_EINVAL, "null chain-state pointer");
+    if (a.ch.alias_pending &&
+        (!src || !a.ch.alias_p_global || (d.n_zones > 0 && !a.ch.alias_p_zones) ||
+         (ctx->C == 3 && d.n_families > 0 && !a.ch.alias_p_fam)))
+        return fail(ctx, SBZ_EINVAL, "alias_pending needs sample_source and the alias_p_* buffers");
     if (a.ch.tape && (!a.ch.tape_pos || !a.ch.tape_len))
         return fail(ctx, SBZ_EINVAL, "tape mode needs tape_pos and tape_len");
+    if (src) return launch_mh_source(ctx, B, a);
+    const size_t lds = mh_lds_bytes(d, ctx->C);
+    if (lds > 64 * 1024) return fail(ctx, SBZ_EINVAL, "sampler state exceeds 64 KiB of LDS (too many sites)");
     if (ctx->C == 3) mh_kernel<3><<<B, WAVE, lds, ctx->stream>>>(a);
     else mh_kernel<2><<<B, WAVE, lds, ctx->stream>>>(a);
     hipError_t e = hipGetLastError();

@@ -1,0 +1,663 @@
+// sbz_mh_src.hip — the MH sampler with SAMPLE_SOURCE = true on CDNA4 (gfx950).
+//
+// MCMCGenerative.step (sbayes/sampling/mcmc_generative.py:282-351) with the operators the
+// reference uses when every observation carries its mixture component ("source",
+// mcmc_setup.py:80-87, zone_sampling.py:180-406):
+//   shrink_zone / grow_zone / swap_zone with source resampling (:704-933; warm-up :1328-1574):
+//       log q_back += sum log posterior[current source] (current sample), then every source is
+//       redrawn from the new sample's posterior and log q += sum log posterior[new source]
+//       (gibbs_sample_sources(as_gibbs=False), :180-220).  ZoneMCMCWarmup passes as_gibbs=True
+//       whatever it is given (:1293-1296), so its zone moves carry log q = -inf: accepted.
+//   gibbs_sample_sources   (:180-215)  every source redrawn (sample_categorical,
+//                                      preprocessing.py:321-348)
+//   gibbs_sample_weights   (:222-331)  Dirichlet(1 + source counts) per feature; with inheritance
+//                                      a Beta draw for one weight ratio (the per-feature accept
+//                                      draw is made and overridden, :325-327: always the new ones)
+//   gibbs_sample_p_global  (:334-357)  40 % of the features, Dirichlet(prior counts + counts)
+//   gibbs_sample_p_zones   (:359-379)  one zone, every feature, Dirichlet(1 + counts)
+//   gibbs_sample_p_families(:381-406)  one family, 40 % of the features
+// The Gibbs operators return Q_GIBBS (log q = -inf): always accepted.
+//
+// One wave runs one chain.  The chain's sources (N x F bytes, current and candidate), zone
+// assignment and counters live in LDS for the whole launch; every operator is a few
+// lane-parallel passes over the N*F observations (per observation: the normalised weights and
+// component likelihoods in the reference's operation order, the posterior, the categorical draw,
+// the source-branch log-likelihood log(w_src * lh_src), model.py:177-184).  Draws come from the
+// replay tape (the reference's own decisions) or from Philox: uniform decisions from the wave's
+// stream, per-observation / per-feature draws from per-lane streams.
+#include <cmath>
+#include <cstdint>
+
+#include "sbz_mh_common.h"
+
+namespace sbz {
+
+namespace {
+
+// Per-lane Philox stream: block (j, base, chain lo, chain hi ^ (lane + 1) << 24), key = seed.
+// `base` is the wave's counter when the phase started (the wave then advances it by one), j
+// counts the lane's draws in the phase.
+struct LaneRng {
+    uint32_t k0, k1, base, c2, c3, j;
+    __device__ void init(const Rng &r, int lane) {
+        k0 = r.key0;
+        k1 = r.key1;
+        base = (uint32_t)r.ctr;
+        c2 = (uint32_t)r.chain;
+        c3 = (uint32_t)(r.chain >> 32) ^ ((uint32_t)(lane + 1) << 24);
+        j = 0;
+    }
+    __device__ double u() {
+        uint32_t c[4] = {j++, base, c2, c3};
+        philox4x32_10(c, k0, k1);
+        const uint64_t bits = ((uint64_t)c[0] << 32) | c[1];
+        return (double)(bits >> 11) * 0x1p-53;
+    }
+    __device__ double normal() {
+        const double u1 = 1.0 - u();
+        const double u2 = u();
+        return sqrt(-2.0 * log(u1)) * cospi(2.0 * u2);
+    }
+    // Marsaglia-Tsang (alpha >= 1; boosted by u^(1/alpha) below 1), at most 64 rounds
+    __device__ double gamma(double alpha) {
+        const double boost = alpha < 1.0 ? pow(u(), 1.0 / alpha) : 1.0;
+        const double a = alpha < 1.0 ? alpha + 1.0 : alpha;
+        const double d = a - 1.0 / 3.0, c = 1.0 / sqrt(9.0 * d);
+        double r = d;
+        for (int it = 0; it < 64; it++) {
+            const double x = normal();
+            double v = 1.0 + c * x;
+            if (v <= 0.0) continue;
+            v = v * v * v;
+            const double w = u();
+            if (w < 1.0 - 0.0331 * (x * x) * (x * x) || log(w) < 0.5 * x * x + d * (1.0 - v + log(v))) {
+                r = d * v;
+                break;
+            }
+        }
+        return r * boost;
+    }
+};
+
+// The component likelihoods and normalised weights of observation (s, f) (update_component_
+// likelihoods model.py:230-249 with NA -> 1 for every component; normalize_weights :436-452).
+template <int C>
+__device__ __forceinline__ void obs_terms(const MhArgs &a, const double *w, const double *pg,
+                                          const double *pz, const double *pf, int s, int f, int zc,
+                                          int fc, double (&l)[3], double (&wn)[3]) {
+    const int S = a.S, F = a.F, Z = a.Z;
+    const int x = a.obs_sm[(size_t)s * F + f];
+    const bool na = x >= S;
+    const int xc = na ? 0 : x;
+    const bool hz = zc < Z;
+    const bool hf = (C == 3) && fc > 0;
+    const double w0 = ldp(w + (size_t)f * C) * 1.0;
+    const double w1 = ldp(w + (size_t)f * C + 1) * (hz ? 1.0 : 0.0);
+    double sum = w0 + w1, w2 = 0.0;
+    if (C == 3) {
+        w2 = ldp(w + (size_t)f * C + 2) * (hf ? 1.0 : 0.0);
+        sum = sum + w2;
+    }
+    wn[0] = w0 / sum;
+    wn[1] = w1 / sum;
+    wn[2] = C == 3 ? w2 / sum : 0.0;
+    l[0] = na ? 1.0 : ldp(pg + (size_t)f * S + xc);
+    l[1] = na ? 1.0 : (hz ? ldp(pz + ((size_t)zc * F + f) * S + xc) : 0.0);
+    l[2] = (C == 3) ? (na ? 1.0 : (hf ? ldp(pf + ((size_t)(fc - 1) * F + f) * S + xc) : 0.0)) : 0.0;
+}
+
+// normalize(lh * w) (zone_sampling.py:202), then sample_categorical: argmax(u < cumsum(p)), 0 if
+// no entry exceeds u (preprocessing.py:335-338).  Returns the component; p[] the posterior.
+template <int C>
+__device__ __forceinline__ int posterior_draw(const double (&l)[3], const double (&wn)[3], double u,
+                                              double (&p)[3]) {
+    const double x0 = l[0] * wn[0], x1 = l[1] * wn[1], x2 = C == 3 ? l[2] * wn[2] : 0.0;
+    double sum = x0 + x1;
+    if (C == 3) sum = sum + x2;
+    p[0] = x0 / sum;
+    p[1] = x1 / sum;
+    p[2] = C == 3 ? x2 / sum : 0.0;
+    const double c0 = p[0], c1 = c0 + p[1], c2 = c1 + p[2];
+    return u < c0 ? 0 : (u < c1 ? 1 : ((C == 3 && u < c2) ? 2 : 0));
+}
+
+}  // namespace
+
+size_t mh_src_lds_bytes(const sbz_dims &d, int C) {
+    const size_t N = d.n_sites, F = d.n_features, S = d.n_states, Z = d.n_zones;
+    const size_t cnt = F * (S > (size_t)C ? S : (size_t)C);
+    return cnt * 4 + ((Z + 1) & ~(size_t)1) * 4 + MH_STAT_INTS * 4 + ((N + 1) & ~(size_t)1) * 2 +
+           ((N * F + 15) & ~(size_t)15) * 2 + ((N + 15) & ~(size_t)15) + ((F + 15) & ~(size_t)15);
+}
+
+namespace {
+
+template <int C>
+__global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int lane = threadIdx.x;
+    const int b = blockIdx.x;
+    const int N = a.N, F = a.F, S = a.S, Z = a.Z, Fam = (C == 3) ? a.Fam : 0;
+    const int NF = N * F;
+    const sbz_chains &ch = a.ch;
+
+    // LDS carve-up (ints first, then u16, then bytes)
+    const int ncnt = F * (S > C ? S : C);
+    int *cnt = reinterpret_cast<int *>(lds);                          // [F][max(S, C)] counts
+    int *zsize = cnt + ncnt;                                          // [Z]
+    int *stat = zsize + ((Z + 1) & ~1);                               // [MH_STAT_INTS]
+    uint16_t *nb = reinterpret_cast<uint16_t *>(stat + MH_STAT_INTS);  // [N] neighbour stamps
+    uint8_t *src = reinterpret_cast<uint8_t *>(nb + ((N + 1) & ~1));   // [N][F] current sources
+    uint8_t *srcb = src + ((NF + 15) & ~15);                         // [N][F] candidate sources
+    uint8_t *zos = srcb + ((NF + 15) & ~15);                         // [N] zone of site
+    uint8_t *sub = zos + ((N + 15) & ~15);                           // [F] feature subset
+
+    uint8_t *gzos = ch.zone_of_site + (size_t)b * N;
+    uint8_t *gsrc = ch.source + (size_t)b * NF;
+    double *w = ch.w + (size_t)b * F * C;
+    double *pg = ch.p_global + (size_t)b * F * S;
+    double *pz = Z > 0 ? ch.p_zones + (size_t)b * Z * F * S : pg;
+    double *pf = (C == 3 && Fam > 0) ? ch.p_fam + (size_t)b * Fam * F * S : pg;
+    const int max_size = ch.max_size[b];
+    const double p_grow = ch.p_grow_connected[b];
+
+    for (int z = lane; z < Z; z += WAVE) zsize[z] = 0;
+    if (lane < MH_STAT_INTS) stat[lane] = 0;
+    for (int s = lane; s < N; s += WAVE) nb[s] = 0;
+    for (int c = lane; c < NF; c += WAVE) src[c] = gsrc[c];
+    wsync();
+    int occ = 0;
+    for (int s = lane; s < N; s += WAVE) {
+        const int z = gzos[s];
+        zos[s] = (uint8_t)z;
+        if (z < Z) {
+            atomicAdd(&zsize[z], 1);
+            occ++;
+        }
+    }
+    int occupied = uni(wave_sum_i(occ));
+    wsync();
+
+    Rng rng;
+    rng.tape = ch.tape ? ch.tape + (size_t)b * ch.tape_stride : nullptr;
+    rng.pos = ch.tape ? uni64(ch.tape_pos[b]) : 0;
+    rng.len = ch.tape ? uni64(ch.tape_len[b]) : 0;
+    rng.key0 = (uint32_t)ch.seed;
+    rng.key1 = (uint32_t)(ch.seed >> 32);
+    rng.chain = ch.chain_id0 + (uint64_t)b;
+    rng.ctr = ch.counter ? (uint64_t)uni64((int64_t)ch.counter[b]) : 0;
+    rng.bad = 0;
+
+    double ll = ch.ll[b];
+    double prior = ch.prior ? ch.prior[b] : 0.0;
+    int alias = ch.alias_pending ? uni(ch.alias_pending[b]) : 0;
+    int err = 0;
+    long long err_val = 0;
+    uint16_t stamp = 0;
+
+    // ---- zone-move helpers (as the SAMPLE_SOURCE = false kernel, sbz_mh.hip)
+    auto mark = [&](int z) {
+        stamp++;
+        if (stamp == 0) {
+            for (int s = lane; s < N; s += WAVE) nb[s] = 0;
+            wsync();
+            stamp = 1;
+        }
+        for (int s = lane; s < N; s += WAVE)
+            if (zos[s] == z)
+                for (int e = a.adj_ptr[s]; e < a.adj_ptr[s + 1]; e++)
+                    nb[MH_IDX(a.adj_idx[MH_IDX(e, a.nnz, 1)], N, 2)] = stamp;
+        wsync();
+    };
+    auto is_nb = [&](int s) { return nb[s] == stamp && zos[s] == NONE; };
+    enum { SEL_NB = 0, SEL_FREE = 1, SEL_ZONE = 2 };
+    auto sel = [&](int mode, int z, int s) -> bool {
+        const int zs = zos[s];
+        return mode == SEL_NB ? (nb[s] == stamp && zs == NONE) : (mode == SEL_FREE ? zs == NONE : zs == z);
+    };
+    auto count_sel = [&](int mode, int z) -> int {
+        int c = 0;
+        for (int s0 = 0; s0 < N; s0 += WAVE) {
+            const int s = s0 + lane;
+            const bool f = s < N ? sel(mode, z, min(s, N - 1)) : false;
+            c += __popcll(__ballot(f));
+        }
+        return uni(c);
+    };
+    auto kth_sel = [&](int mode, int z, int k) -> int {
+        int found = -1;
+        for (int s0 = 0; s0 < N; s0 += WAVE) {
+            const int s = s0 + lane;
+            const bool f = s < N ? sel(mode, z, min(s, N - 1)) : false;
+            const uint64_t m = __ballot(f);
+            const int n = __popcll(m);
+            if (found < 0 && k < n) {
+                const uint64_t hit = __ballot(f && lane_prefix(m) == k);
+                found = hit ? s0 + (int)__builtin_ctzll(hit) : -1;
+                k = -1;
+            } else if (found < 0) {
+                k -= n;
+            }
+        }
+        return uni(found);
+    };
+
+    // ---- passes over the N*F observations (cell c = s*F + f, C order)
+    // sum over observations of log posterior[src] for the current sample (zone_sampling.py:718-722)
+    auto pass_logq = [&]() -> double {
+        double acc = 0.0;
+        for (int c = lane; c < NF; c += WAVE) {
+            const int s = c / F, f = c - s * F;
+            double l[3], wn[3], p[3];
+            obs_terms<C>(a, w, pg, pz, pf, s, f, zos[s], C == 3 ? a.fam_site[s] : 0, l, wn);
+            posterior_draw<C>(l, wn, 2.0, p);
+            acc += log(p[src[c]]);
+        }
+        return uni(wave_sum(acc));
+    };
+    // log-likelihood of the current sample with sources `sv` (combine_lh source branch,
+    // model.py:177-184): sum log(w_src * lh_src), -inf if a selected weight is 0
+    auto pass_ll = [&](const uint8_t *sv) -> double {
+        double acc = 0.0;
+        int zero_w = 0;
+        for (int c = lane; c < NF; c += WAVE) {
+            const int s = c / F, f = c - s * F;
+            double l[3], wn[3];
+            obs_terms<C>(a, w, pg, pz, pf, s, f, zos[s], C == 3 ? a.fam_site[s] : 0, l, wn);
+            const int k = sv[c];
+            zero_w |= wn[k] == 0.0;
+            acc += log(wn[k] * l[k]);
+        }
+        const double v = uni(wave_sum(acc));
+        return __ballot(zero_w) ? -INFINITY : v;
+    };
+    // redraw every source from the current sample's posterior into srcb; returns log q (sum log
+    // posterior[new source]) and the new log-likelihood
+    auto pass_resample = [&](double &log_q_s, double &ll_new) {
+        LaneRng lr;
+        lr.init(rng, lane);
+        double acc_q = 0.0, acc_l = 0.0;
+        int zero_w = 0;
+        const int64_t pos0 = rng.pos;
+        const bool have = !rng.tape || pos0 + NF <= rng.len;
+        for (int c = lane; c < NF; c += WAVE) {
+            const int s = c / F, f = c - s * F;
+            double l[3], wn[3], p[3];
+            obs_terms<C>(a, w, pg, pz, pf, s, f, zos[s], C == 3 ? a.fam_site[s] : 0, l, wn);
+            const double u = rng.tape ? (have ? rng.tape[pos0 + c] : 0.0) : lr.u();
+            const int k = posterior_draw<C>(l, wn, u, p);
+            srcb[c] = (uint8_t)k;
+            acc_q += log(p[k]);
+            zero_w |= wn[k] == 0.0;
+            acc_l += log(wn[k] * l[k]);
+        }
+        if (rng.tape) {
+            if (!have) rng.bad = 1;
+            rng.pos = uni64(pos0 + NF);
+        } else {
+            rng.ctr++;
+        }
+        wsync();
+        log_q_s = uni(wave_sum(acc_q));
+        const double v = uni(wave_sum(acc_l));
+        ll_new = __ballot(zero_w) ? -INFINITY : v;
+    };
+    auto commit_sources = [&]() {
+        for (int c = lane; c < NF; c += WAVE) src[c] = srcb[c];
+        wsync();
+    };
+    // per-feature counts of sources / states into cnt
+    auto clear_cnt = [&]() {
+        for (int i = lane; i < ncnt; i += WAVE) cnt[i] = 0;
+        wsync();
+    };
+    // F uniforms -> sub[f] = u < fraction (np.random.random(n_features) < 0.4, :335, :383)
+    auto draw_subset = [&]() {
+        LaneRng lr;
+        lr.init(rng, lane);
+        const int64_t pos0 = rng.pos;
+        const bool have = !rng.tape || pos0 + F <= rng.len;
+        for (int f = lane; f < F; f += WAVE) {
+            const double u = rng.tape ? (have ? rng.tape[pos0 + f] : 1.0) : lr.u();
+            sub[f] = u < 0.4 ? 1 : 0;
+        }
+        if (rng.tape) {
+            if (!have) rng.bad = 1;
+            rng.pos = uni64(pos0 + F);
+        } else {
+            rng.ctr++;
+        }
+        wsync();
+    };
+    // p_row[idx] = np.random.dirichlet(alpha) over feature f's applicable states, alpha_x =
+    // base(x) + cnt[f][x]; the new values come from the tape (in idx order) or per-lane gammas.
+    // Returns the change of the 'counts' prior (xlogy(alpha_prior - 1, p) terms) if al != null.
+    auto redraw_row = [&](double *row, int f, const double *gc, double gc_default, const double *al) -> double {
+        const int n = a.app_cnt[f];
+        const int x = lane < n ? a.app_list[(size_t)f * S + lane] : 0;
+        double g = 0.0;
+        if (rng.tape) {
+            const int64_t pos0 = rng.pos;
+            const bool have = pos0 + n <= rng.len;
+            g = (lane < n && have) ? rng.tape[pos0 + lane] : 0.0;
+            if (!have) rng.bad = 1;
+            rng.pos = uni64(pos0 + n);
+        } else {
+            LaneRng lr;
+            lr.init(rng, lane);
+            const double alpha = (gc ? ldp(gc + (size_t)f * S + x) : gc_default) + (double)cnt[f * S + x];
+            g = lane < n ? lr.gamma(alpha) : 0.0;
+            rng.ctr++;
+            const double tot = uni(wave_sum(g));
+            g = g / tot;
+        }
+        double dp = 0.0;
+        if (lane < n) {
+            const double old = ldp(row + x);
+            stp(row + x, g);
+            if (al) {
+                const double am1 = ldp(al + (size_t)f * S + x) - 1.0;
+                dp = xlogy(am1, g) - xlogy(am1, old);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        return uni(wave_sum(dp));
+    };
+
+    bool broken = false;
+    for (int step = 0; step < a.n_steps; step++) {
+        if (rng.bad || broken || err) break;
+        const int op = rng.op(a.op_cdf, a.nops);
+        const bool zone_op = op <= SWAP;
+        if (!(zone_op || (op >= G_SOURCES && op <= G_P_FAMILIES)) || (zone_op && Z == 0) ||
+            (op == G_P_ZONES && Z == 0) || (op == G_P_FAMILIES && (C == 2 || Fam == 0))) {
+            broken = true;
+            break;
+        }
+        double log_q = -INFINITY, log_q_back = 0.0;  // Gibbs operators: Q_GIBBS, Q_BACK_GIBBS
+        double dprior = 0.0, ll_new = ll;
+        int sa = -1, zoa = NONE, zna = NONE, sb = -1;
+        bool new_sources = false;
+
+        if (zone_op) {
+            // ---- zone move with source resampling
+            const double log_q_back_s = pass_logq();
+            log_q = 0.0;
+            log_q_back = -INFINITY;
+            const int n_free = N - occupied;
+            const int z = rng.below(Z);
+            if (z < 0 || z >= Z) {
+                broken = true;
+                break;
+            }
+            const int size = uni(zsize[z]);
+            double q = 0.0, q_back = 0.0;
+            if (op == GROW || op == SWAP) {
+                if (op == SWAP || size < max_size) {
+                    mark(z);
+                    const bool connected = rng.real() < p_grow;
+                    const int n_nb = count_sel(SEL_NB, 0);
+                    const int cnt_c = connected ? n_nb : n_free;
+                    if (cnt_c > 0) {
+                        const int site = kth_sel(connected ? SEL_NB : SEL_FREE, 0, rng.below(cnt_c));
+                        int site_rm = -2;
+                        if (op == SWAP) site_rm = kth_sel(SEL_ZONE, z, rng.below(size));
+                        if (site < 0 || site_rm == -1) {
+                            broken = true;
+                            break;
+                        }
+                        q = (1.0 - p_grow) * (1.0 / (double)n_free);
+                        if (is_nb(site)) q += p_grow * (1.0 / (double)n_nb);
+                        if (op == GROW) {
+                            q_back = 1.0 / (double)(size + 1);
+                            dprior = uni(size_prior_delta(a.size_prior, N, size, size + 1));
+                        } else {
+                            q_back = (1.0 - p_grow) * (1.0 / (double)n_free);
+                            if (is_nb(site_rm)) q_back += p_grow * (1.0 / (double)n_nb);
+                            sb = site_rm;
+                        }
+                        sa = site;
+                        zoa = NONE;
+                        zna = z;
+                    }
+                }
+            } else if (size > a.min_size) {  // SHRINK
+                const int site = kth_sel(SEL_ZONE, z, rng.below(size));
+                if (site < 0) {
+                    broken = true;
+                    break;
+                }
+                wsync();
+                if (lane == 0) zos[site] = NONE;
+                wsync();
+                mark(z);
+                const int n_back = count_sel(SEL_NB, 0);
+                q_back = (1.0 - p_grow) * (1.0 / (double)(n_free + 1));
+                if (is_nb(site)) q_back += p_grow * (1.0 / (double)n_back);
+                if (a.warmup) q_back = 1.0 / (double)(size + 1);  // zone_sampling.py:1561
+                wsync();
+                if (lane == 0) zos[site] = (uint8_t)z;
+                wsync();
+                q = 1.0 / (double)size;
+                dprior = uni(size_prior_delta(a.size_prior, N, size, size - 1));
+                sa = site;
+                zoa = z;
+                zna = NONE;
+            }
+            if (sa >= 0) {
+                // the new zones (tentatively, undone on rejection), then every source redrawn
+                wsync();
+                if (lane == 0) {
+                    zos[sa] = (uint8_t)zna;
+                    if (sb >= 0) zos[sb] = NONE;
+                }
+                wsync();
+                double log_q_s;
+                pass_resample(log_q_s, ll_new);
+                new_sources = true;
+                log_q = a.warmup ? -INFINITY : uni(log(q) + log_q_s);
+                log_q_back = uni(log(q_back) + log_q_back_s);
+            }
+        } else if (op == G_SOURCES) {
+            double log_q_s;
+            pass_resample(log_q_s, ll_new);
+            new_sources = true;
+        } else if (op == G_WEIGHTS) {
+            // source counts per feature over the sites of a zone (or of a family)
+            const int fixed = C == 3 ? rng.below(2) : 0;  // random.choice(['inheritance', 'contact'])
+            if (fixed < 0 || fixed > 1) {
+                broken = true;
+                break;
+            }
+            clear_cnt();
+            for (int c = lane; c < NF; c += WAVE) {
+                const int s = c / F, f = c - s * F;
+                const bool in = (C == 2 || fixed == 0) ? zos[s] < Z : a.fam_site[s] > 0;
+                if (in) atomicAdd(&cnt[f * C + src[c]], 1);
+            }
+            wsync();
+            LaneRng lr;
+            lr.init(rng, lane);
+            const int64_t pos0 = rng.pos;
+            const int64_t need = C == 2 ? 2LL * F : 2LL * F;  // C == 3: F beta draws + F uniforms
+            const bool have = !rng.tape || pos0 + need <= rng.len;
+            for (int f = lane; f < F; f += WAVE) {
+                double *wf = w + (size_t)f * C;
+                if (C == 2) {
+                    double d0, d1;
+                    if (rng.tape) {
+                        d0 = have ? rng.tape[pos0 + 2 * f] : 0.5;
+                        d1 = have ? rng.tape[pos0 + 2 * f + 1] : 0.5;
+                    } else {
+                        const double g0 = lr.gamma(1.0 + cnt[f * C]), g1 = lr.gamma(1.0 + cnt[f * C + 1]);
+                        d0 = g0 / (g0 + g1);
+                        d1 = g1 / (g0 + g1);
+                    }
+                    stp(wf, d0);
+                    stp(wf + 1, d1);
+                } else {
+                    const int cu = cnt[f * C], cx = cnt[f * C + (fixed == 0 ? 1 : 2)];
+                    double r;
+                    if (rng.tape) {
+                        r = have ? rng.tape[pos0 + f] : 0.5;
+                    } else {
+                        const double ga = lr.gamma(1.0 + cx), gb = lr.gamma(1.0 + cu);
+                        r = ga / (ga + gb);
+                    }
+                    double w0 = ldp(wf), w1 = ldp(wf + 1), w2 = ldp(wf + 2);
+                    if (fixed == 0) w1 = r * w0 / (1.0 - r);
+                    else w2 = r * w0 / (1.0 - r);
+                    const double sum = (w0 + w1) + w2;
+                    stp(wf, w0 / sum);
+                    stp(wf + 1, w1 / sum);
+                    stp(wf + 2, w2 / sum);
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (rng.tape) {
+                if (!have) rng.bad = 1;
+                rng.pos = uni64(pos0 + need);
+            } else {
+                rng.ctr++;
+            }
+            wsync();
+            ll_new = pass_ll(src);
+        } else {
+            // ---- gibbs_sample_p_global / p_zones / p_families
+            int row = 0;
+            if (op == G_P_ZONES) row = rng.below(Z);        // np.random.randint(0, n_zones)
+            if (op == G_P_FAMILIES) row = rng.below(Fam);   // np.random.randint(0, n_families)
+            if (row < 0 || (op == G_P_ZONES && row >= Z) || (op == G_P_FAMILIES && row >= Fam)) {
+                broken = true;
+                break;
+            }
+            if (op == G_P_ZONES) {
+                for (int f = lane; f < F; f += WAVE) sub[f] = 1;
+                wsync();
+            } else {
+                draw_subset();
+            }
+            const int comp = op == G_P_GLOBAL ? 0 : (op == G_P_ZONES ? 1 : 2);
+            clear_cnt();
+            for (int c = lane; c < NF; c += WAVE) {
+                const int s = c / F, f = c - s * F;
+                const int x = a.obs_sm[c];
+                bool in = sub[f] && src[c] == comp && x < S;
+                if (comp == 1) in = in && zos[s] == row;
+                if (comp == 2) in = in && a.fam_site[s] == row + 1;
+                if (in) atomicAdd(&cnt[f * S + x], 1);
+            }
+            wsync();
+            double *base = comp == 0 ? pg : (comp == 1 ? pz + (size_t)row * F * S : pf + (size_t)row * F * S);
+            const double *gc = comp == 0 ? a.gc_g : (comp == 2 && a.gc_f ? a.gc_f + (size_t)row * F * S : nullptr);
+            const double *al = comp == 0 ? a.alpha_g : (comp == 2 && a.alpha_f ? a.alpha_f + (size_t)row * F * S : nullptr);
+            for (int f = 0; f < F; f++) {
+                if (!sub[f]) continue;
+                dprior += redraw_row(base + (size_t)f * S, f, gc, 1.0, al);
+            }
+            dprior = uni(dprior);
+            wsync();
+            ll_new = pass_ll(src);
+        }
+
+        // ---- metropolis_hastings_ratio (mcmc_generative.py:307-318)
+        bool accept;
+        if (log_q_back == -INFINITY) accept = false;
+        else if (log_q == -INFINITY) accept = true;
+        else accept = log(rng.real()) < ((ll_new - ll) * 1.0) - (log_q - log_q_back) + dprior;
+        if (lane == 0) stat[op]++;
+        if (accept) {
+            if (lane == 0) stat[SBZ_N_OPS + op]++;
+            ll = ll_new;
+            prior = prior + dprior;
+            if (new_sources) commit_sources();
+            if (sa >= 0) {
+                if (lane == 0) {
+                    if (zoa < Z) zsize[zoa]--;
+                    if (zna < Z) zsize[zna]++;
+                    if (sb >= 0) zsize[zna]--;
+                }
+                occupied += (zna < Z ? 1 : -1) + (sb >= 0 ? -1 : 0);
+                wsync();
+            }
+        } else if (sa >= 0) {
+            wsync();
+            if (lane == 0) {  // undo the tentative zone change
+                zos[sa] = (uint8_t)zoa;
+                if (sb >= 0) zos[sb] = (uint8_t)zna;
+            }
+            wsync();
+        }
+        if (alias && accept && op != G_SOURCES && op != G_P_GLOBAL && op != G_P_ZONES &&
+            op != G_P_FAMILIES) {
+            // this accept replaces the reference's Sample object: the arrays of the logged
+            // sample stop changing here (sbz.h, alias_pending)
+            const size_t fs = (size_t)F * S;
+            for (size_t k = lane; k < fs; k += WAVE) ch.alias_p_global[b * fs + k] = ldp(pg + k);
+            for (size_t k = lane; k < (size_t)Z * fs; k += WAVE)
+                ch.alias_p_zones[b * Z * fs + k] = ldp(pz + k);
+            if (C == 3)
+                for (size_t k = lane; k < (size_t)Fam * fs; k += WAVE)
+                    ch.alias_p_fam[b * Fam * fs + k] = ldp(pf + k);
+            alias = 0;
+        }
+        if (ch.trace_op && lane == 0) {
+            const size_t t = (size_t)b * a.n_steps + step;
+            ch.trace_op[t] = (int8_t)op;
+            ch.trace_accept[t] = accept ? 1 : 0;
+            ch.trace_ll[t] = ll;
+        }
+        if (ch.trace_zos) {
+            uint8_t *tz = ch.trace_zos + ((size_t)b * a.n_steps + step) * N;
+            for (int s = lane; s < N; s += WAVE) tz[s] = zos[s];
+        }
+    }
+
+    wsync();
+    for (int s = lane; s < N; s += WAVE) gzos[s] = zos[s];
+    for (int c = lane; c < NF; c += WAVE) gsrc[c] = src[c];
+    if (lane == 0) {
+        ch.ll[b] = ll;
+        if (ch.prior) ch.prior[b] = prior;
+        if (ch.alias_pending) ch.alias_pending[b] = alias;
+        if (ch.tape_pos) ch.tape_pos[b] = rng.pos;
+        if (ch.counter) ch.counter[b] = rng.ctr;
+        if (ch.status) ch.status[b] = broken ? 2 : (rng.bad ? 1 : 0);
+    }
+    if (lane < SBZ_N_OPS) {  // per-operator counters, one lane each
+        if (ch.accepted) ch.accepted[(size_t)b * SBZ_N_OPS + lane] += stat[SBZ_N_OPS + lane];
+        if (ch.proposed) ch.proposed[(size_t)b * SBZ_N_OPS + lane] += stat[lane];
+    }
+    {
+        const uint64_t bad = __ballot(err != 0);
+        if (bad) {
+            const int code = __shfl(err, (int)__builtin_ctzll(bad), 64);
+            if (lane == 0 && ch.status) ch.status[b] = 16 + code;
+        }
+    }
+}
+
+}  // namespace
+
+int launch_mh_source(sbz_ctx *ctx, int B, const MhArgs &a) {
+    const size_t lds = mh_src_lds_bytes(ctx->d, ctx->C);
+    if (lds > 160 * 1024)
+        return fail(ctx, SBZ_EINVAL, "SAMPLE_SOURCE sampler needs " + std::to_string(lds) +
+                                         " B of LDS per chain (> 160 KiB: too many sites x features)");
+    static bool configured = false;
+    if (!configured) {
+        for (const void *fn : {reinterpret_cast<const void *>(&mh_src_kernel<2>),
+                               reinterpret_cast<const void *>(&mh_src_kernel<3>)}) {
+            hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            if (e != hipSuccess) return hip_fail(ctx, e, "hipFuncSetAttribute(sampler LDS)");
+        }
+        configured = true;
+    }
+    if (ctx->C == 3) mh_src_kernel<3><<<B, WAVE, lds, ctx->stream>>>(a);
+    else mh_src_kernel<2><<<B, WAVE, lds, ctx->stream>>>(a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(ctx, e, "source-mode sampler launch");
+    return SBZ_OK;
+}
+
+}  // namespace sbz

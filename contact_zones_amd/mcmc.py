@@ -18,7 +18,9 @@ zones come from the same python ``random`` calls (``random.sample`` of the free-
 to the reference's; weights are uniform and p_* the smoothed MLE.  The MH draws themselves come
 from Philox4x32-10 keyed by (seed, global chain id) — results do not depend on the GPU count.
 
-Supported model (checked, NotImplementedError otherwise): SAMPLE_SOURCE = false; the priors of
+Supported model (checked, NotImplementedError otherwise): SAMPLE_SOURCE = false or true (the
+Gibbs operators of mcmc_setup.py:80-87 and source-resampling zone moves, sbz_mh_src.hip); the
+priors of
 contact_zones_amd/priors.py (zero / uniform terms, 'counts' on universal and inheritance,
 'uniform' / 'quadratic' zone size), read from the reference Model's Prior or given as
 ``priors=``.  MC3 (``mc3=True``) and ``sample_from_prior`` are not part of the batched path.
@@ -95,18 +97,26 @@ def adjacency_csr(adj_mat, n_sites):
     return a.indptr.astype(np.int32), a.indices.astype(np.int32)
 
 
-def check_model(model):
-    """The batched sampler implements SAMPLE_SOURCE = false (priors: contact_zones_amd/priors.py)."""
-    if getattr(model, "sample_source", False):
-        raise NotImplementedError("SAMPLE_SOURCE = true (source Gibbs sampling) is not supported "
-                                  "by the batched sampler")
+GIBBS_OPS = set(OPS[8:])  # the SAMPLE_SOURCE = true operators (mcmc_setup.py:80-87)
+ALTER_OPS = {"alter_weights", "alter_p_global", "alter_p_zones", "alter_p_families"}
+
+
+def check_model(model, operators=()):
+    """The operators must belong to the model's mode: the Gibbs operators need SAMPLE_SOURCE =
+    true; with sources, parameters move by Gibbs steps only (mcmc_setup.py:80-95)."""
+    source = bool(getattr(model, "sample_source", False))
+    ops = {k for k, v in dict(operators).items() if v} if operators else set()
+    if not source and ops & GIBBS_OPS:
+        raise ValueError(f"operators {sorted(ops & GIBBS_OPS)} need SAMPLE_SOURCE = true")
+    if source and ops & ALTER_OPS:
+        raise ValueError(f"operators {sorted(ops & ALTER_OPS)} are not used with SAMPLE_SOURCE = true")
 
 
 class InitialSamples:
     """generate_initial_sample (zone_sampling.py:935-1233) on the host, draw for draw."""
 
     def __init__(self, features, applicable_states, adj_indptr, adj_indices, families, n_zones,
-                 initial_size, inheritance, initial_sample, rng):
+                 initial_size, inheritance, initial_sample, rng, sample_source=False):
         self.features = features
         self.applicable_states = applicable_states
         self.adj_indptr, self.adj_indices = adj_indptr, adj_indices
@@ -116,6 +126,7 @@ class InitialSamples:
         self.inheritance = inheritance
         self.initial_sample = initial_sample if initial_sample is not None else Sample.empty_sample()
         self.rng = rng
+        self.sample_source = sample_source
         self.n_sites, self.n_features = features.shape[:2]
 
     def neighbours(self, zone, already_in_zone):
@@ -226,14 +237,27 @@ class InitialSamples:
         return p
 
     def __call__(self, c=0):
-        """generate_initial_sample (zone_sampling.py:1189-1233), SAMPLE_SOURCE = false."""
+        """generate_initial_sample (zone_sampling.py:1189-1233); with SAMPLE_SOURCE = true the
+        sources get one Gibbs draw from np.random (:1227-1231, contact_zones_amd/sources.py)."""
         zones = self.zones()
         weights = self.weights()
         p_global = self.p_global()
         p_zones = self.p_zones(zones)
         p_families = self.p_families() if self.inheritance else None
-        return Sample(zones=zones, weights=weights, p_global=p_global, p_zones=p_zones,
-                      p_families=p_families, chain=c)
+        sample = Sample(zones=zones, weights=weights, p_global=p_global, p_zones=p_zones,
+                        p_families=p_families, chain=c)
+        if self.sample_source:
+            from .sources import draw_sources, source_posterior
+            if not hasattr(self, "_obs"):
+                self._obs = packing.features_to_obs(self.features)
+                self._fam = packing.families_to_fam_of_site(
+                    self.families if self.inheritance and self.families.shape[0] else None, self.n_sites)
+            zos = packing.zones_to_zone_of_site(zones, self.n_sites)
+            post = source_posterior(self._obs, self._fam, zos, np.asarray(weights, np.float64),
+                                    np.asarray(p_global, np.float64)[0], p_zones, p_families,
+                                    self.inheritance)
+            sample.source = packing.index_to_source(draw_sources(post), 3 if self.inheritance else 2)
+        return sample
 
 
 def _dist():
@@ -256,13 +280,14 @@ class BatchedZoneMCMC:
                  initial_size, initial_sample=None, mc3=False, swap_period=None, chain_swaps=None,
                  sample_from_prior=False, show_screen_log=False, logger=None, *, seed=None,
                  rng=None, device=None, group=None, refresh_every_launch=True, priors=None,
-                 **kwargs):
+                 gibbs_counts=None, **kwargs):
         if mc3:
             raise NotImplementedError("MC3 chain swaps are not part of the batched sampler")
         if sample_from_prior:
             raise NotImplementedError("sample_from_prior is not supported by the batched sampler")
-        check_model(model)
+        check_model(model, operators)
         self.model, self.data = model, data
+        self.sample_source = bool(getattr(model, "sample_source", False))
         self.n_chains = int(n_chains)
         self.chain_idx = list(range(self.n_chains))
         self.rng = rng if rng is not None else _random_module  # the reference's `_random`
@@ -298,6 +323,14 @@ class BatchedZoneMCMC:
         # the prior terms of the MH ratio: from the reference Model's Prior (model.py:455-505)
         # unless given; unsupported prior types raise NotImplementedError
         self.priors = priors if priors is not None else PriorSpec.from_model(model, self.applicable_states)
+        # pseudo-counts of the source-mode Gibbs operators (prior.prior_p_global.counts,
+        # prior.prior_p_families.counts: zone_sampling.py:344, 394)
+        if gibbs_counts is None and self.sample_source:
+            pr = getattr(model, "prior", None)
+            cg = getattr(getattr(pr, "prior_p_global", None), "counts", None)
+            cf = getattr(getattr(pr, "prior_p_families", None), "counts", None) if self.inheritance else None
+            gibbs_counts = (cg, cf)
+        self.gibbs_counts = gibbs_counts
 
         self.statistics = {'sample_id': [], 'sample_likelihood': [], 'sample_prior': [],
                            'sample_zones': [], 'sample_weights': [], 'sample_p_global': [],
@@ -322,7 +355,7 @@ class BatchedZoneMCMC:
         self._init = InitialSamples(self.features, self.applicable_states, self.adj_indptr,
                                     self.adj_indices, self.families, self.n_zones,
                                     self.initial_size, self.inheritance, self.initial_sample,
-                                    self.rng)
+                                    self.rng, sample_source=self.sample_source)
 
     # ---- reference API ---------------------------------------------------------------
     def generate_initial_sample(self, c=0):
@@ -340,10 +373,11 @@ class BatchedZoneMCMC:
 
     def likelihood(self, sample, chain):
         """Full log-likelihood of `sample` on the GPU (MCMCGenerative.likelihood, :106-127)."""
-        zos, w, pg, pz, pf, _ = self._pack(sample)
+        zos, w, pg, pz, pf, src = self._pack(sample)
         eng = self._get_engine()
         return float(eng.loglik(zos[None], w[None], pg[None], pz[None],
-                                None if pf is None else pf[None])[0])
+                                None if pf is None else pf[None],
+                                None if src is None else src[None])[0])
 
     # ---- device plumbing ---------------------------------------------------------------
     def _get_engine(self):
@@ -361,7 +395,9 @@ class BatchedZoneMCMC:
                                             self.inheritance, device=dev)
             self._sampler = Sampler(self._engine, self.applicable_states, self.adj_indptr,
                                     self.adj_indices, self.p_operators, self.precision,
-                                    self.min_size, warmup=self.IS_WARMUP, priors=self.priors)
+                                    self.min_size, warmup=self.IS_WARMUP, priors=self.priors,
+                                    sample_source=self.sample_source,
+                                    gibbs_counts=self.gibbs_counts)
         return self._engine
 
     def _pack(self, s):
@@ -369,7 +405,9 @@ class BatchedZoneMCMC:
         pg = np.asarray(s.p_global, np.float64)
         pg = pg[0] if pg.ndim == 3 else pg
         pf = np.asarray(s.p_families, np.float64) if self.inheritance else None
-        return zos, np.asarray(s.weights, np.float64), pg, np.asarray(s.p_zones, np.float64), pf, None
+        src = (packing.source_to_index(s.source) if self.sample_source and s.source is not None
+               else None)
+        return zos, np.asarray(s.weights, np.float64), pg, np.asarray(s.p_zones, np.float64), pf, src
 
     def _unpack(self, st, i, c):
         """Chain i of this rank's device state -> Sample (host copies)."""
@@ -379,6 +417,8 @@ class BatchedZoneMCMC:
                       p_global=st.p_global[i].cpu().numpy()[None],
                       p_zones=st.p_zones[i].cpu().numpy(),
                       p_families=st.p_fam[i].cpu().numpy() if st.p_fam is not None else None,
+                      source=(packing.index_to_source(st.source[i].cpu().numpy(), self.n_sources)
+                              if st.source is not None else None),
                       chain=c)
 
     def _max_size_for(self, lo, hi):
@@ -405,10 +445,19 @@ class BatchedZoneMCMC:
         pf = stack(4) if self.inheritance else None
         prior0 = self.priors.log_prior(stack(0), stack(2), pf, self.applicable_states,
                                        self.n_zones, self.inheritance)
-        self._state = ChainState(eng, stack(0), stack(1), stack(2), stack(3), pf, prior=prior0)
+        self._state = ChainState(eng, stack(0), stack(1), stack(2), stack(3), pf, prior=prior0,
+                                 source=stack(5) if self.sample_source else None)
         self._acc0 = self._state.accepted.clone()
         self._prop0 = self._state.proposed.clone()
         self._tape_pos = None
+        self._alias = None
+        self._alias_logged = []  # logged samples whose p_* still alias chain 0's (source mode)
+        if self.sample_source and self.lo == 0 and self.hi > 0:
+            import torch
+            st = self._state
+            z = torch.zeros_like
+            self._alias = (torch.zeros(st.B, dtype=torch.int32, device=st.ll.device), z(st.p_global),
+                           z(st.p_zones), z(st.p_fam) if st.p_fam is not None else None)
         if self._tape is not None:
             import torch
             self._tape_pos = torch.zeros(self.hi - self.lo, dtype=torch.int64,
@@ -435,14 +484,30 @@ class BatchedZoneMCMC:
                       tape_pos=self._tape_pos)
         out = self._sampler.run(st, n, self._max_size_for(self.lo, self.hi),
                                 self._p_grow_for(self.lo, self.hi), seed=self._philox_seed,
-                                chain_id0=self.lo, **kw)
+                                chain_id0=self.lo, alias=self._alias, **kw)
         status = out["status"].cpu().numpy()
+        if self._alias_logged and int(self._alias[0][0].item()) == 0:
+            a = self._alias
+            self._resolve_alias(a[1][0], a[2][0], a[3][0] if a[3] is not None else None)
         if np.any(status != 0):
             bad = int(np.flatnonzero(status)[0])
             raise RuntimeError(f"sampler: chain {self.lo + bad} stopped with status {status[bad]}")
         if self.refresh_every_launch:
             st.refresh_ll()  # reset the incremental ll to a full evaluation
         self._sync_host_ll()
+
+    def _resolve_alias(self, pg, pz, pf):
+        """Give the logged samples still aliasing chain 0's arrays the values those arrays had
+        when the reference's Sample was replaced (sbz.h: alias_pending)."""
+        stt = self.statistics
+        pg, pz = pg.cpu().numpy(), pz.cpu().numpy()
+        pf = pf.cpu().numpy() if pf is not None else None
+        for k in self._alias_logged:
+            stt['sample_p_global'][k][0] = pg
+            stt['sample_p_zones'][k][...] = pz
+            if pf is not None:
+                stt['sample_p_families'][k][...] = pf
+        self._alias_logged = []
 
     def _operator_counts(self):
         from .parallel import all_reduce_sum
@@ -519,10 +584,19 @@ class BatchedZoneMCMC:
                     self._prior[self.chain_idx[0]] = self.prior(s0, self.chain_idx[0])
                     self.log_sample_statistics(s0, c=self.chain_idx[0],
                                                sample_id=int(i_step / steps_per_sample))
+                    if self._alias is not None:
+                        # the reference logs references to the Sample's arrays, which its Gibbs
+                        # operators keep changing in place (zone_sampling.py:333-400)
+                        self._alias_logged.append(len(self.statistics['sample_id']) - 1)
+                        self._alias[0][0] = 1
             if (i_step + 1) % 1000 == 0 and self.rank == 0:
                 self.print_screen_log(i_step + 1)
             if i_step % (n_steps - 1) == 0 and i_step != 0 and self.rank == 0:
                 self.log_last_sample(self._chain0_sample())
+        if self._alias_logged:  # still aliased at the end: the final arrays
+            st = self._state
+            self._resolve_alias(st.p_global[0], st.p_zones[0],
+                                st.p_fam[0] if st.p_fam is not None else None)
         t_end = time.time()
         self._count_operators()
         self.statistics['sampling_time'] = t_end - t_start
@@ -550,12 +624,15 @@ class BatchedZoneMCMC:
         if self.lo <= best < self.hi:
             s = self._unpack(self._state, best - self.lo, best)
             arrays = [s.zones, s.weights, s.p_global, s.p_zones] + \
-                     ([s.p_families] if self.inheritance else [])
+                     ([s.p_families] if self.inheritance else []) + \
+                     ([s.source] if self.sample_source else [])
         from .parallel import owner_of
         owner = owner_of(best, self.n_chains, self.world_size)
         arrays = broadcast_arrays(arrays, owner, self._group)
+        k = 4 + int(self.inheritance)
         return Sample(zones=arrays[0], weights=arrays[1], p_global=arrays[2], p_zones=arrays[3],
-                      p_families=arrays[4] if self.inheritance else None, chain=best)
+                      p_families=arrays[4] if self.inheritance else None,
+                      source=arrays[k] if self.sample_source else None, chain=best)
 
 
 class BatchedZoneMCMCWarmup(BatchedZoneMCMC):

@@ -7,8 +7,9 @@ with the ZoneMCMC / ZoneMCMCWarmup operators (sbayes/sampling/zone_sampling.py:4
 ``ChainState`` holds it.  Draws come from Philox (production) or from a replay tape of the
 reference's own decisions (parity tests).
 
-Supported model: SAMPLE_SOURCE = false; zero (uniform) priors, 'counts' priors on p_global /
-p_families and 'uniform' / 'quadratic' zone-size priors (contact_zones_amd/priors.py).  Operator names and their canonical order follow
+Supported models: SAMPLE_SOURCE = false (sbz_mh.hip) and true (sbz_mh_src.hip, ``sample_source=True``:
+Gibbs operators, source-resampling zone moves); zero (uniform) priors, 'counts' priors on
+p_global / p_families and 'uniform' / 'quadratic' zone-size priors (contact_zones_amd/priors.py).  Operator names and their canonical order follow
 ``include/sbz.h`` (sbz_op).
 """
 import ctypes
@@ -18,7 +19,11 @@ import numpy as np
 from ._lib import check, sbz_chains, sbz_mh_config
 
 OPS = ["shrink_zone", "grow_zone", "swap_zone", "alter_weights", "alter_p_global",
-       "alter_p_zones", "alter_p_families", "gibbsish_sample_zones"]
+       "alter_p_zones", "alter_p_families", "gibbsish_sample_zones",
+       # SAMPLE_SOURCE = true operators (mcmc_setup.py:80-87)
+       "gibbs_sample_sources", "gibbs_sample_weights", "gibbs_sample_p_global",
+       "gibbs_sample_p_zones", "gibbs_sample_p_families"]
+N_OPS_MAX = 16  # sbz_mh_config.op_prob / per-chain counter width
 
 
 def _torch():
@@ -28,11 +33,11 @@ def _torch():
 
 def op_probabilities(operators):
     """Operator weights (dict name -> weight, as MCMC.steps_per_operator builds them,
-    mcmc_setup.py:70-95) -> float64[8] in canonical order."""
-    p = np.zeros(len(OPS))
+    mcmc_setup.py:70-95) -> float64[N_OPS_MAX] in canonical order."""
+    p = np.zeros(N_OPS_MAX)
     for name, v in operators.items():
         if name not in OPS:
-            raise ValueError(f"unknown operator {name!r} (sampler supports {OPS[:7]})")
+            raise ValueError(f"unknown operator {name!r} (sampler supports {OPS})")
         p[OPS.index(name)] = float(v)
     if p[OPS.index("gibbsish_sample_zones")] != 0.0:
         raise ValueError("gibbsish_sample_zones must have weight 0 (as in the reference, mcmc_setup.py:77)")
@@ -51,7 +56,8 @@ def precisions(var_proposal):
 class ChainState:
     """Device-resident state of B chains (torch tensors on the engine's GPU)."""
 
-    def __init__(self, engine, zone_of_site, w, p_global, p_zones, p_fam=None, prior=None):
+    def __init__(self, engine, zone_of_site, w, p_global, p_zones, p_fam=None, prior=None,
+                 source=None):
         torch = _torch()
         dev = torch.device("cuda", engine.device)
         self.engine = engine
@@ -70,19 +76,29 @@ class ChainState:
         self.prior = (torch.zeros(self.B, dtype=f64, device=dev) if prior is None else
                       torch.as_tensor(np.broadcast_to(np.asarray(prior, np.float64), (self.B,)).copy(),
                                       device=dev))
-        self.accepted = torch.zeros((self.B, 8), dtype=torch.int64, device=dev)
-        self.proposed = torch.zeros((self.B, 8), dtype=torch.int64, device=dev)
+        self.accepted = torch.zeros((self.B, N_OPS_MAX), dtype=torch.int64, device=dev)
+        self.proposed = torch.zeros((self.B, N_OPS_MAX), dtype=torch.int64, device=dev)
+        # SAMPLE_SOURCE = true: component of every observation, uint8 [B][N][F] (Sample.source)
+        self.source = None
+        if source is not None:
+            src = np.ascontiguousarray(source, np.uint8)
+            if src.shape != (self.B, engine.n_sites, engine.n_features):
+                raise ValueError(f"source: expected {(self.B, engine.n_sites, engine.n_features)}, "
+                                 f"got {src.shape}")
+            self.source = torch.as_tensor(src, device=dev)
         self.counter = torch.zeros(self.B, dtype=torch.int64, device=dev)
         self.refresh_ll()
 
     def refresh_ll(self):
-        """Recompute every chain's log-likelihood from scratch (the likelihood kernel)."""
+        """Recompute every chain's log-likelihood from scratch (the likelihood kernel; the source
+        branch when the chains carry sources)."""
         torch = _torch()
         eng = self.engine
         eng.set_stream(torch.cuda.current_stream(self.ll.device).cuda_stream)
         eng.loglik_device(self.B, self.zone_of_site.data_ptr(), self.w.data_ptr(),
                           self.p_global.data_ptr(), self.p_zones.data_ptr(),
-                          self.p_fam.data_ptr() if self.p_fam is not None else 0, 0,
+                          self.p_fam.data_ptr() if self.p_fam is not None else 0,
+                          self.source.data_ptr() if self.source is not None else 0,
                           self.ll.data_ptr())
         return self.ll
 
@@ -90,6 +106,8 @@ class ChainState:
         out = {"zone_of_site": self.zone_of_site.cpu().numpy(), "w": self.w.cpu().numpy(),
                "p_global": self.p_global.cpu().numpy(), "p_zones": self.p_zones.cpu().numpy(),
                "ll": self.ll.cpu().numpy(), "prior": self.prior.cpu().numpy()}
+        if self.source is not None:
+            out["source"] = self.source.cpu().numpy()
         if self.p_fam is not None:
             out["p_fam"] = self.p_fam.cpu().numpy()
         return out
@@ -99,7 +117,7 @@ class Sampler:
     """MH sampler over a LikelihoodEngine's context (same data, same GPU)."""
 
     def __init__(self, engine, applicable_states, adj_indptr, adj_indices, operators, var_proposal,
-                 min_size, warmup=False, priors=None):
+                 min_size, warmup=False, priors=None, sample_source=False, gibbs_counts=None):
         self.engine = engine
         states = np.ascontiguousarray(applicable_states, dtype=np.uint8)
         if states.shape != (engine.n_features, engine.n_states):
@@ -114,14 +132,35 @@ class Sampler:
                                   indices.ctypes.data_as(ctypes.c_void_p)), engine.ctx)
         self.cfg = sbz_mh_config()
         probs = operators if isinstance(operators, np.ndarray) else op_probabilities(operators)
-        for i in range(8):
+        for i in range(min(N_OPS_MAX, len(probs))):
             self.cfg.op_prob[i] = float(probs[i])
+        self.cfg.sample_source = int(bool(sample_source))
+        self.sample_source = bool(sample_source)
         prec = precisions(var_proposal)
         for i in range(4):
             self.cfg.precision[i] = float(prec[i])
         self.cfg.min_size = int(min_size)
         self.cfg.warmup = int(bool(warmup))
         self.set_priors(priors)
+        if sample_source:
+            cg, cf = gibbs_counts if gibbs_counts is not None else (None, None)
+            self.set_gibbs_counts(cg, cf)
+
+    def set_gibbs_counts(self, counts_global=None, counts_fam=None):
+        """Prior pseudo-counts of the source-mode Gibbs operators (PGlobalPrior.counts [F][S],
+        PFamiliesPrior.counts [Fam][F][S]; None = 1, the 'uniform' priors' counts)."""
+        eng = self.engine
+        F, S = eng.n_features, eng.n_states
+        cg = None if counts_global is None else np.ascontiguousarray(counts_global, np.float64)
+        cf = None if counts_fam is None else np.ascontiguousarray(counts_fam, np.float64)
+        if cg is not None and cg.shape != (F, S):
+            raise ValueError(f"counts_global: expected {(F, S)}, got {cg.shape}")
+        if cf is not None and cf.shape != (eng.n_families, F, S):
+            raise ValueError(f"counts_fam: expected {(eng.n_families, F, S)}, got {cf.shape}")
+        vp = ctypes.c_void_p
+        check(eng._lib.sbz_set_gibbs_counts(eng.ctx, vp(cg.ctypes.data) if cg is not None else None,
+                                            vp(cf.ctypes.data) if cf is not None else None), eng.ctx)
+        self._gibbs_counts = (cg, cf)
 
     def set_priors(self, priors):
         """The prior terms of the MH ratio (contact_zones_amd.priors.PriorSpec; None = zero)."""
@@ -145,7 +184,7 @@ class Sampler:
         self.priors = p
 
     def run(self, state, n_steps, max_size, p_grow_connected, seed=0, chain_id0=0, tape=None,
-            tape_len=None, tape_pos=None, trace=False, trace_zones=False):
+            tape_len=None, tape_pos=None, trace=False, trace_zones=False, alias=None):
         """Run n_steps MH steps on every chain of `state` (in place).
 
         max_size / p_grow_connected: scalars or per-chain arrays (warm-up: get_max_size_list and
@@ -167,6 +206,16 @@ class Sampler:
         ch.p_fam = state.p_fam.data_ptr() if state.p_fam is not None else None
         ch.ll = state.ll.data_ptr()
         ch.prior = state.prior.data_ptr()
+        if self.sample_source:
+            if state.source is None:
+                raise ValueError("SAMPLE_SOURCE sampler needs chains with sources (ChainState(source=...))")
+            ch.source = state.source.data_ptr()
+        if alias is not None:  # (pending [B] int32, p_global, p_zones, p_fam) device tensors
+            pend, apg, apz, apf = alias
+            ch.alias_pending = pend.data_ptr()
+            ch.alias_p_global = apg.data_ptr()
+            ch.alias_p_zones = apz.data_ptr()
+            ch.alias_p_fam = apf.data_ptr() if apf is not None else None
         ch.max_size = ms.data_ptr()
         ch.p_grow_connected = pg.data_ptr()
         out = {"status": torch.zeros(B, dtype=torch.int32, device=dev)}

@@ -124,14 +124,21 @@ uint64_t sbz_lik_lds_bytes(const sbz_dims *dims, int source_mode);
 enum sbz_op {
     SBZ_OP_SHRINK_ZONE = 0, SBZ_OP_GROW_ZONE = 1, SBZ_OP_SWAP_ZONE = 2, SBZ_OP_ALTER_WEIGHTS = 3,
     SBZ_OP_ALTER_P_GLOBAL = 4, SBZ_OP_ALTER_P_ZONES = 5, SBZ_OP_ALTER_P_FAMILIES = 6,
-    SBZ_OP_GIBBSISH_SAMPLE_ZONES = 7 /* reference weight 0 (mcmc_setup.py:77); must stay 0 */
+    SBZ_OP_GIBBSISH_SAMPLE_ZONES = 7, /* reference weight 0 (mcmc_setup.py:77); must stay 0 */
+    /* SAMPLE_SOURCE = true operators (mcmc_setup.py:80-87, zone_sampling.py:180-406) */
+    SBZ_OP_GIBBS_SAMPLE_SOURCES = 8, SBZ_OP_GIBBS_SAMPLE_WEIGHTS = 9,
+    SBZ_OP_GIBBS_SAMPLE_P_GLOBAL = 10, SBZ_OP_GIBBS_SAMPLE_P_ZONES = 11,
+    SBZ_OP_GIBBS_SAMPLE_P_FAMILIES = 12,
+    SBZ_N_OPS = 16 /* width of op_prob and of the per-chain counters */
 };
 
 typedef struct sbz_mh_config {
-    double op_prob[8];    /* operator weights, SBZ_OP_* order (normalised here) (mcmc_setup.py:70-95) */
+    double op_prob[16];   /* operator weights, SBZ_OP_* order (normalised here) (mcmc_setup.py:70-95) */
     double precision[4];  /* PROPOSAL_PRECISION: weights, universal, contact, inheritance */
     int32_t min_size;     /* MIN_M (model.py:43) */
     int32_t warmup;       /* 1: ZoneMCMCWarmup semantics (shrink back-probability 1/(size+1)) */
+    int32_t sample_source;/* 1: SAMPLE_SOURCE = true (sbz_chains.source; Gibbs operators 8-12) */
+    int32_t reserved;
 } sbz_mh_config;
 
 /* Chain state and I/O of a run; every pointer is a device pointer, chain-major (B chains). */
@@ -150,7 +157,7 @@ typedef struct sbz_chains {
     uint64_t seed;
     uint64_t chain_id0;               /* global id of chain 0 (rank offset) */
     uint64_t *counter;                /* [B] in/out, or NULL (start at 0) */
-    int64_t *accepted, *proposed;     /* [B][8] accumulated per operator, or NULL */
+    int64_t *accepted, *proposed;     /* [B][SBZ_N_OPS] accumulated per operator, or NULL */
     int32_t *status;                  /* [B] 1 = tape exhausted, or NULL */
     int8_t *trace_op;                 /* [B][n_steps] or NULL */
     uint8_t *trace_accept;            /* [B][n_steps] (with trace_op) */
@@ -158,6 +165,16 @@ typedef struct sbz_chains {
     uint8_t *trace_zos;               /* [B][n_steps][N] or NULL (tests) */
     double *prior;                    /* [B] in/out: the chain's log prior (sbz_set_priors), or NULL
                                          when every prior term is 0 */
+    uint8_t *source;                  /* [B][N][F] in/out (sample_source): component of each
+                                         observation, 0 global, 1 zone, 2 family (Sample.source) */
+    /* sample_source only: the reference's Gibbs operators on p_global / p_zones / p_families
+     * change the chain's Sample in place (zone_sampling.py:333-400), so the parameter arrays of a
+     * logged sample (mcmc_generative.py:353-367 keeps references) go on changing until an
+     * accepted operator replaces the Sample (Sample.copy, :100-115: the zone moves and
+     * gibbs_sample_weights).  With alias_pending[b] = 1 the first such accept copies the chain's
+     * p_* into alias_* and clears the flag. */
+    int32_t *alias_pending;           /* [B] in/out, or NULL */
+    double *alias_p_global, *alias_p_zones, *alias_p_fam;  /* [B][...] as p_global / p_zones / p_fam */
 } sbz_chains;
 
 /* Sampler-only data: applicable states (uint8 [F][S], data.states) and the site network as CSR
@@ -178,6 +195,13 @@ int sbz_set_network(sbz_ctx *ctx, const uint8_t *applicable, int32_t nnz, const 
  * altered states, or the changed zone size) to the MH ratio and carries sbz_chains.prior. */
 int sbz_set_priors(sbz_ctx *ctx, const double *alpha_global, const double *alpha_fam,
                    int32_t size_prior);
+
+/* Prior pseudo-counts of the source-mode Gibbs operators (SAMPLE_SOURCE = true): p_global is
+ * redrawn from Dirichlet(counts_global[f] + source counts) (gibbs_sample_p_global,
+ * zone_sampling.py:334-357; PGlobalPrior.counts, model.py:576-586), p_families from
+ * Dirichlet(counts_fam[fam][f] + ...) (:381-406; PFamiliesPrior.counts).  double [F][S] and
+ * [Fam][F][S]; NULL = 1 everywhere (the 'uniform' priors' counts). */
+int sbz_set_gibbs_counts(sbz_ctx *ctx, const double *counts_global, const double *counts_fam);
 
 /* Run n_steps MH steps on B device-resident chains; asynchronous on ctx's stream. */
 int sbz_mh_run_device(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg,

@@ -29,8 +29,11 @@ from scipy.special import betaln, gammaln, xlogy
 from . import lik_numpy
 
 OPS = ["shrink_zone", "grow_zone", "swap_zone", "alter_weights", "alter_p_global",
-       "alter_p_zones", "alter_p_families", "gibbsish_sample_zones"]
+       "alter_p_zones", "alter_p_families", "gibbsish_sample_zones",
+       "gibbs_sample_sources", "gibbs_sample_weights", "gibbs_sample_p_global",
+       "gibbs_sample_p_zones", "gibbs_sample_p_families"]
 SHRINK, GROW, SWAP, WEIGHTS, P_GLOBAL, P_ZONES, P_FAMILIES = range(7)
+G_SOURCES, G_WEIGHTS, G_P_GLOBAL, G_P_ZONES, G_P_FAMILIES = range(8, 13)
 NONE = 255
 
 
@@ -46,6 +49,12 @@ class TapeReader:
 
     def int(self):
         return int(self.real())
+
+    def reals(self, n):
+        v = self.items[self.pos:self.pos + n]
+        assert v.size == n, "tape exhausted"
+        self.pos += n
+        return np.asarray(v, np.float64)
 
 
 def dirichlet_logpdf(x, alpha):
@@ -81,6 +90,16 @@ class Model:
         indptr, indices = fx["adj_indptr"], fx["adj_indices"]
         self.adj = [indices[indptr[s]:indptr[s + 1]] for s in range(N)]
         self.n_zones = int(fx["n_zones"])
+        self.sample_source = bool(fx["sample_source"]) if "sample_source" in fx else False
+        if self.sample_source:
+            S = self.states.shape[1]
+            self.features = np.zeros(self.obs.shape + (S,), bool)   # data.features (N, F, S)
+            n, f = np.nonzero(self.obs >= 0)
+            self.features[n, f, self.obs[n, f]] = True
+            self.gibbs_counts_global = fx["gibbs_counts_global"]
+            self.gibbs_counts_fam = fx.get("gibbs_counts_fam")
+            n_fam = 0 if self.gibbs_counts_fam is None else self.gibbs_counts_fam.shape[0]
+            self.families = np.stack([self.fam == i for i in range(n_fam)]) if n_fam else None
         self.size_prior = int(fx["prior_size"]) if "prior_size" in fx else 0
         self.alpha_global = fx.get("prior_alpha_global")
         self.alpha_fam = fx.get("prior_alpha_fam")
@@ -133,7 +152,12 @@ class Model:
 
     def loglik(self, st):
         return lik_numpy.loglik(self.obs, self.fam, st["zos"], st["w"], st["pg"], st["pz"],
-                                st.get("pf"), inheritance=self.inheritance)
+                                st.get("pf"), source=st.get("src"), inheritance=self.inheritance)
+
+    def posterior(self, st):
+        """normalize(lh_per_component * weights) (zone_sampling.py:193-202)."""
+        return lik_numpy.source_posterior(self.obs, self.fam, st["zos"], st["w"], st["pg"],
+                                          st["pz"], st.get("pf"), inheritance=self.inheritance)
 
 
 REJECT = (None, 0.0, -np.inf)
@@ -267,15 +291,138 @@ def op_p_families(m, st, c, tape):
     return new, log_q, log_q_back
 
 
+# ---- SAMPLE_SOURCE = true ------------------------------------------------------------------
+
+def sample_categorical(p, tape):
+    """preprocessing.sample_categorical (:321-348): argmax(u < cumsum(p)) with one uniform per
+    (site, feature) in C order; 0 when no entry of the cdf exceeds u."""
+    N, F, _ = p.shape
+    cdf = np.cumsum(p, axis=-1)
+    z = tape.reals(N * F).reshape(N, F, 1)
+    return np.argmax(z < cdf, axis=-1).astype(np.uint8)
+
+
+def log_q_sources(post, src):
+    """sum log posterior[source] over every observation, in ravel order (zone_sampling.py:218)."""
+    C = post.shape[-1]
+    is_source = np.where(np.eye(C, dtype=bool)[src].ravel())
+    return np.sum(np.log(post.ravel()[is_source]))
+
+
+def with_sources(op):
+    """A zone move with source resampling (zone_sampling.py:716-722, 781-784 etc.): log q_back
+    gains the current sources' posterior terms, then every source is redrawn from the new
+    sample's posterior (gibbs_sample_sources(as_gibbs=False)) and log q gains theirs."""
+    def move(m, st, c, tape):
+        log_q_back_s = log_q_sources(m.posterior(st), st["src"])
+        new, log_q, log_q_back = op(m, st, c, tape)
+        if new is None:
+            return REJECT
+        post = m.posterior(new)
+        new = dict(new, src=sample_categorical(post, tape))
+        if m.warmup:
+            # ZoneMCMCWarmup.gibbs_sample_sources (zone_sampling.py:1293-1296) passes
+            # as_gibbs=True whatever it is given: log q_s = Q_GIBBS = -inf, so the move is
+            # accepted without an acceptance draw (mcmc_generative.py:310-311)
+            return new, -np.inf, log_q_back + log_q_back_s
+        return new, log_q + log_q_sources(post, new["src"]), log_q_back + log_q_back_s
+    return move
+
+
+def op_gibbs_sources(m, st, c, tape):
+    """gibbs_sample_sources as an operator (zone_sampling.py:180-215): a Gibbs step."""
+    return dict(st, src=sample_categorical(m.posterior(st), tape)), -np.inf, 0
+
+
+def _source_counts(m, st, sites):
+    """np.sum(sample.source[sites], axis=0): per feature and component (F, C)."""
+    C = 3 if m.inheritance else 2
+    return np.sum(np.eye(C, dtype=bool)[st["src"]][sites], axis=0)
+
+
+def op_gibbs_weights(m, st, c, tape):
+    """gibbs_sample_weights (zone_sampling.py:222-331).  With inheritance the per-feature accept
+    draw is made and then overridden (sample_new.weights = w_new, :327): always the new weights."""
+    w = st["w"]
+    w_new = w.copy()
+    has_area = st["zos"] != NONE
+    F = w.shape[0]
+    if not m.inheritance:
+        counts = _source_counts(m, st, has_area)
+        for f in range(F):
+            w_new[f, :] = tape.reals(2)  # np.random.dirichlet(1 + counts[f])
+        return dict(st, w=w_new), -np.inf, 0
+    fixed = ["inheritance", "contact"][tape.int()]
+    if fixed == "inheritance":
+        a = tape.reals(F)                # stats.beta(1 + c_contact, 1 + c_univ).rvs()
+        w_new[..., 1] = a * w[..., 0] / (1 - a)
+    else:
+        a = tape.reals(F)                # stats.beta(1 + c_inherit, 1 + c_univ).rvs()
+        w_new[..., 2] = a * w[..., 0] / (1 - a)
+    w_new = normalize(w_new)
+    tape.reals(F)                        # np.random.random(F) < p_accept (overridden)
+    return dict(st, w=w_new), -np.inf, 0
+
+
+def normalize(x, axis=-1):
+    return x / np.sum(x, axis=axis, keepdims=True)
+
+
+def _gibbs_p(tape, p_row, prior_counts, counts, idx):
+    """p[idx] = np.random.dirichlet(prior_counts[idx] + counts) (value from the tape)."""
+    p_row = p_row.copy()
+    p_row[idx] = tape.reals(idx.size)
+    return p_row
+
+
+def op_gibbs_p_global(m, st, c, tape, fraction_of_features=0.4):
+    """gibbs_sample_p_global (zone_sampling.py:334-357)."""
+    F = st["pg"].shape[0]
+    subset = tape.reals(F) < fraction_of_features
+    pg = st["pg"].copy()
+    for f in np.flatnonzero(subset):
+        idx = np.flatnonzero(m.states[f])
+        pg[f] = _gibbs_p(tape, pg[f], None, None, idx)
+    return dict(st, pg=pg), -np.inf, 0
+
+
+def op_gibbs_p_zones(m, st, c, tape):
+    """gibbs_sample_p_zones (zone_sampling.py:359-379)."""
+    z = tape.int()  # np.random.randint(0, n_zones)
+    pz = st["pz"].copy()
+    for f in range(pz.shape[1]):
+        idx = np.flatnonzero(m.states[f])
+        pz[z, f] = _gibbs_p(tape, pz[z, f], None, None, idx)
+    return dict(st, pz=pz), -np.inf, 0
+
+
+def op_gibbs_p_families(m, st, c, tape, fraction_of_features=0.4):
+    """gibbs_sample_p_families (zone_sampling.py:381-406)."""
+    fam = tape.int()  # np.random.randint(0, n_families)
+    F = st["pf"].shape[1]
+    subset = tape.reals(F) < fraction_of_features
+    pf = st["pf"].copy()
+    for f in np.flatnonzero(subset):
+        idx = np.flatnonzero(m.states[f])
+        pf[fam, f] = _gibbs_p(tape, pf[fam, f], None, None, idx)
+    return dict(st, pf=pf), -np.inf, 0
+
+
 OPERATORS = {SHRINK: op_shrink, GROW: op_grow, SWAP: op_swap, WEIGHTS: op_weights,
-             P_GLOBAL: op_p_global, P_ZONES: op_p_zones, P_FAMILIES: op_p_families}
+             P_GLOBAL: op_p_global, P_ZONES: op_p_zones, P_FAMILIES: op_p_families,
+             G_SOURCES: op_gibbs_sources, G_WEIGHTS: op_gibbs_weights,
+             G_P_GLOBAL: op_gibbs_p_global, G_P_ZONES: op_gibbs_p_zones,
+             G_P_FAMILIES: op_gibbs_p_families}
+SOURCE_MOVES = {SHRINK: with_sources(op_shrink), GROW: with_sources(op_grow),
+                SWAP: with_sources(op_swap)}
 
 
 def step(m, st, ll, prior, c, tape):
     """MCMCGenerative.step (mcmc_generative.py:282-329).  Returns (state, ll, prior, op,
     accepted)."""
     op = tape.int()
-    cand, log_q, log_q_back = OPERATORS[op](m, st, c, tape)
+    fn = SOURCE_MOVES[op] if (m.sample_source and op in SOURCE_MOVES) else OPERATORS[op]
+    cand, log_q, log_q_back = fn(m, st, c, tape)
     if log_q_back == -np.inf:
         return st, ll, prior, op, False
     ll_cand = m.loglik(cand)
@@ -295,6 +442,8 @@ def initial_state(fx, c):
           "pg": fx["init_p_global"][c].copy(), "pz": fx["init_p_zones"][c].copy()}
     if bool(fx["inheritance"]):
         st["pf"] = fx["init_p_fam"][c].copy()
+    if "init_source" in fx:
+        st["src"] = fx["init_source"][c].copy()
     return st
 
 
@@ -308,7 +457,7 @@ def replay(fx, chain, n_steps=None):
     init_prior = prior
     tape = TapeReader(fx["tape"][chain, :int(fx["tape_len"][chain])])
     steps = fx["step_op"].shape[1] if n_steps is None else n_steps
-    ops, acc, lls, priors, zos = [], [], [], [], []
+    ops, acc, lls, priors, zos, srcs = [], [], [], [], [], []
     for _ in range(steps):
         st, ll, prior, op, a = step(m, st, ll, prior, chain, tape)
         ops.append(op)
@@ -316,5 +465,8 @@ def replay(fx, chain, n_steps=None):
         lls.append(ll)
         priors.append(prior)
         zos.append(st["zos"].copy())
+        if "src" in st:
+            srcs.append(st["src"].copy())
     return dict(op=np.array(ops), accept=np.array(acc), ll=np.array(lls), prior=np.array(priors),
-                init_prior=init_prior, zos=np.array(zos), state=st, tape_used=tape.pos)
+                init_prior=init_prior, zos=np.array(zos), src=np.array(srcs), state=st,
+                tape_used=tape.pos)

@@ -20,6 +20,16 @@ def golden_cases(prefix="lik_", exclude=("lik_kat",)):
     return [n for n in names if n not in exclude]
 
 
+def mh_cases(source=None):
+    """MH golden cases; source=False / True selects SAMPLE_SOURCE = false / true runs."""
+    out = []
+    for c in golden_cases("mh_", exclude=()):
+        src = c.startswith("mh_src")
+        if source is None or src == source:
+            out.append(c)
+    return out
+
+
 def load_golden(name):
     with np.load(os.path.join(GOLDEN, name + ".npz")) as z:
         return {k: z[k] for k in z.files}

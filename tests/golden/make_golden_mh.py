@@ -37,7 +37,10 @@ refenv.setup()
 
 # canonical operator ids (contact_zones_amd/sampler.py OPS uses the same order)
 OPS = ["shrink_zone", "grow_zone", "swap_zone", "alter_weights", "alter_p_global",
-       "alter_p_zones", "alter_p_families", "gibbsish_sample_zones"]
+       "alter_p_zones", "alter_p_families", "gibbsish_sample_zones",
+       # SAMPLE_SOURCE = true operators (mcmc_setup.py:80-87)
+       "gibbs_sample_sources", "gibbs_sample_weights", "gibbs_sample_p_global",
+       "gibbs_sample_p_zones", "gibbs_sample_p_families"]
 
 
 class Tape:
@@ -87,6 +90,11 @@ def install_recorders(seed, zs_mod, mg_mod):
     mg_mod._random = rec
     orig_choice = np.random.choice
     orig_dirichlet = np.random.dirichlet
+    orig_random = np.random.random
+    orig_randint = np.random.randint
+    from scipy.stats._continuous_distns import beta_gen
+    from scipy.stats._distn_infrastructure import rv_generic
+    orig_beta_rvs = beta_gen.__dict__.get("rvs")
 
     def choice(a, size=None, replace=True, p=None):
         out = orig_choice(a, size, replace, p)
@@ -101,12 +109,39 @@ def install_recorders(seed, zs_mod, mg_mod):
         TAPE.put(*out)
         return out
 
+    def random_(size=None):
+        # np.random.random: the categorical draws of sample_categorical (preprocessing.py:337,
+        # C order) and the feature subsets of the Gibbs operators (zone_sampling.py:335, 383)
+        out = orig_random(size)
+        TAPE.put(*np.ravel(out))
+        return out
+
+    def randint(low, high=None, size=None, dtype=int):
+        out = orig_randint(low, high, size, dtype)
+        TAPE.put(*np.ravel(out))
+        return out
+
+    def beta_rvs(self, *args, **kwds):
+        # scipy.stats.beta(...).rvs() in gibbs_sample_weights (zone_sampling.py:263, 291)
+        out = rv_generic.rvs(self, *args, **kwds)
+        TAPE.put(*np.ravel(out))
+        return out
+
     np.random.choice = choice
     np.random.dirichlet = dirichlet
+    np.random.random = random_
+    np.random.randint = randint
+    beta_gen.rvs = beta_rvs
 
     def restore():
         np.random.choice = orig_choice
         np.random.dirichlet = orig_dirichlet
+        np.random.random = orig_random
+        np.random.randint = orig_randint
+        if orig_beta_rvs is None:
+            del beta_gen.rvs
+        else:
+            beta_gen.rvs = orig_beta_rvs
 
     return restore
 
@@ -123,11 +158,19 @@ def run_case(name, data, model_cfg, mcmc_cfg, steps, seed, warmup, n_chains):
         model = Model(data=data, config=model_cfg)
         a = mcmc_cfg["STEPS"]
         ops = {"shrink_zone": a["area"] * 0.4, "grow_zone": a["area"] * 0.4,
-               "swap_zone": a["area"] * 0.2, "gibbsish_sample_zones": a["area"] * 0.0,
-               "alter_weights": a["weights"], "alter_p_global": a["universal"],
-               "alter_p_zones": a["contact"]}
-        if model_cfg["INHERITANCE"]:
-            ops["alter_p_families"] = a["inheritance"]
+               "swap_zone": a["area"] * 0.2, "gibbsish_sample_zones": a["area"] * 0.0}
+        if model_cfg["SAMPLE_SOURCE"]:  # MCMC.steps_per_operator (mcmc_setup.py:80-87)
+            ops.update({"gibbs_sample_sources": a.get("source", 0.0),
+                        "gibbs_sample_weights": a["weights"],
+                        "gibbs_sample_p_global": a["universal"],
+                        "gibbs_sample_p_zones": a["contact"]})
+            if model_cfg["INHERITANCE"]:
+                ops["gibbs_sample_p_families"] = a["inheritance"]
+        else:
+            ops.update({"alter_weights": a["weights"], "alter_p_global": a["universal"],
+                        "alter_p_zones": a["contact"]})
+            if model_cfg["INHERITANCE"]:
+                ops["alter_p_families"] = a["inheritance"]
         tot = sum(ops.values())
         ops = {k: v / tot for k, v in ops.items()}
         cls = zs.ZoneMCMCWarmup if warmup else zs.ZoneMCMC
@@ -137,7 +180,7 @@ def run_case(name, data, model_cfg, mcmc_cfg, steps, seed, warmup, n_chains):
                       initial_size=mcmc_cfg["M_INITIAL"], logger=None)
 
         N = data.features.shape[0]
-        init, steps_out = {}, {c: [] for c in range(n_chains)}
+        init, final, steps_out = {}, {}, {c: [] for c in range(n_chains)}
         orig_step = sampler.step
         orig_init = sampler.generate_initial_sample
 
@@ -160,7 +203,9 @@ def run_case(name, data, model_cfg, mcmc_cfg, steps, seed, warmup, n_chains):
             steps_out[c].append((op, sampler.statistics["accepted_steps"] > acc0,
                                  float(sampler._ll[c]),
                                  packing.zones_to_zone_of_site(new.zones, N),
-                                 float(sampler._prior[c])))
+                                 float(sampler._prior[c]),
+                                 None if new.source is None else packing.source_to_index(new.source)))
+            final[c] = new
             return new
 
         sampler.step = step
@@ -219,6 +264,24 @@ def run_case(name, data, model_cfg, mcmc_cfg, steps, seed, warmup, n_chains):
     out["step_zone_of_site"] = np.array([[s[3] for s in steps_out[c]] for c in range(n_chains)],
                                         np.uint8)
     out["step_prior"] = np.array([[s[4] for s in steps_out[c]] for c in range(n_chains)])
+    out["sample_source"] = np.array(bool(model_cfg["SAMPLE_SOURCE"]))
+    if model_cfg["SAMPLE_SOURCE"]:
+        # source assignments (component index per site and feature) at the start and after
+        # every step; the Gibbs operators' prior counts (zone_sampling.py:342-343, 391-392)
+        out["init_source"] = np.stack([packing.source_to_index(init[c].source)
+                                       for c in range(n_chains)])
+        out["step_source"] = np.array([[s[5] for s in steps_out[c]] for c in range(n_chains)],
+                                      np.uint8)
+        pr0 = sampler.posterior_per_chain[0].prior
+        out["gibbs_counts_global"] = np.asarray(pr0.prior_p_global.counts, np.float64)
+        if model_cfg["INHERITANCE"]:
+            out["gibbs_counts_fam"] = np.asarray(pr0.prior_p_families.counts, np.float64)
+    # final parameters of every chain
+    out["final_w"] = np.stack([final[c].weights for c in range(n_chains)])
+    out["final_p_global"] = np.stack([final[c].p_global[0] for c in range(n_chains)])
+    out["final_p_zones"] = np.stack([final[c].p_zones for c in range(n_chains)])
+    if model_cfg["INHERITANCE"]:
+        out["final_p_fam"] = np.stack([final[c].p_families for c in range(n_chains)])
     # priors as the chains used them (Prior, model.py:455-505): Dirichlet concentrations of the
     # 'counts' priors scattered to [F][S] / [Fam][F][S] (0 at inapplicable states), size prior.
     # Taken from a chain's model copy (mcmc_generative.py:80): every copy re-parses the config and
@@ -274,10 +337,11 @@ def run_case(name, data, model_cfg, mcmc_cfg, steps, seed, warmup, n_chains):
         out["stat_last_zones"] = np.asarray(st["last_sample"].zones, bool)
         out["stat_last_weights"] = np.asarray(st["last_sample"].weights, np.float64)
         # the reference's per-zone contributions of every logged sample (postprocessing.py:271-313)
-        from sbayes.postprocessing import contribution_per_area
-        contribution_per_area(sampler)
-        out["stat_lh_single_zones"] = np.asarray(sampler.statistics["sample_lh_single_zones"])
-        out["stat_prior_single_zones"] = np.asarray(sampler.statistics["sample_prior_single_zones"])
+        if not model_cfg["SAMPLE_SOURCE"]:  # (the reference's single-zone samples carry no source)
+            from sbayes.postprocessing import contribution_per_area
+            contribution_per_area(sampler)
+            out["stat_lh_single_zones"] = np.asarray(sampler.statistics["sample_lh_single_zones"])
+            out["stat_prior_single_zones"] = np.asarray(sampler.statistics["sample_prior_single_zones"])
     # run metadata (for the host-side drop-in tests: initial samples, warm-up lists)
     out["seed"] = np.array(seed)
     out["initial_size"] = np.array(mcmc_cfg["M_INITIAL"])
@@ -336,7 +400,7 @@ def small_data(seed=7, N=40, F=12, S=4, fam=2):
     return types.SimpleNamespace(features=x, states=states, network=net, families=fams)
 
 
-def model_cfg(Z, inheritance, min_m=3, max_m=50, counts=False, size="none"):
+def model_cfg(Z, inheritance, min_m=3, max_m=50, counts=False, size="none", source=False):
     prior = {"geo": {"type": "uniform"}, "area_size": {"type": size},
              "weights": {"type": "uniform"}, "universal": {"type": "uniform"},
              "inheritance": {"type": "uniform"}, "contact": {"type": "uniform"}}
@@ -344,7 +408,7 @@ def model_cfg(Z, inheritance, min_m=3, max_m=50, counts=False, size="none"):
         prior["universal"] = {"type": "counts", "scale_counts": None}
         prior["inheritance"] = {"type": "counts", "scale_counts": 10}
     return {"N_AREAS": Z, "MIN_M": min_m, "MAX_M": max_m, "INHERITANCE": inheritance,
-            "SAMPLE_SOURCE": False, "PRIOR": prior}
+            "SAMPLE_SOURCE": source, "PRIOR": prior}
 
 
 def with_counts(d, seed=11):
@@ -360,11 +424,11 @@ def with_counts(d, seed=11):
                                  prior_inheritance={"counts": ci})
 
 
-def mcmc_cfg(area=0.4, m_initial=5, p_grow=0.85, inheritance=0.1):
+def mcmc_cfg(area=0.4, m_initial=5, p_grow=0.85, inheritance=0.1, source=0.0):
     return {"P_GROW_CONNECTED": p_grow, "M_INITIAL": m_initial,
             "PROPOSAL_PRECISION": {"weights": 15, "universal": 40, "contact": 20, "inheritance": 20},
             "STEPS": {"area": area, "weights": 0.2, "universal": 0.1, "contact": 0.2,
-                      "inheritance": inheritance}}
+                      "inheritance": inheritance, "source": source}}
 
 
 def main():
@@ -384,6 +448,16 @@ def main():
     sc = with_counts(s)
     run_case("small_priors", sc, model_cfg(3, True, min_m=3, max_m=6, counts=True, size="uniform"),
              mcmc_cfg(area=0.6, m_initial=4), steps=400, seed=9, warmup=False, n_chains=3)
+    # SAMPLE_SOURCE = true (the reference default, config/default_config.json:32)
+    run_case("src_small", s, model_cfg(2, True, min_m=3, max_m=8, source=True),
+             mcmc_cfg(area=0.25, m_initial=4, source=0.05), steps=200, seed=12, warmup=False,
+             n_chains=3)
+    run_case("src_small_noinh", s, model_cfg(2, False, min_m=3, max_m=8, source=True),
+             mcmc_cfg(area=0.25, m_initial=4, inheritance=0.0, source=0.05), steps=200, seed=13,
+             warmup=False, n_chains=2)
+    run_case("src_priors_warmup", sc,
+             model_cfg(2, True, min_m=3, max_m=8, counts=True, size="uniform", source=True),
+             mcmc_cfg(area=0.25, m_initial=4), steps=150, seed=14, warmup=True, n_chains=3)
     run_case("small_priors_warmup", sc,
              model_cfg(2, True, min_m=3, max_m=8, counts=True, size="quadratic"),
              mcmc_cfg(area=0.6, m_initial=4), steps=300, seed=10, warmup=True, n_chains=4)

@@ -3,7 +3,7 @@ against the reference's own outputs (tests/golden/mh_*.npz, make_golden_mh.py)."
 import numpy as np
 import pytest
 
-from conftest import golden_cases, load_golden
+from conftest import golden_cases, load_golden, mh_cases
 from test_mcmc_host import make_sampler
 
 from contact_zones_amd import packing
@@ -11,9 +11,10 @@ from contact_zones_amd.sampler import OPS
 
 pytestmark = pytest.mark.gpu
 
-MH_CASES = golden_cases("mh_", exclude=())
-MAIN = [c for c in MH_CASES if "warmup" not in c]
-WARM = [c for c in MH_CASES if "warmup" in c]
+MH_CASES = mh_cases(source=False)
+SRC_CASES = mh_cases(source=True)  # SAMPLE_SOURCE = true (sbz_mh_src.hip)
+MAIN = [c for c in MH_CASES + SRC_CASES if "warmup" not in c]
+WARM = [c for c in MH_CASES + SRC_CASES if "warmup" in c]
 RTOL = 1e-9  # log-likelihood tolerance (north_star: 1e-9 relative)
 
 
@@ -26,6 +27,7 @@ def test_generate_samples_statistics_match_reference(case, gpu_available):
     smp = make_sampler(fx)
     smp._tape = (fx["tape"], fx["tape_len"])
     n_steps = fx["step_op"].shape[1]
+    np.random.seed(int(fx["seed"]))  # the initial sources' draws (np.random, as the reference)
     smp.generate_samples(n_steps, int(fx["stat_n_samples"]))
     st = smp.statistics
     assert st["sample_id"] == fx["stat_sample_id"].tolist()
@@ -53,6 +55,7 @@ def test_warmup_best_sample_matches_reference(case, gpu_available):
     fx = load_golden(case)
     smp = make_sampler(fx)
     smp._tape = (fx["tape"], fx["tape_len"])
+    np.random.seed(int(fx["seed"]))
     best = smp.generate_samples(0, 0, warm_up=True, warm_up_steps=fx["step_op"].shape[1])
     N = fx["obs"].shape[0]
     np.testing.assert_array_equal(packing.zones_to_zone_of_site(best.zones, N), fx["best_zone_of_site"])
@@ -103,7 +106,7 @@ def test_philox_run_is_self_consistent(gpu_available):
     assert len(m.statistics["sample_id"]) == 10
 
 
-@pytest.mark.parametrize("case", MAIN)
+@pytest.mark.parametrize("case", [c for c in MAIN if c in MH_CASES])
 def test_contribution_per_area_matches_reference(case, gpu_available):
     """postprocessing.contribution_per_area on the reference's logged samples: per-zone
     log-likelihoods within 1e-9, priors bit-exact (one batched likelihood launch)."""

@@ -5,11 +5,11 @@ the GPU) stay within the north_star tolerance of 1e-9 relative of the reference'
 import numpy as np
 import pytest
 
-from conftest import golden_cases, load_golden
+from conftest import golden_cases, load_golden, mh_cases
 
 pytestmark = pytest.mark.gpu
 
-MH_CASES = golden_cases(prefix="mh_", exclude=())
+MH_CASES = mh_cases(source=False)  # source mode: test_gpu_source.py
 REL_TOL = 1e-9
 
 

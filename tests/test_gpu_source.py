@@ -1,0 +1,127 @@
+"""GPU parity of the SAMPLE_SOURCE = true sampler (sbz_mh_src.hip): replaying the reference's
+decision tapes (tests/golden/mh_src_*.npz, make_golden_mh.py — seeded ZoneMCMC / ZoneMCMCWarmup
+with sample_source) reproduces every step's operator, accept flag, zone assignment and the
+final sources bit for bit; Gibbs-drawn parameters are bit-exact too (same tape, same arithmetic),
+log-likelihoods within the north_star tolerance of 1e-9 relative."""
+import numpy as np
+import pytest
+
+from conftest import load_golden, mh_cases
+
+pytestmark = pytest.mark.gpu
+
+SRC_CASES = mh_cases(source=True)
+REL_TOL = 1e-9
+
+
+def _setup(fx):
+    from contact_zones_amd.likelihood import LikelihoodEngine
+    from contact_zones_amd.priors import PriorSpec
+    from contact_zones_amd.sampler import ChainState, Sampler
+    inh = bool(fx["inheritance"])
+    S = fx["states"].shape[1]
+    Z = int(fx["n_zones"])
+    Fam = fx["init_p_fam"].shape[1] if inh else 0
+    eng = LikelihoodEngine(fx["obs"], fx["fam_of_site"], S, Z, Fam, inh)
+    priors = PriorSpec(fx.get("prior_alpha_global"), fx.get("prior_alpha_fam"), int(fx["prior_size"]))
+    smp = Sampler(eng, fx["states"], fx["adj_indptr"], fx["adj_indices"], fx["op_probs"],
+                  fx["precision"], int(fx["min_size"]), warmup=bool(fx["warmup"]), priors=priors,
+                  sample_source=True,
+                  gibbs_counts=(fx["gibbs_counts_global"], fx["gibbs_counts_fam"] if inh else None))
+    st = ChainState(eng, fx["init_zone_of_site"], fx["init_w"], fx["init_p_global"],
+                    fx["init_p_zones"], fx["init_p_fam"] if inh else None, prior=fx["init_prior"],
+                    source=fx["init_source"])
+    return eng, smp, st
+
+
+def _check_final(fx, st, inh):
+    s = st.to_numpy()
+    np.testing.assert_array_equal(s["source"], fx["step_source"][:, -1])
+    np.testing.assert_array_equal(s["w"], fx["final_w"])
+    np.testing.assert_array_equal(s["p_global"], fx["final_p_global"])
+    np.testing.assert_array_equal(s["p_zones"], fx["final_p_zones"])
+    if inh:
+        np.testing.assert_array_equal(s["p_fam"], fx["final_p_fam"])
+
+
+@pytest.mark.parametrize("case", SRC_CASES)
+def test_source_tape_replay_matches_reference(gpu_available, case):
+    import torch
+    fx = load_golden(case)
+    inh = bool(fx["inheritance"])
+    eng, smp, st = _setup(fx)
+    n_steps = fx["step_op"].shape[1]
+    out = smp.run(st, n_steps, fx["max_size"], fx["p_grow_connected"], tape=fx["tape"],
+                  tape_len=fx["tape_len"], trace=True, trace_zones=True)
+    torch.cuda.synchronize()
+    assert out["status"].cpu().numpy().tolist() == [0] * st.B
+    np.testing.assert_array_equal(out["tape_pos"].cpu().numpy(), fx["tape_len"])
+    np.testing.assert_array_equal(out["op"].cpu().numpy(), fx["step_op"])
+    np.testing.assert_array_equal(out["accept"].cpu().numpy().astype(bool), fx["step_accept"])
+    np.testing.assert_array_equal(out["zone_of_site"].cpu().numpy(), fx["step_zone_of_site"])
+    ll = out["ll"].cpu().numpy()
+    rel = np.abs(ll - fx["step_ll"]) / np.abs(fx["step_ll"])
+    assert rel.max() <= REL_TOL, rel.max()
+    _check_final(fx, st, inh)
+    np.testing.assert_allclose(st.prior.cpu().numpy(), fx["step_prior"][:, -1], rtol=1e-12, atol=1e-12)
+    # the tracked source log-likelihood equals a fresh evaluation of the final state
+    final = st.ll.cpu().numpy().copy()
+    fresh = st.refresh_ll().cpu().numpy()
+    assert np.max(np.abs(final - fresh) / np.abs(fresh)) <= REL_TOL
+    acc, prop = st.accepted.cpu().numpy(), st.proposed.cpu().numpy()
+    for b in range(st.B):
+        ops = fx["step_op"][b]
+        np.testing.assert_array_equal(prop[b, :13], np.bincount(ops, minlength=13)[:13])
+        np.testing.assert_array_equal(acc[b, :13], np.bincount(ops[fx["step_accept"][b]], minlength=13)[:13])
+
+
+def test_source_tape_replay_in_chunks(gpu_available):
+    """Several launches (sources and cursor carried in HBM) give the same trajectory."""
+    import torch
+    fx = load_golden(SRC_CASES[0])
+    eng, smp, st = _setup(fx)
+    n = fx["step_op"].shape[1]
+    pos = torch.zeros(st.B, dtype=torch.int64, device=st.ll.device)
+    ops = []
+    for a, b in [(0, 5), (5, 77), (77, n)]:
+        out = smp.run(st, b - a, fx["max_size"], fx["p_grow_connected"], tape=fx["tape"],
+                      tape_len=fx["tape_len"], tape_pos=pos, trace=True)
+        ops.append(out["op"].cpu().numpy())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(np.concatenate(ops, axis=1), fx["step_op"])
+    _check_final(fx, st, bool(fx["inheritance"]))
+
+
+def test_source_philox_chains_are_valid(gpu_available):
+    """Philox draws: every observation's source is a component it can come from (zone only inside
+    a zone, inheritance only inside a family), the parameters stay normalised, the tracked ll
+    equals a fresh evaluation and the carried prior the full prior; the run is reproducible."""
+    import torch
+    from contact_zones_amd.priors import PriorSpec
+    fx = load_golden("mh_src_small")
+    eng, smp, st = _setup(fx)
+    out = smp.run(st, 3000, fx["max_size"], fx["p_grow_connected"], seed=77)
+    torch.cuda.synchronize()
+    assert out["status"].cpu().numpy().tolist() == [0] * st.B
+    s = st.to_numpy()
+    src = s["source"]
+    assert src.max() <= 2
+    in_zone = s["zone_of_site"] < 255
+    assert not np.any((src == 1) & ~in_zone[:, :, None])
+    in_fam = fx["fam_of_site"] < 255
+    assert not np.any((src == 2) & ~in_fam[None, :, None])
+    np.testing.assert_allclose(s["w"].sum(-1), 1.0, rtol=1e-12)
+    np.testing.assert_allclose(s["p_global"].sum(-1), 1.0, rtol=1e-12)
+    np.testing.assert_allclose(s["p_zones"].sum(-1), 1.0, rtol=1e-12)
+    fresh = st.refresh_ll().cpu().numpy()
+    assert np.max(np.abs(s["ll"] - fresh) / np.abs(fresh)) <= REL_TOL
+    spec = PriorSpec(fx.get("prior_alpha_global"), fx.get("prior_alpha_fam"), int(fx["prior_size"]))
+    full = spec.log_prior(s["zone_of_site"], s["p_global"], s["p_fam"], fx["states"],
+                          int(fx["n_zones"]), bool(fx["inheritance"]))
+    np.testing.assert_allclose(s["prior"], full, rtol=1e-12, atol=1e-12)
+    assert st.accepted.sum().item() > 100
+    eng2, smp2, st2 = _setup(fx)
+    smp2.run(st2, 3000, fx["max_size"], fx["p_grow_connected"], seed=77)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(st2.source.cpu().numpy(), src)
+    np.testing.assert_array_equal(st2.zone_of_site.cpu().numpy(), s["zone_of_site"])

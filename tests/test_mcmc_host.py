@@ -7,14 +7,15 @@ import numpy as np
 import pytest
 import scipy.sparse as sp
 
-from conftest import golden_cases, load_golden
+from conftest import golden_cases, load_golden, mh_cases
 from contact_zones_amd import packing
 from contact_zones_amd.mcmc import (BatchedZoneMCMC, BatchedZoneMCMCWarmup, InitialSamples,
                                     check_model, get_max_size_list)
 from contact_zones_amd.priors import PriorSpec
 from contact_zones_amd.sampler import OPS
 
-MH_CASES = golden_cases("mh_", exclude=())
+MH_CASES = mh_cases(source=False)
+SRC_CASES = mh_cases(source=True)
 
 
 def objects_from_fixture(fx):
@@ -30,7 +31,8 @@ def objects_from_fixture(fx):
         network={"adj_mat": adj},
         families=packing.index_to_groups(fx["fam_of_site"], n_fam) if inh else None)
     model = types.SimpleNamespace(n_zones=int(fx["n_zones"]), min_size=int(fx["min_size"]),
-                                  max_size=int(fx["max_m"]), inheritance=inh, sample_source=False)
+                                  max_size=int(fx["max_m"]), inheritance=inh,
+                                  sample_source=bool(fx.get("sample_source", False)))
     ops = {OPS[i]: float(p) for i, p in enumerate(fx["op_probs"]) if p > 0 or OPS[i] == "gibbsish_sample_zones"}
     prec = fx["precision"]
     var_proposal = {"weights": prec[0], "universal": prec[1], "contact": prec[2],
@@ -40,6 +42,8 @@ def objects_from_fixture(fx):
               initial_size=int(fx["initial_size"]),
               priors=PriorSpec(fx.get("prior_alpha_global"), fx.get("prior_alpha_fam"),
                                int(fx["prior_size"])))
+    if bool(fx.get("sample_source", False)):
+        kw["gibbs_counts"] = (fx["gibbs_counts_global"], fx.get("gibbs_counts_fam"))
     return kw
 
 
@@ -49,15 +53,19 @@ def make_sampler(fx, **extra):
     return cls(rng=random.Random(int(fx["seed"])), **kw, **extra)
 
 
-@pytest.mark.parametrize("case", MH_CASES)
+@pytest.mark.parametrize("case", MH_CASES + SRC_CASES)
 def test_initial_samples_match_reference(case):
     """generate_initial_sample for every chain, in the reference's draw order, from the same
-    seeded python random source: zones, weights and p_* identical to the reference's."""
+    seeded python random source (and np.random for the initial sources): zones, weights, p_*
+    and sources identical to the reference's."""
     fx = load_golden(case)
     smp = make_sampler(fx)
     N = fx["obs"].shape[0]
+    np.random.seed(int(fx["seed"]))
     for c in range(fx["init_w"].shape[0]):
         s = smp.generate_initial_sample(c)
+        if bool(fx.get("sample_source", False)):
+            np.testing.assert_array_equal(packing.source_to_index(s.source), fx["init_source"][c])
         np.testing.assert_array_equal(packing.zones_to_zone_of_site(s.zones, N), fx["init_zone_of_site"][c])
         np.testing.assert_array_equal(s.weights, fx["init_w"][c])
         np.testing.assert_array_equal(s.p_global[0], fx["init_p_global"][c])
@@ -96,9 +104,13 @@ def test_initial_sample_reuses_previous_sample():
 
 
 def test_model_checks():
-    check_model(types.SimpleNamespace(sample_source=False, inheritance=True))
-    with pytest.raises(NotImplementedError):
-        check_model(types.SimpleNamespace(sample_source=True, inheritance=False))
+    check_model(types.SimpleNamespace(sample_source=False, inheritance=True), {"grow_zone": 1.0})
+    check_model(types.SimpleNamespace(sample_source=True, inheritance=False),
+                {"grow_zone": 0.5, "gibbs_sample_sources": 0.5})
+    with pytest.raises(ValueError):
+        check_model(types.SimpleNamespace(sample_source=False), {"gibbs_sample_weights": 1.0})
+    with pytest.raises(ValueError):
+        check_model(types.SimpleNamespace(sample_source=True), {"alter_weights": 1.0})
 
 
 def test_unsupported_options_raise():

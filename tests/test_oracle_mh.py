@@ -23,6 +23,14 @@ def test_oracle_replays_reference_trajectory(case):
         assert r["init_prior"] == fx["init_prior"][c]
         np.testing.assert_array_equal(r["prior"], fx["step_prior"][c])
         assert r["tape_used"] == int(fx["tape_len"][c])
+        if bool(fx["sample_source"]):  # source assignments after every step
+            np.testing.assert_array_equal(r["src"], fx["step_source"][c])
+        # final parameters
+        np.testing.assert_array_equal(r["state"]["w"], fx["final_w"][c])
+        np.testing.assert_array_equal(r["state"]["pg"], fx["final_p_global"][c])
+        np.testing.assert_array_equal(r["state"]["pz"], fx["final_p_zones"][c])
+        if bool(fx["inheritance"]):
+            np.testing.assert_array_equal(r["state"]["pf"], fx["final_p_fam"][c])
         lls.append(r["ll"][-1] + r["prior"][-1])
     if bool(fx["warmup"]):
         # best chain = argmax(ll + prior) after the warm-up (mcmc_generative.py:195-200)
@@ -31,15 +39,25 @@ def test_oracle_replays_reference_trajectory(case):
 
 
 def test_fixtures_cover_every_operator_and_rejection_kind():
-    ops = np.zeros(7, int)
+    ops = np.zeros(13, int)
     rejected_zone_moves = 0
     for case in MH_CASES:
         fx = load_golden(case)
-        ops += np.bincount(fx["step_op"].ravel(), minlength=8)[:7]
+        ops += np.bincount(fx["step_op"].ravel(), minlength=13)[:13]
         zone = fx["step_op"] <= 2
         rejected_zone_moves += int(np.sum(zone & ~fx["step_accept"]))
-    assert np.all(ops > 50), ops
+    assert np.all(ops[:7] > 50), ops
     assert rejected_zone_moves > 50
+
+
+def test_fixtures_cover_the_source_mode_operators():
+    """SAMPLE_SOURCE = true: every Gibbs operator and source-resampling zone moves."""
+    ops = np.zeros(13, int)
+    for case in MH_CASES:
+        fx = load_golden(case)
+        if bool(fx["sample_source"]):
+            ops += np.bincount(fx["step_op"].ravel(), minlength=13)
+    assert np.all(ops[[0, 1, 2, 8, 9, 10, 11, 12]] > 20), ops
 
 
 def test_fixtures_cover_the_prior_types():
