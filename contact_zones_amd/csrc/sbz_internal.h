@@ -89,6 +89,11 @@ int lik_configure(sbz_ctx *ctx);
 bool lik_counts_apply(const sbz_dims &d);
 // Sites per lane of the likelihood kernels for n_sites (4, 8, 16 or 32).
 int sites_per_lane(int n_sites);
+// Positions of the likelihood context: n_sites padded to a multiple of 64 * sites_per_lane.
+inline int np_of(int n_sites) {
+    const int chunk = 64 * sites_per_lane(n_sites);
+    return (n_sites + chunk - 1) / chunk * chunk;
+}
 
 // Sampler (sbz_mh.hip)
 size_t mh_lds_bytes(const sbz_dims &d, int C);

@@ -1,6 +1,7 @@
 // sbz_mh.hip — batched Metropolis-Hastings for the sBayes zone model on CDNA4 (gfx950).
 //
-// One wave (64 lanes) runs one chain for n_steps without leaving the kernel:
+// One workgroup of 4 waves (one per SIMD of a CU) runs one chain for n_steps without leaving the
+// kernel:
 // MCMCGenerative.step (sbayes/sampling/mcmc_generative.py:282-351) with the operators of
 // ZoneMCMC / ZoneMCMCWarmup (sbayes/sampling/zone_sampling.py) for SAMPLE_SOURCE = false; priors
 // zero, 'counts' on p_global / p_families and 'uniform' / 'quadratic' zone size (sbz_set_priors):
@@ -8,8 +9,8 @@
 //   swap_zone :704-786 (:1328-1416)             alter_weights :408-452
 //   alter_p_global :454-493   alter_p_zones :495-535   alter_p_families :571-612
 //   dirichlet_proposal :537-569 (q = exp(scipy dirichlet._logpdf) then log)
-// Every decision is wave-uniform: all lanes draw the same values and take the same branches;
-// lanes share the per-site / per-feature work.
+// Every decision is uniform: all lanes of all 4 waves draw the same values and take the same
+// branches; the 256 threads share the per-site / per-feature work.
 //
 // State: the chain's zone assignment lives in LDS for the whole run (written back at the end);
 // parameters stay in HBM and are updated in place on acceptance.  The log-likelihood is updated
@@ -28,25 +29,97 @@
 
 namespace sbz {
 
-
+#ifndef SBZ_MH_STAMP
+#define SBZ_MH_STAMP 0  // diagnostic builds only: trace_ll holds the shader cycles of phase k (1 move
+                        // draw, 2 proposal, 3 delta, 4 accept / apply, 5 whole step) instead of ll
+#endif
+#ifndef SBZ_MH_ABLATE
+#define SBZ_MH_ABLATE 0  // diagnostic builds only (wrong results): 1 = no parameter-move delta,
+                         // 2 = no Dirichlet proposal math, 4 = no zone-move delta
+#endif
 
 namespace {
 
-template <int C>
-__global__ __launch_bounds__(WAVE) void mh_kernel(MhArgs a) {
+// LDS layout of one chain's workgroup (byte offsets from the dynamic base), shared by the kernel
+// and mh_lds_bytes.  Site scans: thread t owns KT consecutive sites c * CH + t * KT + j of chunk
+// c (CH = NT * KT sites per chunk, nsc chunks); zos / nb / lst are padded to NpS = nsc * CH.
+struct MhLayout {
+    int KT, CH, nsc, NpS, nent, ncol;
+    size_t col, zsize, red, nb, zos, selc, lst, stat, tabo, tabn, nw, rowp, ipos, clsinfo, total;
+    __host__ __device__ MhLayout(int N, int Np, int S, int Z, int Fam, int C, int FamC, int NT) {
+        KT = Np / NT;
+        KT = KT < 4 ? 4 : (KT > 32 ? 32 : KT);
+        CH = NT * KT;
+        nsc = (Np + CH - 1) / CH;
+        NpS = nsc * CH;
+        nent = ((Z + 1) * FamC + 1) * (S + 1);
+        ncol = (1 + Z + (C == 3 ? Fam : 0)) * S + C;
+        size_t o = 0;
+        auto take = [&](size_t bytes) {
+            const size_t at = o;
+            o = (o + bytes + 15) & ~(size_t)15;
+            return at;
+        };
+        col = take((size_t)ncol * 8);
+        zsize = take((size_t)(Z + 1) * 4);
+        red = take(64 * 8);              // block reductions: [2][16] doubles + [2][16] ints + misc
+        nb = take((size_t)NpS * 2);
+        zos = take((size_t)NpS);
+        selc = take((size_t)nsc * 16 * 4);  // per chunk: selected sites per wave of the last scan
+        lst = take((size_t)NpS * 2);
+        stat = take(MH_STAT_INTS * 4);
+        tabo = take((size_t)nent * 8);
+        tabn = take((size_t)nent * 8);
+        nw = take(32 * 8);
+        rowp = take((size_t)Np * 4);
+        ipos = take((size_t)N * 2);
+        clsinfo = take((size_t)((Z + 1) * FamC + 1) * 2);
+        total = o;
+    }
+};
+
+// s_barrier after the wave's LDS operations complete.  Unlike __syncthreads() this does not
+// drain the vector-memory counter, so prefetched global loads stay in flight across it.
+__device__ __forceinline__ void bsync() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// One chain per workgroup of NWV waves (one per SIMD of the CU).  Every wave runs the same
+// control flow: all draws and decisions are computed redundantly and identically by every wave
+// (wave-uniform, from the same LDS / HBM state), and the per-site / per-feature work of a step is
+// split over all NWV * 64 threads, with block reductions in a fixed order (deterministic).
+// Shared state is written by thread 0 and published by a barrier.
+template <int C, int NWV>
+__global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const int lane = threadIdx.x;
+    constexpr int NT = NWV * WAVE;
+    const int tid = threadIdx.x, lane = tid & (WAVE - 1), wv = tid >> 6;
     const int b = blockIdx.x;
     const int N = a.N, F = a.F, S = a.S, Z = a.Z, Fam = (C == 3) ? a.Fam : 0;
     const sbz_chains &ch = a.ch;
 
-    // LDS carve-up
-    double *col = reinterpret_cast<double *>(lds);                  // (1+Z+Fam)*S + C doubles
-    const int ncol = (1 + Z + Fam) * S + C;
-    int *zsize = reinterpret_cast<int *>(col + ((ncol + 1) & ~1));  // [Z]
-    uint16_t *nb = reinterpret_cast<uint16_t *>(zsize + ((Z + 1) & ~1));  // [N]
-    uint8_t *zos = reinterpret_cast<uint8_t *>(nb + ((N + 1) & ~1));      // [N]
-    int *stat = reinterpret_cast<int *>(zos + ((N + 3) & ~3));  // [MH_STAT_INTS] proposed | accepted
+    const MhLayout L(N, a.Np, S, Z, a.Fam, C, a.FamC, NT);
+    const int KT = L.KT, CH = L.CH, nsc = L.nsc, ncol = L.ncol;
+    double *col = reinterpret_cast<double *>(lds + L.col);  // staged parameter column
+    int *zsize = reinterpret_cast<int *>(lds + L.zsize);     // [Z]
+    double *redd = reinterpret_cast<double *>(lds + L.red);  // [2][16]
+    int *redi = reinterpret_cast<int *>(redd + 32);           // [2][16]
+    int *misc = redi + 32;                                     // [8] published scalars
+    uint16_t *nb = reinterpret_cast<uint16_t *>(lds + L.nb);  // [NpS] neighbour stamps
+    uint8_t *zos = lds + L.zos;                                // [NpS] zone of site (NONE = none)
+    int *selc = reinterpret_cast<int *>(lds + L.selc);         // [nsc][16] per-wave counts
+    uint16_t *lst = reinterpret_cast<uint16_t *>(lds + L.lst); // [NpS] compacted members
+    int *stat = reinterpret_cast<int *>(lds + L.stat);         // [MH_STAT_INTS] proposed | accepted
+    // Parameter moves gather from two per-step tables (see delta_param): T[cls][x], cls = zone
+    // class * FamC + family class, one neutral row (cls = ncls) for padding positions.
+    const int S1 = S + 1, FamC = a.FamC, ncls = (Z + 1) * FamC, row_bytes = S1 * 8;
+    const int nent = L.nent;
+    double *tabo = reinterpret_cast<double *>(lds + L.tabo);     // [nent] old cells (1 if unchanged)
+    double *tabn = reinterpret_cast<double *>(lds + L.tabn);     // [nent] new cells (1 if unchanged)
+    double *nw = reinterpret_cast<double *>(lds + L.nw);         // [2][4][4] normalised weights
+    uint32_t *rowp = reinterpret_cast<uint32_t *>(lds + L.rowp); // [Np] table row (bytes) by position
+    uint16_t *ipos = reinterpret_cast<uint16_t *>(lds + L.ipos); // [N] position of each site
+    uint16_t *clsinfo = reinterpret_cast<uint16_t *>(lds + L.clsinfo);  // [ncls + 1] zone class | fc << 8
 
     uint8_t *gzos = ch.zone_of_site + (size_t)b * N;
     double *w = ch.w + (size_t)b * F * C;
@@ -57,22 +130,62 @@ __global__ __launch_bounds__(WAVE) void mh_kernel(MhArgs a) {
     const int max_size = ch.max_size[b];
     const double p_grow = ch.p_grow_connected[b];
 
+    // Block reductions (fixed wave order; every thread gets the same value).  Two slots used
+    // alternately: a slot is rewritten only after every wave passed the barrier of the next
+    // reduction, so no wave still reads it.
+    int rslot = 0;
+    auto block_sum = [&](double v) -> double {
+        v = wave_sum(v);
+        double *r = redd + rslot * 16;
+        if (lane == 0) r[wv] = v;
+        bsync();
+        double t = r[0];
+#pragma unroll
+        for (int i = 1; i < NWV; i++) t = t + r[i];
+        rslot ^= 1;
+        return uni(t);
+    };
+    auto block_sum_i = [&](int v) -> int {
+        v = wave_sum_i(v);
+        int *r = redi + rslot * 16;
+        if (lane == 0) r[wv] = v;
+        bsync();
+        int t = 0;
+#pragma unroll
+        for (int i = 0; i < NWV; i++) t += r[i];
+        rslot ^= 1;
+        return uni(t);
+    };
+
     // load the zone assignment; sizes
-    for (int z = lane; z < Z; z += WAVE) zsize[z] = 0;
-    if (lane < MH_STAT_INTS) stat[lane] = 0;
-    for (int s = lane; s < N; s += WAVE) nb[s] = 0;
-    wsync();
+    for (int z = tid; z < Z; z += NT) zsize[z] = 0;
+    if (tid < MH_STAT_INTS) stat[tid] = 0;
+    for (int s = tid; s < L.NpS; s += NT) nb[s] = 0;
+    bsync();
     int occ = 0;
-    for (int s = lane; s < N; s += WAVE) {
-        const int z = gzos[s];
+    for (int s = tid; s < L.NpS; s += NT) {
+        const int z = s < N ? gzos[s] : NONE;
         zos[s] = (uint8_t)z;
         if (z < Z) {
             atomicAdd(&zsize[z], 1);
             occ++;
         }
     }
-    int occupied = uni(wave_sum_i(occ));
-    wsync();
+    for (int c = tid; c <= ncls; c += NT)
+        clsinfo[c] = c == ncls ? (uint16_t)0xffffu : (uint16_t)((c / FamC) | ((c % FamC) << 8));
+    int occupied = block_sum_i(occ);  // (its barrier publishes zos / zsize / clsinfo)
+    // positions (family-sorted order of the likelihood context): site of each, its table row
+    for (int p = tid; p < a.Np; p += NT) {
+        uint32_t r = (uint32_t)(ncls * row_bytes);  // padding: the neutral row
+        if (p < N) {
+            const int s = a.perm[p];  // < N (built by sbz_open)
+            const int z = zos[s];
+            ipos[s] = (uint16_t)p;
+            r = (uint32_t)((((z < Z) ? z + 1 : 0) * FamC + (C == 3 ? (int)a.famc[p] : 0)) * row_bytes);
+        }
+        rowp[p] = r;
+    }
+    bsync();
 
     Rng rng;
     rng.tape = ch.tape ? ch.tape + (size_t)b * ch.tape_stride : nullptr;
@@ -86,68 +199,153 @@ __global__ __launch_bounds__(WAVE) void mh_kernel(MhArgs a) {
 
     double ll = ch.ll[b];
     double prior = ch.prior ? ch.prior[b] : 0.0;  // carried log prior (sbz_set_priors)
-    int err = 0;             // first range-check failure (MH_IDX)
+    int err = 0;             // first range-check failure of this thread (MH_IDX)
     long long err_val = 0;
     const long long nFS = (long long)F * S, nZFS = (long long)Z * F * S, nFamFS = (long long)Fam * F * S;
     uint16_t stamp = 0;
-    // per-operator counters, kept in LDS by lane 0 (no dynamically indexed private array)
 
-    // mark nb[t] = stamp for every site t adjacent to a member of zone z
-    auto mark = [&](int z) {
-        stamp++;
-        if (stamp == 0) {  // wrapped: clear
-            for (int s = lane; s < N; s += WAVE) nb[s] = 0;
-            wsync();
-            stamp = 1;
-        }
-        for (int s = lane; s < N; s += WAVE)
-            if (zos[s] == z)
-                for (int e = a.adj_ptr[s]; e < a.adj_ptr[s + 1]; e++)
-                    nb[MH_IDX(a.adj_idx[MH_IDX(e, a.nnz, 1)], N, 2)] = stamp;
-        wsync();
-    };
     auto is_nb = [&](int s) { return nb[s] == stamp && zos[s] == NONE; };
     // site selections: SEL_NB (neighbours of the marked zone, free), SEL_FREE, SEL_ZONE (members of z)
     enum { SEL_NB = 0, SEL_FREE = 1, SEL_ZONE = 2 };
-    auto sel = [&](int mode, int z, int s) -> bool {
-        const int zs = zos[s];
-        return mode == SEL_NB ? (nb[s] == stamp && zs == NONE) : (mode == SEL_FREE ? zs == NONE : zs == z);
-    };
-    // number of selected sites; the k-th selected site in ascending order (-1 if none)
-    auto count_sel = [&](int mode, int z) -> int {
-        int c = 0;
-        for (int s0 = 0; s0 < N; s0 += WAVE) {
-            const int s = s0 + lane;
-            const bool f = s < N ? sel(mode, z, min(s, N - 1)) : false;
-            c += __popcll(__ballot(f));
-        }
-        return uni(c);
-    };
-    auto kth_sel = [&](int mode, int z, int k) -> int {
-        int found = -1;
-        for (int s0 = 0; s0 < N; s0 += WAVE) {
-            const int s = s0 + lane;
-            const bool f = s < N ? sel(mode, z, min(s, N - 1)) : false;
-            const uint64_t m = __ballot(f);
-            const int n = __popcll(m);
-            if (found < 0 && k < n) {
-                const uint64_t hit = __ballot(f && lane_prefix(m) == k);
-                found = hit ? s0 + (int)__builtin_ctzll(hit) : -1;
-                k = -1;
-            } else if (found < 0) {
-                k -= n;
+    // Scan: every thread builds the bit mask of its selected sites (bit j = site base + j, KT <= 32
+    // sites read with a few wide LDS reads) of chunk c; per-wave counts go to selc.
+    auto scan_mask = [&](int mode, int z, int c) -> uint32_t {
+        const int s0 = c * CH + tid * KT;
+        uint32_t m = 0;
+#pragma unroll
+        for (int g = 0; g < 8; g++) {
+            if (4 * g >= KT) break;  // uniform
+            const uint32_t zw = *reinterpret_cast<const uint32_t *>(zos + s0 + 4 * g);
+            const uint2 nw2 = *reinterpret_cast<const uint2 *>(nb + s0 + 4 * g);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t zs = (zw >> (8 * j)) & 0xffu;
+                const uint32_t ns = ((j < 2 ? nw2.x : nw2.y) >> (16 * (j & 1))) & 0xffffu;
+                const bool f = mode == SEL_NB ? (ns == stamp && zs == NONE)
+                                              : (mode == SEL_FREE ? zs == NONE : zs == (uint32_t)z);
+                m |= (f ? 1u : 0u) << (4 * g + j);
             }
         }
-        return uni(found);
+        // padding sites (>= N) hold zone NONE and a stale stamp: never selected
+        const int nv = min(max(N - s0, 0), KT);
+        return m & (nv >= 32 ? 0xffffffffu : ((1u << nv) - 1u));
+    };
+    // exclusive prefix of n over the block's threads (thread order) from the per-wave totals in
+    // cnt[0..NWV); incl = the inclusive prefix within the wave
+    auto wave_incl = [&](int n) -> int {
+        int incl = n;
+#pragma unroll
+        for (int off = 1; off < WAVE; off <<= 1) {
+            const int t = __shfl_up(incl, off, WAVE);
+            if (lane >= off) incl += t;
+        }
+        return incl;
+    };
+    uint32_t msk[4];  // this thread's masks of the last scan (chunks 0..3; more chunks rescan)
+    int scan_mode = 0, scan_z = 0;
+    // number of selected sites; leaves per-wave counts in selc and the masks in msk
+    auto scan_sel = [&](int mode, int z) -> int {
+        scan_mode = mode;
+        scan_z = z;
+        for (int c = 0; c < nsc; c++) {
+            const uint32_t m = scan_mask(mode, z, c);
+            if (c < 4) msk[c & 3] = m;
+            const int wt = uni(__shfl(wave_incl(__popc(m)), WAVE - 1, WAVE));
+            if (lane == 0) selc[c * 16 + wv] = wt;
+        }
+        bsync();
+        // every wave sums the per-wave counts of every chunk
+        int all = 0;
+        for (int c = 0; c < nsc; c++)
+#pragma unroll
+            for (int i = 0; i < NWV; i++) all += selc[c * 16 + i];
+        return uni(all);
+    };
+    // The k-th selected site of the last scan in ascending order (-1 if none).
+    auto kth_scan = [&](int k) -> int {
+        for (int c = 0; c < nsc; c++) {
+            int tot = 0, woff = 0;
+#pragma unroll
+            for (int i = 0; i < NWV; i++) {
+                const int t = selc[c * 16 + i];
+                woff += i < wv ? t : 0;
+                tot += t;
+            }
+            tot = uni(tot);
+            if (k < tot) {
+                const uint32_t m = c < 4 ? msk[c & 3] : scan_mask(scan_mode, scan_z, c);
+                const int n = __popc(m);
+                const int incl = woff + wave_incl(n);
+                const int excl = incl - n;
+                int site = -1;
+                if (excl <= k && k < incl) {  // exactly one thread
+                    uint32_t mm = m;
+                    for (int r = k - excl; r > 0; r--) mm &= mm - 1;
+                    site = c * CH + tid * KT + (int)__builtin_ctz(mm);
+                    misc[0] = site;
+                }
+                bsync();
+                site = uni(misc[0]);
+                bsync();  // misc[0] may be rewritten by the next call
+                return site;
+            }
+            k -= tot;
+        }
+        return -1;
+    };
+    // mark nb[t] = stamp for every site t adjacent to a member of zone z: the members are
+    // compacted into lst, then every thread marks one member's neighbours (the adjacency loads of
+    // all members in flight at once)
+    auto mark = [&](int z) {
+        stamp++;
+        if (stamp == 0) {  // wrapped: clear
+            for (int s = tid; s < L.NpS; s += NT) nb[s] = 0;
+            bsync();
+            stamp = 1;
+        }
+        const int nmem = scan_sel(SEL_ZONE, z);
+        int base = 0;
+        for (int c = 0; c < nsc; c++) {
+            uint32_t m = c < 4 ? msk[c & 3] : scan_mask(SEL_ZONE, z, c);
+            int woff = 0, tot = 0;
+#pragma unroll
+            for (int i = 0; i < NWV; i++) {
+                const int t = selc[c * 16 + i];
+                woff += i < wv ? t : 0;
+                tot += t;
+            }
+            const int n = __popc(m);
+            int o = base + woff + wave_incl(n) - n;
+            while (m) {
+                lst[o++] = (uint16_t)(c * CH + tid * KT + (int)__builtin_ctz(m));
+                m &= m - 1;
+            }
+            base += uni(tot);
+        }
+        bsync();
+        for (int i = tid; i < nmem; i += NT) {
+            const int s = lst[i];
+            const int e0 = a.adj_ptr[s], e1 = a.adj_ptr[s + 1];
+            for (int e = e0; e < e1; e += 8) {
+                int t[8];
+#pragma unroll
+                for (int k = 0; k < 8; k++) t[k] = a.adj_idx[MH_IDX(min(e + k, e1 - 1), a.nnz, 1)];
+#pragma unroll
+                for (int k = 0; k < 8; k++)
+                    if (e + k < e1) nb[MH_IDX(t[k], N, 2)] = stamp;
+            }
+        }
+        bsync();
     };
 
-    // delta log-likelihood of moving site s from zone zo to zone zn (NONE = no zone)
+    // delta log-likelihood of moving site s from zone zo to zone zn (NONE = no zone): features
+    // split over the block's threads
     auto delta_site = [&](int s, int zo, int zn) {
         const int fc = (C == 3) ? a.fam_site[MH_IDX(s, N, 3)] : 0;
         const bool hf = fc > 0;
         double mn = 1.0, mo = 1.0;
         int en = 0, eo = 0;
-        for (int f = lane; f < F; f += WAVE) {
+        for (int f = tid; f < F; f += NT) {
             const int x = a.obs_sm[MH_IDX((long long)s * F + f, (long long)N * F, 4)];
             const bool na = x == S;
             const int xc = na ? 0 : x;
@@ -167,79 +365,146 @@ __global__ __launch_bounds__(WAVE) void mh_kernel(MhArgs a) {
             renorm(mo, eo);
             renorm(mn, en);
         }
-        const double d = (log(mn) - log(mo)) + (double)(en - eo) * LN2;
-        return uni(wave_sum(d));
+        return (log(mn) - log(mo)) + (double)(en - eo) * LN2;  // this thread's part (block_sum)
     };
 
-    // stage feature f's parameter column into LDS: pg | pz[z] | pf[fam] | w
-    auto stage_col = [&](int f) {
-        for (int i = lane; i < ncol; i += WAVE) {
-            // one unconditional load from a pointer chosen per element (always a valid index)
-            const int seg = i / S, r = i - seg * S;
-            const double *src;
-            long long idx, lim;
-            if (i >= (1 + Z + Fam) * S) {
-                src = w;
-                idx = (long long)f * C + (i - (1 + Z + Fam) * S);
-                lim = (long long)F * C;
-            } else if (seg == 0) {
-                src = pg;
-                idx = (long long)f * S + r;
-                lim = nFS;
-            } else if (seg <= Z) {
-                src = pz;
-                idx = ((long long)(seg - 1) * F + f) * S + r;
-                lim = nZFS;
-            } else {
-                src = pf;
-                idx = ((long long)(seg - 1 - Z) * F + f) * S + r;
-                lim = nFamFS;
-            }
-            col[i] = ldp(src + MH_IDX(idx, lim, 9));
-        }
-        wsync();
+    // Feature f's parameter column pg | pz[z] | pf[fam] | w: loaded into registers early
+    // (col_load, issued before the proposal math so the loads are in flight meanwhile) and
+    // written to LDS later (col_store); columns longer than NCV * NT load the rest synchronously.
+    constexpr int NCV = 1;
+    auto col_src = [&](int f, int i) -> const double * {
+        // one unconditional load from a pointer chosen per element (always a valid index)
+        const int seg = i / S, r = i - seg * S;
+        if (i >= (1 + Z + Fam) * S) return w + MH_IDX((long long)f * C + (i - (1 + Z + Fam) * S), (long long)F * C, 9);
+        if (seg == 0) return pg + MH_IDX((long long)f * S + r, nFS, 9);
+        if (seg <= Z) return pz + MH_IDX(((long long)(seg - 1) * F + f) * S + r, nZFS, 9);
+        return pf + MH_IDX(((long long)(seg - 1 - Z) * F + f) * S + r, nFamFS, 9);
+    };
+    auto col_load = [&](int f, double (&cv)[NCV]) {
+#pragma unroll
+        for (int k = 0; k < NCV; k++) cv[k] = ldp(col_src(f, min(tid + NT * k, ncol - 1)));
+    };
+    auto col_store = [&](int f, const double (&cv)[NCV]) {
+#pragma unroll
+        for (int k = 0; k < NCV; k++)
+            if (tid + NT * k < ncol) col[tid + NT * k] = cv[k];
+        for (int i = tid + NT * NCV; i < ncol; i += NT) col[i] = ldp(col_src(f, i));
+        bsync();
+    };
+    // Observation words of feature f: chunk k = 256 positions (4 per lane); wave wv gathers
+    // chunks wv, wv + NWV, ...  OB of them are loaded ahead (clamped: unconditional loads, so
+    // they all issue back to back).
+    constexpr int OB = 4;
+    const int nch = a.Np / 256;
+    const uint32_t *obs32 = reinterpret_cast<const uint32_t *>(a.obs_fm);
+    auto obs_load = [&](int f, int i0, uint32_t (&o)[OB]) {
+        const size_t fo = (size_t)MH_IDX(f, F, 13) * (size_t)(a.Np / 4);
+#pragma unroll
+        for (int i = 0; i < OB; i++)
+            o[i] = obs32[fo + (size_t)min(wv + NWV * (i0 + i), nch - 1) * WAVE + lane];
     };
     // delta of a parameter move on feature f: component comp (0 global, 1 zone, 2 family,
-    // 3 weights), row (zone / family), the two altered entries ia, ib with new values va, vb
-    auto delta_param = [&](int f, int comp, int row, int ia, int ib, double va, double vb) {
+    // 3 weights), row (zone / family), the two altered entries ia, ib with new values va, vb.
+    // A cell's value depends only on (zone class, family class, x), so the block builds two
+    // tables for feature f — the reference cell before and after the move for every (class, x)
+    // whose value the move changes, 1.0 for every other entry — and each site then multiplies one
+    // factor from each (its row offset in rowp, its observation byte), with no per-site tests.
+    // The changed entries are exactly the cells the reference recomputes: every cell for the
+    // weights, state ia / ib of the component's rows otherwise (NA cells do not change).
+    // `o` holds the wave's first OB observation chunks (obs_load, issued early).  Returns this
+    // thread's part of the delta (block_sum).
+    auto delta_param = [&](int f, int comp, int row, int ia, int ib, double va, double vb,
+                           uint32_t (&o)[OB]) {
         const double *wc = col + (1 + Z + Fam) * S;
-        double wold[3], wnew[3];
+        // normalize_weights (model.py:436-452) for the 4 (has_zone, has_family) classes, before
+        // (nw[0..15]) and after (nw[16..31]) the move; one division per weight as the reference
+        if (tid < 8) {
+            const int h = tid & 3, nu = tid >> 2;
+            double wv3[3];
 #pragma unroll
-        for (int i = 0; i < 3; i++) {
-            wold[i] = (C == 3 || i < 2) ? wc[i] : 0.0;
-            wnew[i] = (comp == 3 && i == ia) ? va : ((comp == 3 && i == ib) ? vb : wold[i]);
+            for (int i = 0; i < 3; i++) {
+                const double wo = (C == 3 || i < 2) ? wc[i] : 0.0;
+                wv3[i] = (nu && comp == 3 && i == ia) ? va : ((nu && comp == 3 && i == ib) ? vb : wo);
+            }
+            const double w0 = wv3[0] * 1.0, w1 = wv3[1] * ((h & 1) ? 1.0 : 0.0);
+            double sum = w0 + w1, w2 = 0.0;
+            if (C == 3) {
+                w2 = wv3[2] * ((h & 2) ? 1.0 : 0.0);
+                sum = sum + w2;
+            }
+            double *o4 = nw + nu * 16 + h * 4;
+            o4[0] = w0 / sum;
+            o4[1] = w1 / sum;
+            o4[2] = C == 3 ? w2 / sum : 0.0;
         }
-        const uint8_t *ob = a.obs_fm + MH_IDX((long long)f * a.Np, (long long)F * a.Np, 13);
+        bsync();
+        // tables: entry e = cls * S1 + x, threads step through e by NT (cls, x kept incrementally)
+        int cls = tid / S1, x = tid - (tid / S1) * S1;
+        const int dq = NT / S1, dr = NT - dq * S1;
+        int wide = 0;
+        for (int e = tid; e < nent; e += NT) {
+            const uint32_t ci = clsinfo[cls];
+            double to = 1.0, tn = 1.0;
+            if (ci != 0xffffu) {
+                const int zcl = (int)(ci & 0xffu), fc = (int)(ci >> 8);
+                const bool na = x == S, hz = zcl > 0, hf = fc > 0;
+                const int xc = na ? 0 : x, h = (hz ? 1 : 0) | (hf ? 2 : 0);
+                const double l0 = col[xc];
+                const double l1 = hz ? col[zcl * S + xc] : 0.0;
+                const double l2 = hf ? col[(Z + fc) * S + xc] : 0.0;
+                const bool pick = !na && (x == ia || x == ib);
+                const bool changed = comp == 3 || (pick && (comp == 0 || (comp == 1 && zcl == row + 1) ||
+                                                            (comp == 2 && fc == row + 1)));
+                const double nv = x == ia ? va : vb;
+                const double n0 = comp == 0 && pick ? nv : l0;
+                const double n1 = comp == 1 && pick ? nv : l1;
+                const double n2 = comp == 2 && pick ? nv : l2;
+                const double *wo = nw + h * 4, *wn = nw + 16 + h * 4;
+                const double wold[3] = {wo[0], wo[1], wo[2]}, wnew[3] = {wn[0], wn[1], wn[2]};
+                const double vo = cell_nw<C>(wold, hz, hf, na, l0, l1, l2);
+                const double vn = cell_nw<C>(wnew, hz, hf, na, n0, n1, n2);
+                to = changed ? vo : 1.0;
+                tn = changed ? vn : 1.0;
+                wide |= !(safe_cell(to) && safe_cell(tn)) ? 1 : 0;
+            }
+            tabo[e] = to;
+            tabn[e] = tn;
+            cls += dq;
+            x += dr;
+            if (x >= S1) {
+                x -= S1;
+                cls++;
+            }
+        }
+        const bool wid = block_sum_i(wide) != 0;  // (its barrier publishes the tables)
+        // gathers: position p = 256 k + 4 lane + j of the wave's chunks k = wv + NWV * i
         double mn = 1.0, mo = 1.0;
         int en = 0, eo = 0;
-        for (int p = lane; p < N; p += WAVE) {
-            const int s = a.perm[p];
-            const int zc = zos[s];
-            const int fc = (C == 3) ? a.famc[p] : 0;
-            const int x = a.xs8 ? (ob[p] >> 3) : ob[p];
-            const bool na = x == S;
-            bool hit;
-            if (comp == 3) hit = true;
-            else if (comp == 0) hit = !na && (x == ia || x == ib);
-            else if (comp == 1) hit = zc == row && !na && (x == ia || x == ib);
-            else hit = fc == row + 1 && !na && (x == ia || x == ib);
-            if (!hit) continue;
-            const int xc = na ? 0 : x;
-            const bool hz = zc < Z, hf = fc > 0;
-            const double l0 = col[xc];
-            const double l1 = hz ? col[(1 + zc) * S + xc] : 0.0;
-            const double l2 = hf ? col[(1 + Z + fc - 1) * S + xc] : 0.0;
-            double n0 = l0, n1 = l1, n2 = l2;
-            if (comp == 0) n0 = x == ia ? va : vb;
-            else if (comp == 1) n1 = x == ia ? va : vb;
-            else if (comp == 2) n2 = x == ia ? va : vb;
-            mo *= cell<C>(wold, hz, hf, na, l0, l1, l2);
-            mn *= cell<C>(comp == 3 ? wnew : wold, hz, hf, na, n0, n1, n2);
-            renorm(mo, eo);
-            renorm(mn, en);
+        const int nci = (nch - wv + NWV - 1) / NWV;  // this wave's chunks
+        for (int i0 = 0; i0 < nci; i0 += OB) {
+            if (i0 > 0) obs_load(f, i0, o);
+#pragma unroll
+            for (int i = 0; i < OB; i++) {
+                if (i0 + i >= nci) break;
+                const int k = wv + NWV * (i0 + i);
+                const uint4 rp = *reinterpret_cast<const uint4 *>(rowp + k * 256 + 4 * lane);
+                const uint32_t r4[4] = {rp.x, rp.y, rp.z, rp.w};
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const uint32_t xb = (o[i] >> (8 * j)) & 0xffu;
+                    const uint32_t ad = r4[j] + (a.xs8 ? xb : (xb << 3));
+                    mo *= *reinterpret_cast<const double *>(reinterpret_cast<const unsigned char *>(tabo) + ad);
+                    mn *= *reinterpret_cast<const double *>(reinterpret_cast<const unsigned char *>(tabn) + ad);
+                    if (wid) {
+                        renorm(mo, eo);
+                        renorm(mn, en);
+                    }
+                }
+                renorm(mo, eo);
+                renorm(mn, en);
+            }
         }
-        const double d = (log(mn) - log(mo)) + (double)(en - eo) * LN2;
-        return uni(wave_sum(d));
+        return (log(mn) - log(mo)) + (double)(en - eo) * LN2;
     };
 
     // One MH step per iteration, in four phases with one call site each (keeps the kernel small):
@@ -248,6 +513,8 @@ __global__ __launch_bounds__(WAVE) void mh_kernel(MhArgs a) {
     //   3. delta log-likelihood;  4. accept / reject and apply.
     bool broken = false;  // a tape decision with no matching candidate (replay mismatch)
     for (int step = 0; step < a.n_steps; step++) {
+        uint64_t tph[6];
+        tph[0] = SBZ_MH_STAMP ? __builtin_amdgcn_s_memtime() : 0;
         if (rng.bad || broken) break;
         const int op = rng.op(a.op_cdf, a.nops);
         if (op < 0 || op > P_FAMILIES || (op == P_FAMILIES && (C == 2 || Fam == 0)) ||
@@ -278,12 +545,16 @@ __global__ __launch_bounds__(WAVE) void mh_kernel(MhArgs a) {
                 if (op == SWAP || size < max_size) {
                     mark(z);
                     const bool connected = rng.real() < p_grow;
-                    const int n_nb = count_sel(SEL_NB, 0);
+                    const int n_nb = scan_sel(SEL_NB, 0);
                     const int cnt = connected ? n_nb : n_free;
                     if (cnt > 0) {
-                        const int site = kth_sel(connected ? SEL_NB : SEL_FREE, 0, rng.below(cnt));
+                        if (!connected) scan_sel(SEL_FREE, 0);
+                        const int site = kth_scan(rng.below(cnt));
                         int site_rm = -2;
-                        if (op == SWAP) site_rm = kth_sel(SEL_ZONE, z, rng.below(size));
+                        if (op == SWAP) {
+                            scan_sel(SEL_ZONE, z);
+                            site_rm = kth_scan(rng.below(size));
+                        }
                         if (site < 0 || site_rm == -1) {
                             broken = true;
                             break;
@@ -308,23 +579,23 @@ __global__ __launch_bounds__(WAVE) void mh_kernel(MhArgs a) {
                     }
                 }
             } else if (size > a.min_size) {  // SHRINK
-                const int site = kth_sel(SEL_ZONE, z, rng.below(size));
+                scan_sel(SEL_ZONE, z);
+                const int site = kth_scan(rng.below(size));
                 if (site < 0) {
                     broken = true;
                     break;
                 }
                 // back step: grow of the shrunk zone (neighbours of the zone without the site)
-                wsync();
-                if (lane == 0) zos[site] = NONE;
-                wsync();
+                if (tid == 0) zos[site] = NONE;
+                bsync();
                 mark(z);
-                const int n_back = count_sel(SEL_NB, 0);
+                const int n_back = scan_sel(SEL_NB, 0);
                 double q_back = (1.0 - p_grow) * (1.0 / (double)(n_free + 1));
                 if (is_nb(site)) q_back += p_grow * (1.0 / (double)n_back);
                 if (a.warmup) q_back = 1.0 / (double)(size + 1);  // zone_sampling.py:1561
-                wsync();
-                if (lane == 0) zos[site] = (uint8_t)z;
-                wsync();
+                bsync();  // every wave read zos[site] (is_nb) before it is restored
+                if (tid == 0) zos[site] = (uint8_t)z;
+                bsync();
                 log_q = uni(log(1.0 / (double)size));
                 log_q_back = uni(log(q_back));
                 dprior = uni(size_prior_delta(a.size_prior, N, size, size - 1));
@@ -359,9 +630,10 @@ __global__ __launch_bounds__(WAVE) void mh_kernel(MhArgs a) {
             const long long lim = comp == 3 ? (long long)F * C : (comp == 0 ? nFS : (comp == 1 ? nZFS : nFamFS));
             const long long off = comp == 3 ? (long long)f * C : ((long long)row * F + f) * S;
             prec = a.prec[comp == 3 ? 0 : comp + 1];
-            MH_IDX(off + ia, lim, 15);
-            MH_IDX(off + ib, lim, 15);
-            if (__ballot(err != 0)) {
+            // uniform indices: every thread of every wave takes the same branch
+            if (!(off + ia >= 0 && off + ia < lim && off + ib >= 0 && off + ib < lim)) {
+                MH_IDX(off + ia, lim, 15);
+                MH_IDX(off + ib, lim, 15);
                 broken = true;
                 break;
             }
@@ -369,16 +641,23 @@ __global__ __launch_bounds__(WAVE) void mh_kernel(MhArgs a) {
             poff = off;
         }
 
+        if (SBZ_MH_STAMP) tph[1] = __builtin_amdgcn_s_memtime();
         // ---- 2. Dirichlet proposal of the pair (zone_sampling.py:421-438, :537-569)
         double nv0 = 0.0, nv1 = 0.0;
+        double cv[NCV];
+        uint32_t ow[OB];
         if (comp >= 0) {
             const double c0 = uni(ldp(base + ia)), c1 = uni(ldp(base + ib));
+            // the move's column and observations: in flight during the proposal math
+            col_load(f, cv);
+            obs_load(f, 0, ow);
             // without inheritance the weight pair is used as is (zone_sampling.py:440-443)
             const bool raw = C == 2 && comp == 3;
             const double sum = raw ? 1.0 : c0 + c1;
             const double t0 = raw ? c0 : c0 / sum, t1 = raw ? c1 : c1 / sum;
-            double u0, u1;
-            dirichlet_proposal2(rng, t0, t1, prec, u0, u1, log_q, log_q_back);
+            double u0 = t0, u1 = t1;
+            if (SBZ_MH_ABLATE & 2) log_q = log_q_back = 0.0;
+            else dirichlet_proposal2(rng, t0, t1, prec, u0, u1, log_q, log_q_back);
             nv0 = raw ? u0 : u0 * sum;
             nv1 = raw ? u1 : u1 * sum;
             // 'counts' priors: dirichlet_logpdf(p[f, states], alpha) changes only in the two
@@ -393,20 +672,27 @@ __global__ __launch_bounds__(WAVE) void mh_kernel(MhArgs a) {
             }
         }
 
-        // ---- 3. delta log-likelihood
+        if (SBZ_MH_STAMP) tph[2] = __builtin_amdgcn_s_memtime();
+        // ---- 3. delta log-likelihood (one block reduction; it also makes a range-check failure
+        // of any thread known to every wave)
         double delta = 0.0;
-        if (sa >= 0) {
-            delta = delta_site(sa, zoa, zna);
-            if (sb >= 0) delta = delta + delta_site(sb, zna, NONE);
-        } else if (comp >= 0) {
-            stage_col(f);
-            delta = delta_param(f, comp, row, ia, ib, nv0, nv1);
-        }
-        if (__ballot(err != 0)) {  // a range check failed: stop before using the move
-            broken = true;
-            break;
+        if (sa >= 0 || comp >= 0) {
+            double part = 0.0;
+            if (sa >= 0 && !(SBZ_MH_ABLATE & 4)) {
+                part = delta_site(sa, zoa, zna);
+                if (sb >= 0) part = part + delta_site(sb, zna, NONE);
+            } else if (comp >= 0 && !(SBZ_MH_ABLATE & 1)) {
+                col_store(f, cv);
+                part = delta_param(f, comp, row, ia, ib, nv0, nv1, ow);
+            }
+            delta = block_sum(part);
+            if (block_sum_i(err != 0 ? 1 : 0) != 0) {  // a range check failed: stop before using the move
+                broken = true;
+                break;
+            }
         }
 
+        if (SBZ_MH_STAMP) tph[3] = __builtin_amdgcn_s_memtime();
         // ---- 4. metropolis_hastings_ratio (mcmc_generative.py:331-351, uniform priors)
         bool accept = false;
         if (log_q_back == -INFINITY) {
@@ -417,14 +703,16 @@ __global__ __launch_bounds__(WAVE) void mh_kernel(MhArgs a) {
             const double mh = (delta * 1.0) - (log_q - log_q_back) + dprior;
             accept = log(rng.real()) < mh;
         }
-        if (lane == 0) stat[op]++;
+        if (tid == 0) stat[op]++;
         if (accept) {
-            if (lane == 0) stat[SBZ_N_OPS + op]++;
+            if (tid == 0) stat[SBZ_N_OPS + op]++;
             ll = ll + delta;
             prior = prior + dprior;
-            wsync();
             if (sa >= 0) {
-                if (lane == 0) {
+                if (tid == 0) {
+                    const int fca = C == 3 ? (int)a.fam_site[sa] : 0;
+                    rowp[ipos[sa]] = (uint32_t)(((zna < Z ? zna + 1 : 0) * FamC + fca) * row_bytes);
+                    if (sb >= 0) rowp[ipos[sb]] = (uint32_t)((C == 3 ? (int)a.fam_site[sb] : 0) * row_bytes);
                     zos[sa] = (uint8_t)zna;
                     if (zoa < Z) zsize[zoa]--;
                     if (zna < Z) zsize[zna]++;
@@ -434,54 +722,64 @@ __global__ __launch_bounds__(WAVE) void mh_kernel(MhArgs a) {
                     }
                 }
                 occupied += (zna < Z ? 1 : -1) + (sb >= 0 ? -1 : 0);
-            } else if (lane == 0) {
+            } else if (tid == 0) {
                 stp(base + ia, nv0);
                 stp(base + ib, nv1);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
-            wsync();
+            bsync();
         }
-        if (ch.trace_op && lane == 0) {
+        if (ch.trace_op && tid == 0) {
             const size_t t = (size_t)b * a.n_steps + step;
             ch.trace_op[t] = (int8_t)op;
             ch.trace_accept[t] = accept ? 1 : 0;
             ch.trace_ll[t] = ll;
+            if (SBZ_MH_STAMP) {
+                tph[4] = __builtin_amdgcn_s_memtime();
+                ch.trace_ll[t] = SBZ_MH_STAMP == 5 ? (double)(tph[4] - tph[0])
+                                                   : (double)(tph[SBZ_MH_STAMP] - tph[SBZ_MH_STAMP > 0 ? SBZ_MH_STAMP - 1 : 0]);
+            }
         }
         if (ch.trace_zos) {
             uint8_t *tz = ch.trace_zos + ((size_t)b * a.n_steps + step) * N;
-            for (int s = lane; s < N; s += WAVE) tz[s] = zos[s];
+            for (int s = tid; s < N; s += NT) tz[s] = zos[s];
         }
     }
 
-    for (int s = lane; s < N; s += WAVE) gzos[s] = zos[s];
-    if (lane == 0) {
+    bsync();
+    for (int s = tid; s < N; s += NT) gzos[s] = zos[s];
+    if (tid == 0) {
         ch.ll[b] = ll;
         if (ch.prior) ch.prior[b] = prior;
         if (ch.tape_pos) ch.tape_pos[b] = rng.pos;
         if (ch.counter) ch.counter[b] = rng.ctr;
         if (ch.status) ch.status[b] = broken ? 2 : (rng.bad ? 1 : 0);
     }
-    if (lane < SBZ_N_OPS) {  // per-operator counters, one lane each
-        if (ch.accepted) ch.accepted[(size_t)b * SBZ_N_OPS + lane] += stat[SBZ_N_OPS + lane];
-        if (ch.proposed) ch.proposed[(size_t)b * SBZ_N_OPS + lane] += stat[lane];
+    if (tid < SBZ_N_OPS) {  // per-operator counters, one thread each
+        if (ch.accepted) ch.accepted[(size_t)b * SBZ_N_OPS + tid] += stat[SBZ_N_OPS + tid];
+        if (ch.proposed) ch.proposed[(size_t)b * SBZ_N_OPS + tid] += stat[tid];
     }
+    // the first range-check failure (lowest thread): status 16 + code
     {
         const uint64_t bad = __ballot(err != 0);
-        if (bad) {
-            const int code = __shfl(err, (int)__builtin_ctzll(bad), 64);
-            if (lane == 0 && ch.status) ch.status[b] = 16 + code;
+        if (lane == 0) redi[wv] = bad ? __shfl(err, (int)__builtin_ctzll(bad), 64) : 0;
+        bsync();
+        if (tid == 0) {
+            int code = 0;
+            for (int i = 0; i < NWV && !code; i++) code = redi[i];
+            if (code && ch.status) ch.status[b] = 16 + code;
         }
     }
 }
 
+constexpr int MH_WAVES = 4;  // waves per chain (one workgroup per chain)
+
 }  // namespace
 
 size_t mh_lds_bytes(const sbz_dims &d, int C) {
-    const size_t Fam = C == 3 ? (size_t)d.n_families : 0;
-    const size_t ncol = (1 + (size_t)d.n_zones + Fam) * d.n_states + C;
-    return ((ncol + 1) & ~(size_t)1) * 8 + (((size_t)d.n_zones + 1) & ~(size_t)1) * 4 +
-           (((size_t)d.n_sites + 1) & ~(size_t)1) * 2 + (((size_t)d.n_sites + 3) & ~(size_t)3) +
-           MH_STAT_INTS * 4;
+    const int FamC = C == 3 ? d.n_families + 1 : 1;
+    return MhLayout(d.n_sites, np_of(d.n_sites), d.n_states, d.n_zones, d.n_families, C, FamC,
+                    MH_WAVES * WAVE).total;
 }
 
 int launch_mh(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg, const sbz_chains *chains) {
@@ -563,10 +861,11 @@ int launch_mh(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg, const 
     if (a.ch.tape && (!a.ch.tape_pos || !a.ch.tape_len))
         return fail(ctx, SBZ_EINVAL, "tape mode needs tape_pos and tape_len");
     if (src) return launch_mh_source(ctx, B, a);
+    if (d.n_sites > 65535) return fail(ctx, SBZ_EINVAL, "sampler supports at most 65535 sites");
     const size_t lds = mh_lds_bytes(d, ctx->C);
     if (lds > 64 * 1024) return fail(ctx, SBZ_EINVAL, "sampler state exceeds 64 KiB of LDS (too many sites)");
-    if (ctx->C == 3) mh_kernel<3><<<B, WAVE, lds, ctx->stream>>>(a);
-    else mh_kernel<2><<<B, WAVE, lds, ctx->stream>>>(a);
+    if (ctx->C == 3) mh_kernel<3, MH_WAVES><<<B, MH_WAVES * WAVE, lds, ctx->stream>>>(a);
+    else mh_kernel<2, MH_WAVES><<<B, MH_WAVES * WAVE, lds, ctx->stream>>>(a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(ctx, e, "sampler launch");
     return SBZ_OK;

@@ -84,7 +84,7 @@ __device__ __forceinline__ void philox_round(uint32_t (&c)[4], const uint32_t (&
     c[3] = (uint32_t)p0;
 }
 
-__device__ void philox4x32_10(uint32_t (&c)[4], uint32_t k0, uint32_t k1) {
+__device__ __forceinline__ void philox4x32_10(uint32_t (&c)[4], uint32_t k0, uint32_t k1) {
     uint32_t k[2] = {k0, k1};
 #pragma unroll
     for (int i = 0; i < 10; i++) {
@@ -106,16 +106,35 @@ __device__ __forceinline__ double uni(double v) {
     return __longlong_as_double((long long)uni64((int64_t)__double_as_longlong(v)));
 }
 
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)b, l);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(b >> 32), l);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+__device__ __forceinline__ double u53(uint32_t hi, uint32_t lo) {
+    return (double)((((uint64_t)hi << 32) | lo) >> 11) * 0x1p-53;
+}
+
 // The draw source: a replay tape (read straight from HBM, one item per draw, broadcast to the
-// wave) or Philox4x32-10.  Plain scalar members only: nothing of it lives in per-lane scratch.
+// wave) or Philox4x32-10.  Philox uniforms are numbered by `ctr` (per chain, carried across
+// launches): uniform i is half (i & 1) of block (i >> 1, chain) under key = seed.  The wave keeps
+// a pool of 32 consecutive uniforms (uniforms 2l, 2l + 1 in lane l < 16, computed by 16 lanes at
+// once) and broadcasts them with v_readlane, so a draw costs no Philox rounds on the step's
+// critical path.  The numbering does not depend on the pool, so a run split into several
+// launches draws the same uniforms.  The scalar members live in SGPRs; nothing of it lives in
+// per-lane scratch.
 struct Rng {
     const double *tape;  // this chain's tape, or null (Philox)
     int64_t pos, len;    // tape cursor / length
     uint32_t key0, key1;
-    uint64_t chain, ctr; // Philox stream (global chain id) and counter (one block per uniform)
+    uint64_t chain, ctr; // Philox stream (global chain id) and uniform counter
     int bad;             // tape exhausted
+    uint64_t pbase = 1ull << 63;  // index of the pool's first uniform (multiple of 32); none yet
+    double pool0, pool1;          // per lane: uniforms pbase + 2 lane, pbase + 2 lane + 1
 
-    __device__ double tape_item() {
+    __device__ __forceinline__ double tape_item() {
         if (pos >= len) {
             bad = 1;
             return 0.0;
@@ -124,22 +143,28 @@ struct Rng {
         pos = uni64(pos + 1);
         return uni(v);
     }
-    __device__ double uniform53() {  // [0, 1) with 53 random bits, one Philox block per call
-        uint32_t c[4] = {(uint32_t)ctr, (uint32_t)(ctr >> 32), (uint32_t)chain,
-                         (uint32_t)(chain >> 32)};
+    __device__ __forceinline__ void fill(uint64_t base) {  // wave-uniform call
+        const uint64_t blk = (base >> 1) + (uint64_t)(threadIdx.x & 15);
+        uint32_t c[4] = {(uint32_t)blk, (uint32_t)(blk >> 32), (uint32_t)chain, (uint32_t)(chain >> 32)};
         philox4x32_10(c, key0, key1);
+        pool0 = u53(c[0], c[1]);
+        pool1 = u53(c[2], c[3]);
+        pbase = base;
+    }
+    __device__ __forceinline__ double uniform53() {  // [0, 1) with 53 random bits
+        if (ctr - pbase >= 32) fill(ctr & ~31ull);
+        const int i = (int)(ctr - pbase);
         ctr++;
-        const uint64_t bits = ((uint64_t)c[0] << 32) | c[1];
-        return uni((double)(bits >> 11) * 0x1p-53);
+        return uni(readlane_d((i & 1) ? pool1 : pool0, i >> 1));
     }
     // a real in [0, 1): python random.random() / the acceptance and connected-step uniforms
-    __device__ double real() { return tape ? tape_item() : uniform53(); }
+    __device__ __forceinline__ double real() { return tape ? tape_item() : uniform53(); }
     // an index in [0, n): np.random.choice(range(n)) / random.choice(seq) -> seq[k]
-    __device__ int below(int n) {
+    __device__ __forceinline__ int below(int n) {
         if (tape) return uni((int)tape_item());
         return uni(min((int)(uniform53() * (double)n), n - 1));
     }
-    __device__ int op(const double *cdf, int nops) {
+    __device__ __forceinline__ int op(const double *cdf, int nops) {
         if (tape) return uni((int)tape_item());
         const double u = uniform53();  // numpy choice(p): first cdf entry > u
         int i = 0;                     // = the number of entries <= u (the cdf is non-decreasing)
@@ -148,7 +173,7 @@ struct Rng {
         return uni(i);
     }
     // random.sample(population, 2): two distinct values in draw order (pop == null: 0..n-1)
-    __device__ void pair(const int *pop, int n, int &a, int &b) {
+    __device__ __forceinline__ void pair(const int *pop, int n, int &a, int &b) {
         if (tape) {
             a = uni((int)tape_item());
             b = uni((int)tape_item());
@@ -160,44 +185,74 @@ struct Rng {
         a = uni(pop ? pop[i] : i);
         b = uni(pop ? pop[j] : j);
     }
-    __device__ double normal() {  // Box-Muller (Philox mode only)
-        const double u1 = 1.0 - uniform53();  // (0, 1]
-        const double u2 = uniform53();
+    // np.random.dirichlet(alpha) for 2 components; Philox mode: the two gammas run at once on
+    // lanes 0 and 1, each on its own lane stream (LaneRng) based at the current counter
+    __device__ __forceinline__ void dirichlet2(double a0, double a1, double &x0, double &x1);
+};
+
+// Per-lane Philox stream: block (j, base, chain lo, chain hi ^ (lane + 1) << 24), key = seed.
+// `base` is the wave's counter when the phase started (the wave then advances it by one), j
+// counts the lane's draws in the phase.
+struct LaneRng {
+    uint32_t k0, k1, base, c2, c3, j;
+    __device__ __forceinline__ void init(const Rng &r, int lane) {
+        k0 = r.key0;
+        k1 = r.key1;
+        base = (uint32_t)r.ctr;
+        c2 = (uint32_t)r.chain;
+        c3 = (uint32_t)(r.chain >> 32) ^ ((uint32_t)(lane + 1) << 24);
+        j = 0;
+    }
+    __device__ __forceinline__ double u() {
+        uint32_t c[4] = {j++, base, c2, c3};
+        philox4x32_10(c, k0, k1);
+        return u53(c[0], c[1]);
+    }
+    __device__ __forceinline__ double normal() {
+        const double u1 = 1.0 - u();
+        const double u2 = u();
         // cos(2 pi u2) as cospi(2 u2): no large-argument reduction (u2 in [0, 1))
         return sqrt(-2.0 * log(u1)) * cospi(2.0 * u2);
     }
-    // Marsaglia-Tsang, alpha >= 1.  Each round accepts with probability > 0.95 (alpha >= 1);
-    // the loop is bounded at 64 rounds (probability of reaching it < 1e-80).
-    __device__ double gamma(double alpha) {
-        const double d = alpha - 1.0 / 3.0, c = 1.0 / sqrt(9.0 * d);
+    // Marsaglia-Tsang (alpha >= 1; boosted by u^(1/alpha) below 1), at most 64 rounds
+    // (each round accepts with probability > 0.95; reaching 64 has probability < 1e-80)
+    __device__ __forceinline__ double gamma(double alpha) {
+        const double boost = alpha < 1.0 ? pow(u(), 1.0 / alpha) : 1.0;
+        const double a = alpha < 1.0 ? alpha + 1.0 : alpha;
+        const double d = a - 1.0 / 3.0, c = 1.0 / sqrt(9.0 * d);
         double r = d;
         for (int it = 0; it < 64; it++) {
             const double x = normal();
             double v = 1.0 + c * x;
             if (v <= 0.0) continue;
             v = v * v * v;
-            const double u = uniform53();
-            if (u < 1.0 - 0.0331 * (x * x) * (x * x) ||
-                log(u) < 0.5 * x * x + d * (1.0 - v + log(v))) {
+            const double w = u();
+            if (w < 1.0 - 0.0331 * (x * x) * (x * x) || log(w) < 0.5 * x * x + d * (1.0 - v + log(v))) {
                 r = d * v;
                 break;
             }
         }
-        return uni(r);
-    }
-    // np.random.dirichlet(alpha) for 2 components
-    __device__ void dirichlet2(double a0, double a1, double &x0, double &x1) {
-        if (tape) {
-            x0 = tape_item();
-            x1 = tape_item();
-            return;
-        }
-        const double g0 = gamma(a0), g1 = gamma(a1);
-        const double s = g0 + g1;
-        x0 = g0 / s;
-        x1 = g1 / s;
+        return r * boost;
     }
 };
+
+__device__ __forceinline__ void Rng::dirichlet2(double a0, double a1, double &x0, double &x1) {
+    if (tape) {
+        x0 = tape_item();
+        x1 = tape_item();
+        return;
+    }
+    const int lane = threadIdx.x & 63;
+    LaneRng lr;
+    lr.init(*this, lane);
+    double g = 0.0;
+    if (lane < 2) g = lr.gamma(lane ? a1 : a0);
+    ctr++;
+    const double g0 = readlane_d(g, 0), g1 = readlane_d(g, 1);
+    const double s = g0 + g1;
+    x0 = uni(g0 / s);
+    x1 = uni(g1 / s);
+}
 
 // scipy.stats.dirichlet._logpdf for 2 components:
 //   -(sum gammaln(a) - gammaln(sum a)) + sum xlogy(a - 1, x)
@@ -208,16 +263,37 @@ __device__ __forceinline__ double dirichlet_logpdf2(double x0, double x1, double
     return -lnB + (t0 + t1);
 }
 
-// dirichlet_proposal on a pair w (sums to 1): new pair, log q, log q_back
+// dirichlet_proposal on a pair w (sums to 1): new pair, log q, log q_back.  q = exp(logpdf) and
+// log q as the reference (zone_sampling.py:537-569, util.py dirichlet_pdf); the ten lgamma / log
+// terms of the two densities run at once on lanes 0..9 (same functions, same arguments as
+// dirichlet_logpdf2), then exp and log on lanes 0 / 1.
 __device__ __forceinline__ void dirichlet_proposal2(Rng &rng, double w0, double w1, double prec, double &n0,
                                     double &n1, double &log_q, double &log_q_back) {
     const double a0 = 1.0 + prec * w0, a1 = 1.0 + prec * w1;
     rng.dirichlet2(a0, a1, n0, n1);
-    const double q = exp(dirichlet_logpdf2(n0, n1, a0, a1));
     const double b0 = 1.0 + prec * n0, b1 = 1.0 + prec * n1;
-    const double qb = exp(dirichlet_logpdf2(w0, w1, b0, b1));
-    log_q = uni(log(q));
-    log_q_back = uni(log(qb));
+    const int lane = threadIdx.x & 63;
+    const double args[10] = {a0, a1, a0 + a1, b0, b1, b0 + b1, n0, n1, w0, w1};
+    double arg = 1.0;
+#pragma unroll
+    for (int i = 0; i < 10; i++) arg = lane == i ? args[i] : arg;
+    double r;
+    if (lane < 6) r = lgamma(arg);
+    else r = log(arg);
+    double v[10];
+#pragma unroll
+    for (int i = 0; i < 10; i++) v[i] = readlane_d(r, i);
+    // -(sum gammaln(a) - gammaln(sum a)) + sum xlogy(a - 1, x)
+    const double tq0 = (a0 - 1.0) == 0.0 ? 0.0 : (a0 - 1.0) * v[6];
+    const double tq1 = (a1 - 1.0) == 0.0 ? 0.0 : (a1 - 1.0) * v[7];
+    const double tb0 = (b0 - 1.0) == 0.0 ? 0.0 : (b0 - 1.0) * v[8];
+    const double tb1 = (b1 - 1.0) == 0.0 ? 0.0 : (b1 - 1.0) * v[9];
+    const double lq = -((v[0] + v[1]) - v[2]) + (tq0 + tq1);
+    const double lb = -((v[3] + v[4]) - v[5]) + (tb0 + tb1);
+    const double e = exp(lane == 0 ? lq : lb);
+    const double l = log(lane == 0 ? readlane_d(e, 0) : readlane_d(e, 1));
+    log_q = uni(readlane_d(l, 0));
+    log_q_back = uni(readlane_d(l, 1));
 }
 
 // scipy.special.xlogy(a, x): 0 where a == 0, else a * log(x)
@@ -252,6 +328,26 @@ __device__ __forceinline__ double cell(const double (&w)[3], bool hz, bool hf, b
     double v = (w0 / sum) * L0 + (w1 / sum) * L1;
     if (C == 3) v = v + (w2 / sum) * (na ? 1.0 : (hf ? l2 : 0.0));
     return v;
+}
+
+// The reference cell from pre-normalised weights n (normalize_weights, model.py:436-452, computed
+// exactly as cell() computes them): the same operations in the same order as cell().
+template <int C>
+__device__ __forceinline__ double cell_nw(const double (&n)[3], bool hz, bool hf, bool na, double l0,
+                                          double l1, double l2) {
+    const double L0 = na ? 1.0 : l0;
+    const double L1 = na ? 1.0 : (hz ? l1 : 0.0);
+    double v = n[0] * L0 + n[1] * L1;
+    if (C == 3) v = v + n[2] * (na ? 1.0 : (hf ? l2 : 0.0));
+    return v;
+}
+
+// A table factor that keeps a 4-factor product of mantissas in the normal range: 0 or within
+// [2^-120, 2^120]; otherwise the gathers renormalise after every factor.
+__device__ __forceinline__ bool safe_cell(double v) { return v == 0.0 || (v >= 0x1p-120 && v <= 0x1p120); }
+
+__device__ __forceinline__ void *align16(void *p) {
+    return reinterpret_cast<void *>((reinterpret_cast<uintptr_t>(p) + 15) & ~(uintptr_t)15);
 }
 
 struct Chain {

@@ -34,51 +34,6 @@ namespace sbz {
 
 namespace {
 
-// Per-lane Philox stream: block (j, base, chain lo, chain hi ^ (lane + 1) << 24), key = seed.
-// `base` is the wave's counter when the phase started (the wave then advances it by one), j
-// counts the lane's draws in the phase.
-struct LaneRng {
-    uint32_t k0, k1, base, c2, c3, j;
-    __device__ void init(const Rng &r, int lane) {
-        k0 = r.key0;
-        k1 = r.key1;
-        base = (uint32_t)r.ctr;
-        c2 = (uint32_t)r.chain;
-        c3 = (uint32_t)(r.chain >> 32) ^ ((uint32_t)(lane + 1) << 24);
-        j = 0;
-    }
-    __device__ double u() {
-        uint32_t c[4] = {j++, base, c2, c3};
-        philox4x32_10(c, k0, k1);
-        const uint64_t bits = ((uint64_t)c[0] << 32) | c[1];
-        return (double)(bits >> 11) * 0x1p-53;
-    }
-    __device__ double normal() {
-        const double u1 = 1.0 - u();
-        const double u2 = u();
-        return sqrt(-2.0 * log(u1)) * cospi(2.0 * u2);
-    }
-    // Marsaglia-Tsang (alpha >= 1; boosted by u^(1/alpha) below 1), at most 64 rounds
-    __device__ double gamma(double alpha) {
-        const double boost = alpha < 1.0 ? pow(u(), 1.0 / alpha) : 1.0;
-        const double a = alpha < 1.0 ? alpha + 1.0 : alpha;
-        const double d = a - 1.0 / 3.0, c = 1.0 / sqrt(9.0 * d);
-        double r = d;
-        for (int it = 0; it < 64; it++) {
-            const double x = normal();
-            double v = 1.0 + c * x;
-            if (v <= 0.0) continue;
-            v = v * v * v;
-            const double w = u();
-            if (w < 1.0 - 0.0331 * (x * x) * (x * x) || log(w) < 0.5 * x * x + d * (1.0 - v + log(v))) {
-                r = d * v;
-                break;
-            }
-        }
-        return r * boost;
-    }
-};
-
 // The component likelihoods and normalised weights of observation (s, f) (update_component_
 // likelihoods model.py:230-249 with NA -> 1 for every component; normalize_weights :436-452).
 template <int C>

@@ -127,3 +127,60 @@ def test_philox_carried_prior_matches_full_prior(gpu_available):
                           int(fx["n_zones"]), True)
     np.testing.assert_allclose(s["prior"], full, rtol=1e-12)
     assert np.any(s["prior"] != fx["init_prior"])  # the prior moved
+
+
+@pytest.mark.parametrize("N,F,S,Z,Fam,inh", [
+    (3000, 40, 12, 3, 3, True),    # two batches of observation chunks (Np = 4096)
+    (700, 30, 40, 2, 2, True),     # S + 1 > 32: observation bytes hold x, not x * 8
+    (2000, 50, 10, 8, 4, True),    # the bench shape's site count / zones / families
+    (300, 20, 5, 2, 0, False),     # no inheritance (C = 2)
+])
+def test_philox_large_shapes_carried_ll(gpu_available, N, F, S, Z, Fam, inh):
+    """Philox runs on shapes the golden tapes do not reach: the incrementally carried ll equals a
+    fresh full evaluation (likelihood kernel) within 1e-9 after every operator type ran, zones
+    stay disjoint and within bounds, and parameters stay normalised."""
+    import random
+    import torch
+    from scipy.spatial import Delaunay
+    from contact_zones_amd import packing
+    from contact_zones_amd.likelihood import LikelihoodEngine
+    from contact_zones_amd.mcmc import InitialSamples
+    from contact_zones_amd.sampler import ChainState, Sampler
+    rng = np.random.default_rng(N + F + S)
+    obs = rng.integers(0, S, size=(N, F)).astype(np.int8)
+    obs[rng.random((N, F)) < 0.03] = -1
+    fam = rng.integers(0, max(Fam, 1), size=N).astype(np.uint8) if Fam else np.full(N, 255, np.uint8)
+    if Fam:
+        fam[rng.random(N) < 0.1] = 255
+    indptr, indices = Delaunay(rng.random((N, 2))).vertex_neighbor_vertices
+    order = [np.sort(indices[indptr[i]:indptr[i + 1]]) for i in range(N)]
+    indices = np.concatenate(order).astype(np.int32)
+    indptr = indptr.astype(np.int32)
+    states = np.ones((F, S), bool)
+    init = InitialSamples(packing.obs_to_features(obs, S), states, indptr, indices,
+                          packing.index_to_groups(fam, Fam) if Fam else None, Z, 5, inh, None,
+                          random.Random(11))
+    B = 6
+    zos = np.stack([packing.zones_to_zone_of_site(init.zones(), N) for _ in range(B)])
+    w = rng.dirichlet(np.ones(3 if inh else 2), size=(B, F))
+    pg = rng.dirichlet(np.ones(S), size=(B, F))
+    pz = rng.dirichlet(np.ones(S), size=(B, Z, F))
+    pf = rng.dirichlet(np.ones(S), size=(B, Fam, F)) if inh else None
+    eng = LikelihoodEngine(obs, fam, S, Z, Fam, inh)
+    ops = {"shrink_zone": 0.1, "grow_zone": 0.1, "swap_zone": 0.05, "alter_weights": 0.3,
+           "alter_p_global": 0.15, "alter_p_zones": 0.2, "alter_p_families": 0.1 if inh and Fam else 0.0}
+    smp = Sampler(eng, states, indptr, indices, ops, [15, 40, 20, 20], 3)
+    st = ChainState(eng, zos, w, pg, pz, pf)
+    out = smp.run(st, 1500, 40, 0.85, seed=5)
+    torch.cuda.synchronize()
+    assert out["status"].cpu().numpy().tolist() == [0] * B
+    acc = st.accepted.cpu().numpy()
+    assert np.all(acc[:, :7].sum(0)[[0, 1, 3, 4, 5]] > 0)  # zone and parameter moves accepted
+    s = st.to_numpy()
+    fresh = st.refresh_ll().cpu().numpy()
+    assert np.max(np.abs(s["ll"] - fresh) / np.abs(fresh)) <= REL_TOL
+    for b in range(B):
+        sizes = np.bincount(s["zone_of_site"][b][s["zone_of_site"][b] < 255], minlength=Z)
+        assert np.all(sizes >= 3) and np.all(sizes <= 40)
+    np.testing.assert_allclose(s["w"].sum(-1), 1.0, rtol=1e-12)
+    np.testing.assert_allclose(s["p_zones"].sum(-1), 1.0, rtol=1e-12)
