@@ -153,7 +153,9 @@ int sbz_open(int device, const sbz_dims *dims, const int8_t *obs, const uint8_t 
         }
     }
     if (const char *v = getenv("SBZ_LIK_KERNEL"))
-        ctx->lik_kernel = strcmp(v, "zoned") == 0 ? 2 : (strcmp(v, "db") == 0 ? 3 : 1);
+        ctx->lik_kernel = strcmp(v, "zoned") == 0 ? 2 : strcmp(v, "db") == 0 ? 3 : strcmp(v, "ws") == 0 ? 4 : 1;
+    if (const char *v = getenv("SBZ_WS_NG")) ctx->ws_ng = std::min(2, std::max(1, atoi(v)));
+    if (const char *v = getenv("SBZ_WS_NB")) ctx->ws_nb = std::min(2, std::max(1, atoi(v)));
     if (const char *v = getenv("SBZ_LIK_TASKS")) ctx->tasks_per_cu = std::max(1, atoi(v));
     if (const char *v = getenv("SBZ_LIK_ZSPL")) {
         const int z = atoi(v);

@@ -67,7 +67,11 @@ struct sbz_ctx {
     double *d_gc_f = nullptr;     // [Fam][F][S] of p_families
     int zspl = 8;          // zoned sites per lane and chunk of the zone-sparse kernel
     int lik_kernel = 1;    // SBZ_LIK_KERNEL: 1 dense (default), 2 zone-sparse ("zoned"),
-                           // 3 dense double-buffered ("db", where the table fits 4 KiB)
+                           // 3 dense double-buffered ("db", where the table fits 4 KiB),
+                           // 4 wave-specialised builder + gatherers ("ws", same condition)
+    int ws_ng = 2;         // SBZ_WS_NG: gatherer waves of the wave-specialised kernel (1 or 2)
+    int ws_nb = 2;         // SBZ_WS_NB: its builder waves (1 or 2; 2 split the zone-class slots)
+    const void *mix_occ_fn = nullptr;  // the kernel mix_occ was queried for
     int tasks_per_cu = 0;  // SBZ_LIK_TASKS: single-wave tasks per CU per launch (0: occupancy)
     int mix_occ = 0;       // resident mixture-kernel waves per CU (queried at first launch)
     int n_cu = 256;        // compute units of the device

@@ -75,8 +75,9 @@ __device__ __forceinline__ void wave_lds_sync() {
 // store), the storing lane waits vmcnt(0), then adds to the chain's ticket (agent atomic); the
 // lane whose add returned W-1 reads every partial with sc1 loads.  An agent-scope acq_rel fence
 // here would write back / invalidate caches once per task and cost ~2x the kernel.
-__device__ __forceinline__ void finish_chain(const LikArgs &a, int b, double tot) {
-    if (threadIdx.x != 0) return;
+__device__ __forceinline__ void finish_chain(const LikArgs &a, int b, double tot,
+                                             bool leader = threadIdx.x == 0) {
+    if (!leader) return;
     if (a.W == 1) {
         a.out[b] = tot;
         return;
@@ -182,15 +183,20 @@ struct MixParams {
 
 // Normalised weights are computed for NWC features at a time (MixTable::prep) and kept in LDS.
 constexpr int NWC = 32;
-constexpr int NW_PER_F = 12;  // [h = hz | hf << 1][c]
+// Per feature, h = hz | hf << 1: (c0, c1) of h at [2h, 2h + 1]; c2 of h at 8 + 2 * hz + hf, so
+// c2 of (h, h + 2) is one 16-B pair.  Every read of build() is a ds_read_b128.
+constexpr int NW_PER_F = 12;
 
 // Double-buffered layout (DB, lik_mixture_db_kernel): two tables of DB_TAB_BYTES each, so the
 // table of feature f+1 is built while feature f is gathered; every zone class has FR + 1 family
 // rows (rows >= Fam unused) so the build has no branches.
 constexpr int DB_TAB_BYTES = 4096;
 
-template <int C, int FR, bool DB = false>
+template <int C, int FR, bool DB = false, int SLOT = -1>
 struct MixTable {
+    // SLOT >= 0: this wave loads and builds only zone-class slot SLOT (i = SLOT of the ZR
+    // slots); the wave-specialised kernel splits the table between two builder waves this way.
+    static constexpr bool has(int i) { return SLOT < 0 || i == SLOT; }
     static constexpr int RPZ_DB = (C == 3) ? FR + 1 : 1;  // rows per zone class (DB layout)
     int lane, S, S1, FamC, RPZ, Z, Fam, ncls, G, lx, lg, row_bytes;
     uint32_t lxc;
@@ -208,7 +214,7 @@ struct MixTable {
     __device__ __forceinline__ MixTable(const LikArgs &a, unsigned char *lds_, int b,
                                         double *tab0 = nullptr, double *tab1 = nullptr)
         : lds(lds_) {
-        lane = threadIdx.x;
+        lane = threadIdx.x % WAVE;
         S = a.S;
         S1 = a.S + 1;
         FamC = a.FamC;
@@ -226,7 +232,8 @@ struct MixTable {
         tab = DB ? tab0 : reinterpret_cast<double *>(lds);
         double *dyn = DB ? reinterpret_cast<double *>(lds) : tab + (ncls + 1) * S1;
         junk = dyn + lane;
-        nwt = dyn + WAVE;
+        // nwt 16-B aligned (one 8-B pad slot in the LDS budget)
+        nwt = dyn + WAVE + (DB ? 0 : (((ncls + 1) * S1) & 1));
         nwf0 = -(1 << 30);
         nwbad = 0;
         hz0 = lg > 0 ? 1 : 0;
@@ -249,7 +256,8 @@ struct MixTable {
         const uint32_t fo = (uint32_t)f * (uint32_t)S;
         r.g = pgb[fo + lxc];
 #pragma unroll
-        for (int i = 0; i < ZR; i++) r.z[i] = zbase[fo + pzo[i]];
+        for (int i = 0; i < ZR; i++)
+            if (has(i)) r.z[i] = zbase[fo + pzo[i]];
 #pragma unroll
         for (int fm = 0; fm < FR; fm++)
             r.fm[fm] = fbase[(uint32_t)min(fm, max(Fam - 1, 0)) * zfs + fo + lxc];
@@ -280,11 +288,13 @@ struct MixTable {
             ok &= (int)tame(n[hz][0]) & (int)tame(n[hz][1]) & (int)tame(n[hz][2]);
         }
         lds_phase();  // earlier features' reads of nwt are done
-        double *o = nwt + k * NW_PER_F + 6 * hp;  // h = 2hp + hz -> offset 3h
+        double *o = nwt + k * NW_PER_F;  // h = 2hp + hz
 #pragma unroll
-        for (int hz = 0; hz < 2; hz++)
-#pragma unroll
-            for (int c = 0; c < 3; c++) o[3 * hz + c] = n[hz][c];
+        for (int hz = 0; hz < 2; hz++) {
+            o[2 * (2 * hp + hz)] = n[hz][0];
+            o[2 * (2 * hp + hz) + 1] = n[hz][1];
+            o[8 + 2 * hz + hp] = n[hz][2];
+        }
         nwbad = __ballot(!ok);
         nwf0 = f0;
         lds_phase();
@@ -296,7 +306,8 @@ struct MixTable {
         const int k = f - nwf0;
         int ok = (int)tame(r.g);
 #pragma unroll
-        for (int i = 0; i < ZR; i++) ok &= (int)tame(r.z[i]);
+        for (int i = 0; i < ZR; i++)
+            if (has(i)) ok &= (int)tame(r.z[i]);
 #pragma unroll
         for (int fm = 0; fm < FR; fm++) ok &= (int)tame(r.fm[fm]);
 #if SBZ_ABLATE & 4
@@ -306,16 +317,26 @@ struct MixTable {
         // 1. normalised weights from nwt.  Slot i >= 1 holds zone classes only (zc >= G >= 1):
         //    wave-uniform weights of h = 1 (no family) and h = 3 (family).  Slot 0 mixes zc = 0
         //    (lanes lg == 0, h = 0 / 2) and zone classes (h = 1 / 3).
-        const double *nk = nwt + k * NW_PER_F;
+        //    Six 16-B reads: (c0, c1) of each h, and c2 of (h, h + 2) as one pair.
+        const double *nk = static_cast<const double *>(__builtin_assume_aligned(nwt + k * NW_PER_F, 16));
+        auto pair = [&](int at) { return *reinterpret_cast<const double2 *>(nk + at); };
         double u[2][3], p[2][3];
+        const double2 cu = pair(10), cp = pair(8 + 2 * hz0);  // c2 of (h, h + 2), hz = 1 / hz0
 #pragma unroll
-        for (int hf = 0; hf < 2; hf++)
+        for (int hf = 0; hf < 2; hf++) {
+            if (C == 2 && hf == 1) {
 #pragma unroll
-            for (int cc = 0; cc < 3; cc++) {
-                const bool used = !(C == 2 && (hf == 1 || cc == 2));
-                u[hf][cc] = used ? nk[3 * (1 + 2 * hf) + cc] : 0.0;
-                p[hf][cc] = used ? nk[3 * (hz0 + 2 * hf) + cc] : 0.0;
+                for (int cc = 0; cc < 3; cc++) u[hf][cc] = p[hf][cc] = 0.0;
+                continue;
             }
+            const double2 a = pair(2 * (1 + 2 * hf)), q = pair(2 * (hz0 + 2 * hf));
+            u[hf][0] = a.x;
+            u[hf][1] = a.y;
+            u[hf][2] = C == 3 ? (hf ? cu.y : cu.x) : 0.0;
+            p[hf][0] = q.x;
+            p[hf][1] = q.y;
+            p[hf][2] = C == 3 ? (hf ? cp.y : cp.x) : 0.0;
+        }
         // 2. table: the reference cell (n0*l0 + n1*l1) + n2*l2 for every class.  Branch-free:
         //    lanes without an entry write to their junk slot.  The family term of a class
         //    without family is n2 * l2 = (w2 * 0 / sum) * (0 or 1): +0 for tame inputs, left
@@ -330,6 +351,7 @@ struct MixTable {
 #if SBZ_ABLATE & 2
             break;  // diagnostic build: skip the table build
 #endif
+            if (!has(i)) continue;
             const int zc = lg + i * G;
             const bool valid = (lane < G * S1) && (zc <= Z);
             const double n00 = i == 0 ? p[0][0] : u[0][0], n01 = i == 0 ? p[0][1] : u[0][1];
@@ -626,6 +648,201 @@ __global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_db_kernel(Lik
     v = v + (double)e * LN2;
     const double tot = wave_sum(v);
     finish_chain(a, b, tot);
+}
+
+// ---------------------------------------------------------------------------------------
+// Dense mixture kernel, wave-specialised (SBZ_LIK_KERNEL=ws; the default where the table fits
+// DB_TAB_BYTES and obs hold x*8).  A task (chain b, features [fa, fb)) is one workgroup of
+// 1 + NG waves on separate SIMDs:
+//   wave 0      the builder: loads the parameters and builds feature f + 1's table (MixTable,
+//               DB row layout) into one of two static LDS buffers, plus its `wide` flag;
+//   waves 1..NG the gatherers: each owns SPL sites per lane of the chunk and multiplies feature
+//               f's cells out of the other buffer.
+// One s_barrier per feature hands the buffers over: the builder writes buffer (k+1)&1 in step k,
+// which the gatherers last read in step k-1, before the previous barrier.  Table build and
+// gathers, which the single-wave kernel runs back to back, overlap on two SIMDs, and each role
+// keeps only its own registers live (the gatherers hold no parameters, the builder no sites).
+// ---------------------------------------------------------------------------------------
+#ifndef SBZ_WS_WAVES
+#define SBZ_WS_WAVES 4  // launch bound: minimum waves per SIMD of the wave-specialised kernel
+#endif
+
+// s_barrier after this wave's LDS operations completed; a compiler memory barrier on both sides
+// (the bare builtin is not one) and, unlike __syncthreads(), no vmcnt drain: prefetched global
+// loads stay in flight.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// bytes of one builder's [junk | nwt] region (16-B multiple)
+__host__ __device__ constexpr size_t mix_db_lds_bytes_d() { return ((size_t)WAVE + 2 + (size_t)NWC * NW_PER_F) * 8; }
+
+template <int C, int SPL, int FR, int NG, int NB>
+__global__ __launch_bounds__(WAVE *(NB + NG), SBZ_WS_WAVES) void lik_mixture_ws_kernel(LikArgs a) {
+    __shared__ __attribute__((aligned(16))) double tab0[DB_TAB_BYTES / 8];
+    __shared__ __attribute__((aligned(16))) double tab1[DB_TAB_BYTES / 8];
+    __shared__ int wflag[2][NB];
+    __shared__ double red[NG];
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];  // builder: junk | nwt
+    constexpr int NO = SPL / 4;  // observation words (4 sites each) per lane per feature
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
+    const int lane = threadIdx.x % WAVE;
+    const int b = blockIdx.y;
+    const int fa = blockIdx.x * a.fpw;
+    const int fb = min(a.F, fa + a.fpw);
+    const int nf = fb - fa;
+    const int chunk = NG * SPL * WAVE;
+
+    auto builder = [&](auto slot) {
+        constexpr int SL = decltype(slot)::value;
+        constexpr int BW = SL < 0 ? 0 : SL;  // builder index
+        MixTable<C, FR, true, SL> t(a, lds + BW * mix_db_lds_bytes_d(), b, tab0, tab1);
+        MixParams<C, FR> P;
+        for (int c0 = 0; c0 < a.Np; c0 += chunk) {
+            t.load(fa, P);
+            if (fa < t.nwf0 || fa >= t.nwf0 + NWC) t.prep(fa, fb);
+            bool wide = t.build(P, fa, tab0);
+            t.load(min(fa + 1, fb - 1), P);
+            if (t.lane == 0) wflag[0][BW] = wide;
+            lds_barrier();
+            for (int k = 0; k < nf; k++) {
+                const int fn = fa + k + 1;
+                if (fn < fb) {
+                    if (fn < t.nwf0 || fn >= t.nwf0 + NWC) t.prep(fn, fb);
+                    wide = t.build(P, fn, (k & 1) ? tab0 : tab1);
+                    t.load(min(fn + 1, fb - 1), P);
+                    if (t.lane == 0) wflag[(k + 1) & 1][BW] = wide;
+                }
+                lds_barrier();
+            }
+        }
+        lds_barrier();  // the gatherers' partials
+    };
+    if (wv < NB) {
+        if (NB == 1) builder(std::integral_constant<int, -1>());
+        else if (wv == 0) builder(std::integral_constant<int, 0>());
+        else builder(std::integral_constant<int, 1>());
+        return;
+    }
+
+    // ------------------------------ gatherers ------------------------------
+    const int g = wv - NB;
+    auto wide_of = [&](int j) {
+        int w = wflag[j][0];
+#pragma unroll
+        for (int i = 1; i < NB; i++) w |= wflag[j][i];
+        return w != 0;
+    };
+    const int Z = a.Z;
+    const int RPZ = MixTable<C, FR, true>::RPZ_DB;
+    static_assert(NB == 1 || ZR == 2, "two builder waves split the ZR = 2 zone-class slots");
+    const int ncls = (Z + 1) * RPZ;
+    const uint32_t row_bytes = (uint32_t)(a.S + 1) * 8u;
+    double m[4] = {1.0, 1.0, 1.0, 1.0};  // four independent product chains
+    int e = 0;
+    uint32_t base2[SPL / 2];  // per-site class row offsets (bytes, < DB_TAB_BYTES), two per register
+    uint32_t O[2][NO];        // observations of the feature being gathered / the next one
+
+    auto load_obs = [&](int f, int s0, uint32_t (&o)[NO]) {
+        const uint32_t *op = reinterpret_cast<const uint32_t *>(a.obs_fm + (size_t)f * a.Np + s0);
+#pragma unroll
+        for (int k = 0; k < NO; k++) o[k] = op[(uint32_t)(lane + 64 * k)];
+    };
+    auto cell = [&](auto jc, uint32_t off) -> double {
+        constexpr int J = decltype(jc)::value;
+        const unsigned char *tb = reinterpret_cast<const unsigned char *>(J ? tab1 : tab0);
+        return *reinterpret_cast<const double *>(tb + off);
+    };
+    auto gather = [&](auto jc, const uint32_t (&ob)[NO], bool wide) {
+        if (SBZ_ABLATE & 1) return;
+        if (!wide) {
+#pragma unroll
+            for (int k = 0; k < NO; k++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const uint32_t bw = base2[2 * k + (j >> 1)];
+                    const uint32_t bs = (j & 1) ? (bw >> 16) : (bw & 0xffffu);
+                    m[k & 3] *= cell(jc, bs + ((ob[k] >> (8 * j)) & 0xffu));
+                    // <= 8 reads in flight: the group's products are inputs of the barrier
+                    if (j == 3 && (k & 1))
+                        asm volatile("" : "+v"(m[0]), "+v"(m[1]), "+v"(m[2]), "+v"(m[3])::"memory");
+                }
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                if (q < NO) renorm(m[q], e);
+        } else {
+            // untamed inputs: renormalise after every factor (exact for any normal double)
+#pragma unroll
+            for (int k = 0; k < NO; k++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    uint32_t bw = base2[2 * k + (j >> 1)];
+                    asm volatile("" : "+v"(bw));
+                    const uint32_t bs = (j & 1) ? (bw >> 16) : (bw & 0xffffu);
+                    m[0] *= cell(jc, bs + ((ob[k] >> (8 * j)) & 0xffu));
+                    renorm(m[0], e);
+                }
+        }
+    };
+
+    for (int c0 = 0; c0 < a.Np; c0 += chunk) {
+        const int s0 = c0 + g * SPL * WAVE;  // this gatherer's first position
+        {
+            const uint8_t *zb = a.zone + (size_t)b * a.N;
+            uint32_t zs[SPL];
+            int4 pv[NO];
+            uint32_t fw[NO];
+#pragma unroll
+            for (int k = 0; k < NO; k++) {
+                const uint32_t p0 = (uint32_t)(s0 + 4 * lane + 256 * k);  // < Np (arrays padded)
+                pv[k] = *reinterpret_cast<const int4 *>(a.perm + p0);
+                fw[k] = *reinterpret_cast<const uint32_t *>(a.famc + p0);
+            }
+#pragma unroll
+            for (int k = 0; k < NO; k++) {
+                zs[4 * k + 0] = zb[(uint32_t)pv[k].x];
+                zs[4 * k + 1] = zb[(uint32_t)pv[k].y];
+                zs[4 * k + 2] = zb[(uint32_t)pv[k].z];
+                zs[4 * k + 3] = zb[(uint32_t)pv[k].w];
+            }
+#pragma unroll
+            for (int i = 0; i < SPL; i++) {
+                const int pos = s0 + 4 * lane + 256 * (i / 4) + (i % 4);
+                const int z = (int)zs[i];
+                const int fc = (int)((fw[i / 4] >> (8 * (i % 4))) & 0xffu);
+                const int cls = pos < a.N ? ((z < Z ? z + 1 : 0) * RPZ + fc) : ncls;
+                const uint32_t off = (uint32_t)cls * row_bytes;
+                if (i & 1) base2[i >> 1] |= off << 16;
+                else base2[i >> 1] = off;
+            }
+        }
+        load_obs(fa, s0, O[0]);
+        lds_barrier();  // feature fa's table
+        int k = 0;
+        for (; k + 1 < nf; k += 2) {
+            load_obs(fa + k + 1, s0, O[1]);
+            gather(std::integral_constant<int, 0>(), O[0], wide_of(0));
+            lds_barrier();
+            load_obs(min(fa + k + 2, fb - 1), s0, O[0]);
+            gather(std::integral_constant<int, 1>(), O[1], wide_of(1));
+            lds_barrier();
+        }
+        if (k < nf) {  // odd tail: buffer 0
+            gather(std::integral_constant<int, 0>(), O[0], wide_of(0));
+            lds_barrier();
+        }
+    }
+    double v = (log(m[0]) + log(m[1])) + (log(m[2]) + log(m[3]));
+    v = v + (double)e * LN2;
+    const double tot = wave_sum(v);
+    if (lane == 0) red[g] = tot;
+    lds_barrier();
+    if (g == 0) {
+        double s = red[0];
+#pragma unroll
+        for (int i = 1; i < NG; i++) s += red[i];
+        finish_chain(a, b, s, lane == 0);
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1021,6 +1238,29 @@ const void *mix_db_kernel(int C, int fr, int spl) {
     return mix_db_kernel_x<2, 4>(spl);
 }
 
+// The wave-specialised kernel for SPL sites per gatherer lane (spl / ng), NG gatherers and NB
+// builders.
+template <int C, int FR, int NG, int NB>
+const void *mix_ws_kernel_x(int spl) {
+    switch (spl) {
+        case 4: return reinterpret_cast<const void *>(&lik_mixture_ws_kernel<C, 4, FR, NG, NB>);
+        case 8: return reinterpret_cast<const void *>(&lik_mixture_ws_kernel<C, 8, FR, NG, NB>);
+        case 16: return reinterpret_cast<const void *>(&lik_mixture_ws_kernel<C, 16, FR, NG, NB>);
+        default: return reinterpret_cast<const void *>(&lik_mixture_ws_kernel<C, 32, FR, NG, NB>);
+    }
+}
+
+template <int C, int FR>
+const void *mix_ws_kernel_c(int spl, int ng, int nb) {
+    if (nb == 2) return ng == 1 ? mix_ws_kernel_x<C, FR, 1, 2>(spl) : mix_ws_kernel_x<C, FR, 2, 2>(spl);
+    return ng == 1 ? mix_ws_kernel_x<C, FR, 1, 1>(spl) : mix_ws_kernel_x<C, FR, 2, 1>(spl);
+}
+
+const void *mix_ws_kernel(int C, int fr, int spl, int ng, int nb) {
+    if (C == 3) return fr == 4 ? mix_ws_kernel_c<3, 4>(spl, ng, nb) : mix_ws_kernel_c<3, 8>(spl, ng, nb);
+    return mix_ws_kernel_c<2, 4>(spl, ng, nb);
+}
+
 template <int C, int FR, bool XS8>
 const void *mix_kernel_x(bool zoned, int spl, int zspl) {
     if (zoned) {
@@ -1066,6 +1306,9 @@ void configure_mix_x(std::vector<const void *> &v) {
     v.push_back(reinterpret_cast<const void *>(&lik_mixture_kernel<C, 16, FR, XS8>));
     v.push_back(reinterpret_cast<const void *>(&lik_mixture_kernel<C, 32, FR, XS8>));
     if (XS8) {
+        for (int nb = 1; nb <= 2; nb++)
+            for (int ng = 1; ng <= 2; ng++)
+                for (int spl = 4; spl <= 32; spl *= 2) v.push_back(mix_ws_kernel(C, FR, spl, ng, nb));
         v.push_back(reinterpret_cast<const void *>(&lik_mixture_db_kernel<C, 4, FR>));
         v.push_back(reinterpret_cast<const void *>(&lik_mixture_db_kernel<C, 8, FR>));
         v.push_back(reinterpret_cast<const void *>(&lik_mixture_db_kernel<C, 16, FR>));
@@ -1102,11 +1345,13 @@ size_t mix_lds_bytes(const sbz_dims &d, int C) {
     const size_t S1 = (size_t)d.n_states + 1;
     const size_t Fam = C == 3 ? (size_t)d.n_families : 0;
     const size_t ncls = (size_t)(d.n_zones + 1) * (Fam + 1);
-    return ((ncls + 1) * S1 + WAVE + (size_t)NWC * NW_PER_F) * 8;
+    return ((ncls + 1) * S1 + WAVE + 1 + (size_t)NWC * NW_PER_F) * 8;
 }
 
 // dynamic LDS of lik_mixture_db_kernel (the two tables are static): junk + nwt
-size_t mix_db_lds_bytes() { return ((size_t)WAVE + (size_t)NWC * NW_PER_F) * 8; }
+size_t mix_db_lds_bytes() { return ((size_t)WAVE + 2 + (size_t)NWC * NW_PER_F) * 8; }
+// dynamic LDS of lik_mixture_ws_kernel: junk + nwt per builder wave
+size_t mix_ws_lds_bytes() { return 2 * mix_db_lds_bytes(); }
 
 MixPlan plan_mixture(const sbz_dims &d, int C, bool xs8 = false) {
     MixPlan p;
@@ -1195,7 +1440,8 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
     a.pf = pf;
 
     MixPlan plan;
-    bool zoned = false;
+    bool zoned = false, ws = false;
+    int block = WAVE;
     const void *mix_fn = nullptr;
     size_t lds = 0;
     int rc;
@@ -1206,6 +1452,10 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
             // (the <C=3, SPL=32, FR=8> instantiation of the double-buffered kernel spills)
             const bool db = plan.db && !zoned && ctx->lik_kernel == 3 &&
                             !(ctx->C == 3 && plan.fr == 8 && ctx->spl == 32);
+            // wave-specialised: a builder wave and ng gatherer waves of spl / ng sites per lane
+            int ng = ctx->ws_ng;
+            while (ng > 1 && ctx->spl / ng < 4) ng--;
+            ws = plan.db && !zoned && ctx->lik_kernel == 4;
             if (zoned) {
                 rc = ensure(ctx, ctx->zl, (size_t)B * d.n_sites * sizeof(uint32_t));
                 if (rc) return rc;
@@ -1218,15 +1468,21 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
                 a.nzs = static_cast<const int *>(ctx->nzs.ptr);
                 a.cnt = ctx->d_cnt;
             }
-            lds = db ? mix_db_lds_bytes() : mix_lds_bytes(d, ctx->C);
-            mix_fn = db ? mix_db_kernel(ctx->C, plan.fr, ctx->spl)
-                        : mix_kernel(ctx->C, plan.fr, ctx->xs8 != 0, zoned, ctx->spl, ctx->zspl);
+            lds = ws ? mix_ws_lds_bytes() : db ? mix_db_lds_bytes() : mix_lds_bytes(d, ctx->C);
+            if (ws) {
+                block = WAVE * (ctx->ws_nb + ng);
+                mix_fn = mix_ws_kernel(ctx->C, plan.fr, ctx->spl / ng, ng, ctx->ws_nb);
+            } else {
+                mix_fn = db ? mix_db_kernel(ctx->C, plan.fr, ctx->spl)
+                            : mix_kernel(ctx->C, plan.fr, ctx->xs8 != 0, zoned, ctx->spl, ctx->zspl);
+            }
             // Long tasks: one resident round of single-wave tasks (occupancy x CUs) over the
             // launch, so every wave streams its features with no tail of late tasks.
-            if (ctx->mix_occ == 0) {
+            if (ctx->mix_occ == 0 || ctx->mix_occ_fn != mix_fn) {
                 int occ = 0;
-                hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, mix_fn, WAVE, lds);
+                hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, mix_fn, block, lds);
                 ctx->mix_occ = (e == hipSuccess && occ > 0) ? occ : 8;
+                ctx->mix_occ_fn = mix_fn;
             }
             const int per_cu = ctx->tasks_per_cu > 0 ? ctx->tasks_per_cu : ctx->mix_occ;
             const int W = std::max(1, std::min((F + 1) / 2, (ctx->n_cu * per_cu + B - 1) / B));
@@ -1277,7 +1533,7 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
         else lik_mixture_generic_kernel<2><<<grid, WAVE, 0, st>>>(a);
     } else {
         void *args[] = {&a};
-        hipError_t e = hipLaunchKernel(mix_fn, grid, dim3(WAVE), args, lds, st);
+        hipError_t e = hipLaunchKernel(mix_fn, grid, dim3(block), args, lds, st);
         if (e != hipSuccess) return hip_fail(ctx, e, "mixture kernel launch");
     }
     hipError_t e = hipGetLastError();

@@ -35,14 +35,20 @@ def _assert_close(got, ref, tol=REL_TOL):
 
 
 # Mixture-mode kernels: "dense" = every site gathered from the table (default), "db" = the
-# double-buffered dense kernel (where the table fits 4 KiB), "zoned" = zone-sparse counts kernel
-# (SBZ_LIK_KERNEL is read when a context opens).
-MODES = [("mixture", "dense"), ("mixture", "db"), ("mixture", "zoned"), ("source", "dense")]
+# double-buffered dense kernel (where the table fits 4 KiB), "ws" / "ws1" = the wave-specialised
+# kernel (a builder wave + 2 / 1 gatherer waves, same condition), "zoned" = zone-sparse counts
+# kernel (SBZ_LIK_KERNEL and SBZ_WS_NG are read when a context opens).
+MODES = [("mixture", "dense"), ("mixture", "db"), ("mixture", "ws"), ("mixture", "ws1"),
+         ("mixture", "zoned"), ("source", "dense")]
 
 
 @pytest.fixture
 def lik_kernel(request, monkeypatch):
-    monkeypatch.setenv("SBZ_LIK_KERNEL", request.param)
+    kernel = request.param
+    if kernel.startswith("ws"):
+        monkeypatch.setenv("SBZ_WS_NG", "1" if kernel == "ws1" else "2")
+        kernel = "ws"
+    monkeypatch.setenv("SBZ_LIK_KERNEL", kernel)
     return request.param
 
 
