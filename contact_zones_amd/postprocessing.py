@@ -65,3 +65,43 @@ def contribution_per_area(mcmc_sampler, batch=4096):
     stats["sample_prior_single_zones"] = [list(r) for r in pr]
     stats["sample_posterior_single_zones"] = [list(a + b) for a, b in zip(lh, pr)]
     smp.statistics = stats
+
+
+def match_areas(samples):
+    """sbayes/postprocessing.py:205-268: relabel every logged sample's zones so that they agree
+    best with the running sum of the relabelled earlier samples.  The reference scores every
+    permutation p of the zone labels as sum(s_sum * s[:, p]) and keeps the first maximum in
+    itertools.permutations order; that score is sum_z M[z, p[z]] with the Z x Z overlap matrix
+    M = s_sum^T s, so all Z! scores come from one gather of M per sample.  The counts are
+    integers, so the scores (and their ties) are exact as in the reference."""
+    from itertools import permutations
+    zones = np.asarray([np.asarray(s) for s in samples["sample_zones"]])   # [n][Z][N]
+    n, Z, N = zones.shape
+    perms = np.array(list(permutations(range(Z))), dtype=np.int64)          # [Z!][Z]
+    s_sum = np.zeros((Z, N))                                                 # zone-major
+    matching = []
+    rows = np.arange(Z)
+    for s in zones.astype(np.float64):
+        M = s_sum @ s.T                                                      # M[a][b] = sum_site s_sum[a] s[b]
+        score = M[rows[None, :], perms].sum(axis=1)
+        best = perms[int(np.argmax(score))]
+        matching.append(best)
+        s_sum += s[best]
+    for key in ("sample_zones", "sample_p_zones"):
+        samples[key] = [samples[key][i][:][m] if key == "sample_zones" else samples[key][i][m]
+                        for i, m in enumerate(matching[:len(samples[key])])]
+    for key in ("sample_lh_single_zones", "sample_prior_single_zones", "sample_posterior_single_zones"):
+        samples[key] = [[samples[key][i][j] for j in m] for i, m in enumerate(matching[:len(samples[key])])]
+    return samples
+
+
+def rank_areas(samples):
+    """sbayes/postprocessing.py:316-363: order the zones of every sample by their mean posterior
+    contribution (sample_posterior_single_zones), largest first (np.argsort(-mean))."""
+    to_rank = np.mean(np.asarray(samples["sample_posterior_single_zones"]), axis=0)
+    ranked = np.argsort(-to_rank)
+    samples["sample_zones"] = [np.asarray(z)[ranked] for z in samples["sample_zones"]]
+    for key in ("sample_lh_single_zones", "sample_prior_single_zones", "sample_posterior_single_zones"):
+        samples[key] = [[v[r] for r in ranked] for v in samples[key]]
+    samples["sample_p_zones"] = [np.asarray(p)[ranked] for p in samples["sample_p_zones"]]
+    return samples

@@ -1,0 +1,157 @@
+"""Capture golden vectors for the I/O row (contact_zones_amd/io.py, postprocessing.match_areas /
+rank_areas) from the reference itself — BUILD CONTAINER ONLY (imports /root/reference via
+refenv; writes tests/golden/io/*).
+
+Inputs are data files the reference ships (experiments/balkan, experiments/south_america,
+test/test_files), copied under tests/golden/io/data/ so the tests read the same bytes without
+the reference.  Outputs:
+  io_expected.npz   per dataset: what sbayes.util.read_features_from_csv returns (features as
+                    obs codes, applicable states, names, families, locations, NA count, log),
+                    the counts of read_universal_counts / read_inheritance_counts, and the
+                    Delaunay network of compute_network (CSR + distance matrix)
+  samples_in.npz    a seeded statistics dict (balkan names, 3 zones, 12 logged samples)
+  stats_expected.txt / areas_expected.txt
+                    the files sbayes.util.samples2file writes for it after
+                    sbayes.postprocessing.match_areas and rank_areas (MCMC.save_samples order)
+Run: python tests/golden/make_golden_io.py
+"""
+import json
+import os
+import shutil
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import refenv  # noqa: E402
+
+OUT = os.path.join(HERE, "io")
+DATA = os.path.join(OUT, "data")
+
+DATASETS = {
+    "balkan": ("experiments/balkan/data/features/features.csv",
+               "experiments/balkan/data/features/feature_states.csv",
+               "experiments/balkan/data/prior_universal/universal_counts.csv",
+               {"Greek": "experiments/balkan/data/prior_inheritance/greek_counts.csv",
+                "Romance": "experiments/balkan/data/prior_inheritance/romance_counts.csv",
+                "Slavic": "experiments/balkan/data/prior_inheritance/slavic_counts.csv",
+                "Turkish": "experiments/balkan/data/prior_inheritance/turkish_counts.csv"}),
+    "south_america": ("experiments/south_america/data/features/features.csv",
+                      "experiments/south_america/data/features/feature_states.csv",
+                      "experiments/south_america/data/prior_universal/universal_counts.csv",
+                      {"Arawak": "experiments/south_america/data/prior_inheritance/arawak_counts.csv",
+                       "Panoan": "experiments/south_america/data/prior_inheritance/panoan_counts.csv",
+                       "Quechuan": "experiments/south_america/data/prior_inheritance/quechuan_counts.csv",
+                       "Tucanoan": "experiments/south_america/data/prior_inheritance/tucanoan_counts.csv",
+                       "Tupian": "experiments/south_america/data/prior_inheritance/tupian_counts.csv"}),
+    "test_files": ("test/test_files/features.csv", "test/test_files/feature_states_expected.csv",
+                   None, {}),
+}
+
+
+def local(rel):
+    """Copy a reference data file under io/data/ (same relative path) and return the copy."""
+    dst = os.path.join(DATA, rel)
+    os.makedirs(os.path.dirname(dst), exist_ok=True)
+    shutil.copyfile(os.path.join(refenv.REFERENCE, rel), dst)
+    return dst
+
+
+def rel(path):
+    return os.path.relpath(path, DATA)
+
+
+def capture_readers(out):
+    from sbayes import preprocessing, util
+    for name, (feat, states, uni, inh) in DATASETS.items():
+        feat_l, states_l = local(feat), local(states)
+        (sites, site_names, features, feature_names, state_names, applicable, families,
+         family_names, log) = util.read_features_from_csv(feat_l, states_l)
+        features = np.asarray(features, bool)
+        obs = np.where(features.any(-1), features.argmax(-1), -1).astype(np.int8)
+        p = name + "_"
+        out[p + "obs"] = obs
+        out[p + "applicable"] = np.asarray(applicable, bool)
+        out[p + "locations"] = np.asarray(sites["locations"], np.float64)
+        out[p + "families"] = np.asarray(families, np.int64).reshape(len(family_names["external"]), -1)
+        meta = {"feature_names": [str(x) for x in feature_names["external"]],
+                "state_names": [[str(s) for s in st] for st in state_names["external"]],
+                "family_names": [str(x) for x in family_names["external"]],
+                "site_ids": [str(x) for x in site_names["external"]],
+                "site_names": [str(x) for x in sites["names"]],
+                "log": log.replace(feat_l, "<FEATURES>"),
+                "files": {"features": rel(feat_l), "feature_states": rel(states_l)}}
+        if uni is not None:
+            uni_l = local(uni)
+            counts, ulog = preprocessing.read_universal_counts(
+                feature_names=feature_names, state_names=state_names, file=uni_l,
+                file_type="counts_file", feature_states_file=states_l)
+            out[p + "universal_counts"] = np.asarray(counts)
+            inh_l = {k: local(v) for k, v in inh.items()}
+            icounts, ilog = preprocessing.read_inheritance_counts(
+                family_names=family_names, feature_names=feature_names, state_names=state_names,
+                files=inh_l, file_type="counts_file", feature_states_file=states_l)
+            out[p + "inheritance_counts"] = np.asarray(icounts)
+            meta["files"]["universal"] = rel(uni_l)
+            meta["files"]["inheritance"] = {k: rel(v) for k, v in inh_l.items()}
+        net = preprocessing.compute_network(sites)
+        adj = net["adj_mat"].tocsr()
+        out[p + "adj_indptr"] = adj.indptr.astype(np.int64)
+        out[p + "adj_indices"] = adj.indices.astype(np.int64)
+        out[p + "dist_mat"] = np.asarray(net["dist_mat"], np.float64)
+        out[p + "meta"] = np.array(json.dumps(meta))
+
+
+def capture_results_files():
+    """samples2file after match_areas + rank_areas on a seeded statistics dict."""
+    import types
+
+    from sbayes import postprocessing, util
+    rng = np.random.default_rng(11)
+    feat, states = DATASETS["balkan"][0], DATASETS["balkan"][1]
+    (_, _, features, feature_names, state_names, applicable, families, family_names,
+     _) = util.read_features_from_csv(os.path.join(DATA, feat), os.path.join(DATA, states))
+    N, F, S = np.asarray(features).shape
+    Z, n, Fam = 3, 12, len(family_names["external"])
+    stats = {"sample_zones": [], "sample_weights": [], "sample_p_global": [], "sample_p_zones": [],
+             "sample_p_families": [], "sample_likelihood": [], "sample_prior": [],
+             "sample_lh_single_zones": [], "sample_prior_single_zones": [],
+             "sample_posterior_single_zones": []}
+    for _ in range(n):
+        lab = rng.integers(0, Z + 2, size=N)
+        stats["sample_zones"].append(np.stack([lab == z for z in range(Z)]))
+        stats["sample_weights"].append(rng.dirichlet(np.ones(3), size=F))
+        stats["sample_p_global"].append(rng.dirichlet(np.ones(S), size=(1, F)))
+        stats["sample_p_zones"].append(rng.dirichlet(np.ones(S), size=(Z, F)))
+        stats["sample_p_families"].append(rng.dirichlet(np.ones(S), size=(Fam, F)))
+        stats["sample_likelihood"].append(float(-rng.random() * 1000))
+        stats["sample_prior"].append(float(-rng.random() * 10))
+        lh, pr = list(-rng.random(Z) * 500), list(-rng.random(Z) * 5)
+        stats["sample_lh_single_zones"].append(lh)
+        stats["sample_prior_single_zones"].append(pr)
+        stats["sample_posterior_single_zones"].append([a + b for a, b in zip(lh, pr)])
+    np.savez_compressed(os.path.join(OUT, "samples_in.npz"),
+                        **{k: np.asarray(v) for k, v in stats.items()})
+    config = {"model": {"INHERITANCE": True, "N_AREAS": Z}, "mcmc": {"N_STEPS": 1200, "N_SAMPLES": n}}
+    data = types.SimpleNamespace(feature_names=feature_names, state_names=state_names,
+                                 family_names=family_names, is_simulated=False)
+    stats = postprocessing.match_areas(stats)
+    stats = postprocessing.rank_areas(stats)
+    paths = {"parameters": os.path.join(OUT, "stats_expected.txt"),
+             "areas": os.path.join(OUT, "areas_expected.txt")}
+    util.samples2file(stats, data, config, paths)
+
+
+def main():
+    refenv.setup()
+    os.makedirs(OUT, exist_ok=True)
+    out = {}
+    capture_readers(out)
+    np.savez_compressed(os.path.join(OUT, "io_expected.npz"), **out)
+    capture_results_files()
+    print("wrote", sorted(os.listdir(OUT)))
+
+
+if __name__ == "__main__":
+    main()
