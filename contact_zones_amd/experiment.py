@@ -1,0 +1,319 @@
+"""Run an sBayes experiment config end to end on the GPU: the reference's CLI path
+(sbayes/cli.py:13-87: Experiment -> Data -> MCMC.warm_up -> MCMC.sample -> save_samples) with
+the batched GPU sampler in place of ZoneMCMCWarmup / ZoneMCMC, and no dependency on the
+reference package.
+
+  config        sbayes/experiment_setup.py:62-90 (load_config), :124-260 (verify_config),
+                defaults of sbayes/config/default_config.json (DEFAULT_CONFIG below)
+  data          sbayes/load_data.py:63-121 via contact_zones_amd.io (packed features, Delaunay
+                network, prior counts)
+  operators     sbayes/mcmc_setup.py:70-95 (steps_per_operator)
+  priors        sbayes/model.py:538-680: 'counts' priors on p_global / p_families
+                (initial count 1 + scale_counts), zone-size prior; geo / weights / contact
+                must be 'uniform' (NotImplementedError otherwise, as the batched sampler)
+  sampling      warm-up: BatchedZoneMCMCWarmup, N_WARM_UP_CHAINS chains in one launch; main:
+                BatchedZoneMCMC from the warm-up's best sample (mcmc_setup.py:97-121, 174-187)
+  results       contribution_per_area (GPU batch), match_areas, rank_areas, samples2file
+                (mcmc_setup.py:189-260) -> <RESULTS_PATH>/<name>/<file_info>/stats_*.txt, areas_*.txt
+
+Simulation configs ('simulation' key) are not supported here.
+Usage: python -m contact_zones_amd <config.json> [--name NAME] [--seed S] [--device D]
+"""
+import copy
+import json
+import logging
+import os
+import random
+import time
+import types
+
+import numpy as np
+
+REQUIRED = "<REQUIRED>"
+
+# sbayes/config/default_config.json
+DEFAULT_CONFIG = {
+    "mcmc": {
+        "N_STEPS": 1000000, "N_SAMPLES": 1000, "N_RUNS": 1, "P_GROW_CONNECTED": 0.85,
+        "PROPOSAL_PRECISION": {"weights": 15, "universal": 40, "contact": 20, "inheritance": 20},
+        "STEPS": {"area": 0.05, "weights": 0.4, "universal": 0.05, "contact": 0.4,
+                  "inheritance": 0.1, "source": 0.0},
+        "M_INITIAL": 5,
+        "WARM_UP": {"N_WARM_UP_STEPS": 100000, "N_WARM_UP_CHAINS": 15},
+    },
+    "model": {
+        "N_AREAS": REQUIRED, "MIN_M": 3, "MAX_M": 50, "INHERITANCE": REQUIRED, "SAMPLE_SOURCE": True,
+        "PRIOR": {"geo": {"type": "uniform"}, "area_size": {"type": "none"},
+                  "weights": {"type": "uniform"}, "universal": {"type": "uniform"},
+                  "inheritance": {"type": "uniform"}, "contact": {"type": "uniform"}},
+    },
+    "data": {"FEATURES": REQUIRED, "FEATURE_STATES": REQUIRED},
+}
+
+
+def set_defaults(cfg, default):
+    """experiment_setup.py:263-281: fill missing keys recursively."""
+    for k, v in default.items():
+        if k not in cfg:
+            cfg[k] = copy.deepcopy(v)
+        elif isinstance(v, dict) and isinstance(cfg[k], dict):
+            set_defaults(cfg[k], v)
+    return cfg
+
+
+def update_recursive(cfg, new):
+    for k, v in new.items():
+        if isinstance(v, dict) and isinstance(cfg.get(k), dict):
+            update_recursive(cfg[k], v)
+        else:
+            cfg[k] = v
+    return cfg
+
+
+def _iter_items(d, prefix=""):
+    for k, v in d.items():
+        if isinstance(v, dict):
+            yield from _iter_items(v, prefix + k + ".")
+        else:
+            yield prefix + k, v
+
+
+def load_config(config_file, custom_settings=None):
+    """The reference's load_config + verify_config for data-based experiments: returns the
+    verified config (paths made relative to the config's directory) and that directory."""
+    base = os.path.dirname(os.path.abspath(config_file))
+    with open(config_file) as f:
+        cfg = json.load(f)
+    if "simulation" in cfg:
+        raise NotImplementedError("simulation experiments are not supported by this runner")
+    data = cfg.setdefault("data", {})
+    for low, up in (("features", "FEATURES"), ("feature_states", "FEATURE_STATES")):
+        if low in data and up not in data:  # experiments/balkan/config.json spells them lowercase
+            data[up] = data.pop(low)
+    set_defaults(cfg, DEFAULT_CONFIG)
+    if custom_settings:
+        update_recursive(cfg, custom_settings)
+
+    def fix(p):
+        return p if os.path.isabs(p) else os.path.join(base, p)
+
+    for k, v in _iter_items(cfg):
+        if v == REQUIRED:
+            raise NameError(f"{k} is not defined in {config_file}")
+    model, mcmc = cfg["model"], cfg["mcmc"]
+    inh = bool(model["INHERITANCE"])
+    pri = model["PRIOR"]
+    if not inh:
+        pri["inheritance"] = None
+    for key in ["geo", "area_size", "weights", "universal", "contact"] + (["inheritance"] if inh else []):
+        prior = pri[key]
+        if "type" not in prior:
+            raise NameError(f"type for prior '{key}' is not defined in {config_file}.")
+        if prior["type"] == "counts":
+            if "file_type" not in prior:
+                raise NameError(f"counts file for prior '{key}' is not defined in {config_file}.")
+            prior.setdefault("scale_counts", None)
+            if key == "universal":
+                prior["file"] = fix(prior["file"])
+            elif key == "inheritance":
+                prior["files"] = {fam: fix(p) for fam, p in prior["files"].items()}
+    mcmc["N_CHAINS"] = 1  # MC3 is disabled in the reference (experiment_setup.py:200-206)
+    if mcmc["N_STEPS"] % mcmc["N_SAMPLES"] != 0:
+        raise ValueError("Non-consistent spacing between samples. Set N_STEPS to be a multiple of N_SAMPLES. ")
+    steps = mcmc["STEPS"]
+    if not inh:
+        steps["inheritance"] = 0.0
+    if not model["SAMPLE_SOURCE"]:
+        steps["source"] = 0.0
+    total = sum(steps.values())
+    for k in steps:
+        steps[k] = steps[k] / total
+    res = cfg.setdefault("results", {})
+    res.setdefault("RESULTS_PATH", "results")
+    res.setdefault("FILE_INFO", "n")
+    data["FEATURES"] = fix(data["FEATURES"])
+    data["FEATURE_STATES"] = fix(data["FEATURE_STATES"])
+    res["RESULTS_PATH"] = fix(res["RESULTS_PATH"])
+    return cfg, base
+
+
+def operators(config):
+    """mcmc_setup.py:70-95 (steps_per_operator)."""
+    steps = config["mcmc"]["STEPS"]
+    ops = {"shrink_zone": steps["area"] * 0.4, "grow_zone": steps["area"] * 0.4,
+           "swap_zone": steps["area"] * 0.2, "gibbsish_sample_zones": steps["area"] * 0.0}
+    if config["model"]["SAMPLE_SOURCE"]:
+        ops.update({"gibbs_sample_sources": steps["source"], "gibbs_sample_weights": steps["weights"],
+                    "gibbs_sample_p_global": steps["universal"], "gibbs_sample_p_zones": steps["contact"],
+                    "gibbs_sample_p_families": steps["inheritance"]})
+    else:
+        ops.update({"alter_weights": steps["weights"], "alter_p_global": steps["universal"],
+                    "alter_p_zones": steps["contact"], "alter_p_families": steps["inheritance"]})
+    return ops
+
+
+EPS = np.finfo(float).eps  # sbayes/util.py:EPS
+
+
+def scale_counts(counts, scale_to):
+    """util.py:569-586."""
+    s = np.sum(counts, axis=-1)
+    s = np.where(s == 0, EPS, s)
+    factor = scale_to / s
+    factor = np.where(factor < 1, factor, 1)
+    return counts * factor[..., None]
+
+
+class ExperimentData:
+    """The attributes of the reference's Data (load_data.py:25-61) the batched sampler and the
+    results writer use, from contact_zones_amd.io."""
+
+    def __init__(self, config):
+        from . import io
+        import scipy.sparse as sp
+        d = config["data"]
+        self.table = io.read_features_packed(d["FEATURES"], d["FEATURE_STATES"])
+        t = self.table
+        self.features = t.one_hot()
+        self.states = t.applicable
+        self.families = t.families
+        self.feature_names = {"external": t.feature_names, "internal": list(range(t.n_features))}
+        self.state_names = {"external": t.state_names,
+                            "internal": [list(range(len(s))) for s in t.state_names]}
+        self.family_names = {"external": t.family_names, "internal": list(range(len(t.family_names)))}
+        indptr, indices, dist = io.compute_network(t.locations)
+        N = t.n_sites
+        self.network = {"adj_mat": sp.csr_matrix((np.ones(indices.size, int), indices, indptr), shape=(N, N)),
+                        "dist_mat": dist, "locations": t.locations}
+        self.is_simulated = False
+        self.log = [t.log]
+        pri = config["model"]["PRIOR"]
+        self.universal_counts = self.inheritance_counts = None
+        if pri["universal"]["type"] == "counts":
+            self.universal_counts, lg = io.read_universal_counts(
+                t, pri["universal"]["file"], pri["universal"]["file_type"], d["FEATURE_STATES"])
+            self.log.append(lg)
+        if config["model"]["INHERITANCE"] and pri["inheritance"]["type"] == "counts":
+            self.inheritance_counts, lg = io.read_inheritance_counts(
+                t, pri["inheritance"]["files"], pri["inheritance"]["file_type"], d["FEATURE_STATES"])
+            self.log.append(lg)
+
+
+def build_priors(config, data):
+    """The prior terms the batched sampler uses (model.py:538-680): Dirichlet concentrations
+    alpha [F][S] / [Fam][F][S] (1 + scaled counts on the applicable states) and, in source mode,
+    the Gibbs pseudo-counts (prior.prior_p_*.counts)."""
+    from .priors import PriorSpec
+    model = config["model"]
+    pri = model["PRIOR"]
+    for key in ("geo", "weights", "contact"):
+        if pri[key]["type"] != "uniform":
+            raise NotImplementedError(f"{key} prior of type '{pri[key]['type']}' is not supported")
+    F, S = data.states.shape
+    Fam = data.families.shape[0]
+    cg = np.ones((F, S))
+    ag = None
+    if pri["universal"]["type"] == "counts":
+        c = data.universal_counts.astype(float)
+        if pri["universal"]["scale_counts"] is not None:
+            c = scale_counts(c, pri["universal"]["scale_counts"])
+        cg = 1.0 + c                                    # prior.counts (model.py:585)
+        ag = np.where(data.states, cg + 1.0, 0.0)       # counts_to_dirichlet adds 1 (util.py:618)
+    elif pri["universal"]["type"] != "uniform":
+        raise NotImplementedError(f"universal prior of type '{pri['universal']['type']}' is not supported")
+    cf, af = None, None
+    if model["INHERITANCE"]:
+        cf = np.ones((Fam, F, S))
+        t = pri["inheritance"]["type"]
+        if t == "counts":
+            c = data.inheritance_counts.astype(float)
+            if pri["inheritance"]["scale_counts"] is not None:
+                c = scale_counts(c, pri["inheritance"]["scale_counts"])
+            cf = 1.0 + c                                # model.py:664
+            af = np.where(data.states[None], cf + 1.0, 0.0)  # util.py:547-566, 618
+        elif t != "uniform":
+            raise NotImplementedError(f"inheritance prior of type '{t}' is not supported")
+    size = pri["area_size"]["type"]
+    return PriorSpec(ag, af, size), (cg, cf)
+
+
+def model_spec(config, n_zones):
+    m = config["model"]
+    return types.SimpleNamespace(n_zones=int(n_zones), min_size=int(m["MIN_M"]), max_size=int(m["MAX_M"]),
+                                 inheritance=bool(m["INHERITANCE"]), sample_source=bool(m["SAMPLE_SOURCE"]))
+
+
+def run_experiment(config, data, n_zones, run=0, name="experiment", seed=None, device=None,
+                   logger=None, warmup_chains=None):
+    """One run for one number of zones (cli.py:13-27): warm-up, sampling, results files.
+    Returns (statistics, paths)."""
+    from . import io
+    from .mcmc import BatchedZoneMCMC, BatchedZoneMCMCWarmup
+    from .postprocessing import contribution_per_area, match_areas, rank_areas
+    logger = logger or logging.getLogger("sbz")
+    mc = config["mcmc"]
+    cfg = copy.deepcopy(config)
+    cfg["model"]["N_AREAS"] = int(n_zones)
+    priors, gibbs = build_priors(cfg, data)
+    model = model_spec(cfg, n_zones)
+    ops = operators(cfg)
+    rng = random.Random(seed)
+    if seed is not None:
+        np.random.seed(seed)
+    common = dict(model=model, data=data, operators=ops, var_proposal=mc["PROPOSAL_PRECISION"],
+                  p_grow_connected=mc["P_GROW_CONNECTED"], initial_size=mc["M_INITIAL"],
+                  logger=logger, rng=rng, seed=seed, device=device, priors=priors,
+                  gibbs_counts=gibbs if model.sample_source else None)
+    t0 = time.time()
+    warm = BatchedZoneMCMCWarmup(n_chains=warmup_chains or mc["WARM_UP"]["N_WARM_UP_CHAINS"], **common)
+    best = warm.generate_samples(n_steps=0, n_samples=0, warm_up=True,
+                                 warm_up_steps=mc["WARM_UP"]["N_WARM_UP_STEPS"])
+    logger.info("warm-up: %d chains x %d steps in %.2f s", warm.n_chains, mc["WARM_UP"]["N_WARM_UP_STEPS"],
+                time.time() - t0)
+    smp = BatchedZoneMCMC(n_chains=mc["N_CHAINS"], initial_sample=best, **common)
+    smp.generate_samples(mc["N_STEPS"], mc["N_SAMPLES"])
+    contribution_per_area(smp)
+    stats = rank_areas(match_areas(smp.statistics))
+    fi = {"n": f"n{n_zones}", "i": f"i{int(cfg['model']['INHERITANCE'])}",
+          "p": f"p{0 if cfg['model']['PRIOR']['universal']['type'] == 'uniform' else 1}"}.get(
+              cfg["results"]["FILE_INFO"])
+    if fi is None:
+        raise ValueError("file_info must be 'n', 'i' or 'p'")
+    pth = os.path.join(cfg["results"]["RESULTS_PATH"], name, fi)
+    os.makedirs(pth, exist_ok=True)
+    paths = {"parameters": os.path.join(pth, f"stats_{fi}_{run}.txt"),
+             "areas": os.path.join(pth, f"areas_{fi}_{run}.txt")}
+    rank = getattr(smp, "rank", 0)
+    if rank == 0:
+        io.samples2file(stats, data, cfg, paths)
+    logger.info("sampling: %d steps, acceptance %.3f, %.2f s; results in %s", mc["N_STEPS"],
+                stats["acceptance_ratio"], stats["sampling_time"], pth)
+    return stats, paths
+
+
+def main(argv=None):
+    import argparse
+    p = argparse.ArgumentParser(description="sBayes experiment on the GPU (batched sampler)")
+    p.add_argument("config")
+    p.add_argument("--name", default=None, help="experiment name (results sub-directory)")
+    p.add_argument("--seed", type=int, default=None)
+    p.add_argument("--device", type=int, default=None)
+    p.add_argument("--set", default=None, help="JSON object merged into the config (custom settings)")
+    a = p.parse_args(argv)
+    logging.basicConfig(level=logging.INFO, format="%(message)s")
+    logger = logging.getLogger("sbz")
+    config, _ = load_config(a.config, json.loads(a.set) if a.set else None)
+    name = a.name or time.strftime("%Y%m%d-%H%M%S")
+    data = ExperimentData(config)
+    for line in data.log:
+        logger.info(line)
+    n_areas = config["model"]["N_AREAS"]
+    sweep = n_areas if isinstance(n_areas, list) else [n_areas]
+    if not all(isinstance(n, int) for n in sweep):
+        raise ValueError(f"N_AREAS must be an integer or a list of integers, got {n_areas!r} "
+                         "(set it with --set '{\"model\": {\"N_AREAS\": 3}}')")
+    for run in range(config["mcmc"]["N_RUNS"]):
+        for n in sweep:
+            run_experiment(config, data, int(n), run=run, name=name, seed=a.seed, device=a.device,
+                           logger=logger)
+    return 0

@@ -143,11 +143,64 @@ def capture_results_files():
     util.samples2file(stats, data, config, paths)
 
 
+def capture_model_setup(out):
+    """The reference's Experiment -> Data -> MCMC setup for the Balkan and South America configs
+    (N_AREAS set to 3): the verified config's operator table (MCMC.steps_per_operator) and the
+    'counts' priors' pseudo-counts and Dirichlet concentrations (model.py:538-680)."""
+    from sbayes.experiment_setup import Experiment
+    from sbayes.load_data import Data
+    from sbayes.mcmc_setup import MCMC
+    cwd = os.getcwd()
+    for name, rel_dir in (("balkan", "experiments/balkan"), ("south_america", "experiments/south_america")):
+        local(rel_dir + "/config.json")  # the config the tests load (data paths relative to it)
+        d = refenv.scratch_copy(rel_dir)
+        os.chdir(d)  # load_universal_counts writes universal_counts.csv into the CWD
+        try:
+            custom = {"model": {"N_AREAS": 3}}
+            cfg_path = os.path.join(d, "config.json")
+            with open(cfg_path) as f:
+                raw = json.load(f)
+            data_cfg = raw.get("data", {})
+            for low, up in (("features", "FEATURES"), ("feature_states", "FEATURE_STATES")):
+                if low in data_cfg:
+                    custom.setdefault("data", {})[up] = data_cfg[low]
+            if name == "south_america":
+                custom.setdefault("data", {})["CRS"] = None
+            exp = Experiment(experiment_name="golden", log=False)
+            exp.load_config(config_file=cfg_path, custom_settings=custom)
+            data = Data(experiment=exp)
+            data.load_features()
+            data.load_universal_counts()
+            data.load_inheritance_counts()
+            mcmc = MCMC(data=data, experiment=exp)
+            p = "setup_" + name + "_"
+            out[p + "ops"] = np.array(json.dumps(mcmc.ops))
+            out[p + "steps"] = np.array(json.dumps(exp.config["mcmc"]["STEPS"]))
+            pr = mcmc.model.prior
+            F, S = data.states.shape
+            ag = np.zeros((F, S))
+            for f in range(F):
+                ag[f, data.states[f]] = pr.prior_p_global.dirichlet[f]
+            out[p + "alpha_global"] = ag
+            out[p + "counts_global"] = np.asarray(pr.prior_p_global.counts, np.float64)
+            fam = pr.prior_p_families
+            n_fam = len(fam.dirichlet)
+            af = np.zeros((n_fam, F, S))
+            for k in range(n_fam):
+                for f in range(F):
+                    af[k, f, data.states[f]] = fam.dirichlet[k][f]
+            out[p + "alpha_fam"] = af
+            out[p + "counts_fam"] = np.asarray(fam.counts, np.float64)
+        finally:
+            os.chdir(cwd)
+
+
 def main():
     refenv.setup()
     os.makedirs(OUT, exist_ok=True)
     out = {}
     capture_readers(out)
+    capture_model_setup(out)
     np.savez_compressed(os.path.join(OUT, "io_expected.npz"), **out)
     capture_results_files()
     print("wrote", sorted(os.listdir(OUT)))

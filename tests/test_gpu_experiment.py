@@ -1,0 +1,58 @@
+"""An sBayes experiment config end to end on the GPU (contact_zones_amd/experiment.py): the
+Balkan config (tests/golden/io/data, the reference's data files) through warm-up, sampling,
+per-zone contributions, match / rank and the results files."""
+import os
+
+import numpy as np
+import pytest
+
+from contact_zones_amd import experiment, io
+
+pytestmark = pytest.mark.gpu
+CFG = os.path.join(os.path.dirname(__file__), "golden", "io", "data", "experiments", "balkan", "config.json")
+
+
+def _short(tmp_path, **model):
+    return {"model": {"N_AREAS": 2, **model},
+            "mcmc": {"N_STEPS": 2000, "N_SAMPLES": 20, "WARM_UP": {"N_WARM_UP_STEPS": 400, "N_WARM_UP_CHAINS": 6}},
+            "results": {"RESULTS_PATH": str(tmp_path)}}
+
+
+def _read_stats(path):
+    with open(path) as f:
+        head = f.readline().rstrip("\r\n").split("\t")
+        rows = [line.rstrip("\r\n").split("\t") for line in f]
+    return head, rows
+
+
+@pytest.mark.parametrize("source", [True, False])
+def test_balkan_experiment_end_to_end(gpu_available, tmp_path, source):
+    cfg, _ = experiment.load_config(CFG, _short(tmp_path, SAMPLE_SOURCE=source))
+    data = experiment.ExperimentData(cfg)
+    stats, paths = experiment.run_experiment(cfg, data, 2, name="t", seed=3)
+    head, rows = _read_stats(paths["parameters"])
+    t = data.table
+    assert head == io.stats_columns(t.feature_names, t.state_names, t.family_names, 2, True, False, True)
+    assert len(rows) == 20 and all(len(r) == len(head) for r in rows)
+    assert [int(r[0]) for r in rows] == [100 * i for i in range(20)]
+    with open(paths["areas"]) as f:
+        areas = [line.rstrip("\n").split("\t") for line in f]
+    assert len(areas) == 20 and all(len(a) == 2 and len(a[0]) == t.n_sites for a in areas)
+    zones = np.array([[[c == "1" for c in z] for z in a] for a in areas])
+    assert not np.any(zones.sum(axis=1) > 1)                          # disjoint zones
+    sizes = zones.sum(axis=2)
+    assert np.all((sizes >= cfg["model"]["MIN_M"]) & (sizes <= cfg["model"]["MAX_M"]))
+    np.testing.assert_array_equal(sizes, np.array([[int(r[4]), int(r[5])] for r in rows]))
+    ll = np.array([float(r[2]) for r in rows])
+    assert np.all(np.isfinite(ll))
+    if not source:
+        # mixture mode: every logged likelihood equals the oracle's full evaluation of that sample
+        from oracle import lik_numpy
+        for s in range(20):
+            zos = np.full(t.n_sites, 255, np.uint8)
+            for z in range(2):
+                zos[stats["sample_zones"][s][z]] = z
+            ref = lik_numpy.loglik(t.obs, t.fam_of_site, zos, stats["sample_weights"][s],
+                                   stats["sample_p_global"][s][0], stats["sample_p_zones"][s],
+                                   stats["sample_p_families"][s], inheritance=True)
+            assert ll[s] == pytest.approx(ref, rel=1e-9)

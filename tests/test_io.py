@@ -125,3 +125,37 @@ def test_results_files_match_reference(gold, tmp_path):
     for mine, ref in (("stats.txt", "stats_expected.txt"), ("areas.txt", "areas_expected.txt")):
         with open(tmp_path / mine, "rb") as a, open(os.path.join(GOLD, ref), "rb") as b:
             assert a.read() == b.read(), mine
+
+
+# ---- experiment setup (contact_zones_amd/experiment.py) vs the reference's Experiment/Data/MCMC ----
+@pytest.mark.parametrize("name", ["balkan", "south_america"])
+def test_experiment_setup_matches_reference(gold, name):
+    from contact_zones_amd import experiment
+    cfg_path = os.path.join(DATA, "experiments", name, "config.json")
+    cfg, _ = experiment.load_config(cfg_path, {"model": {"N_AREAS": 3}})
+    p = "setup_" + name + "_"
+    assert cfg["mcmc"]["STEPS"] == json.loads(str(gold[p + "steps"]))
+    assert experiment.operators(cfg) == json.loads(str(gold[p + "ops"]))
+    data = experiment.ExperimentData(cfg)
+    spec, (cg, cf) = experiment.build_priors(cfg, data)
+    np.testing.assert_array_equal(spec.alpha_global, gold[p + "alpha_global"])
+    np.testing.assert_array_equal(spec.alpha_fam, gold[p + "alpha_fam"])
+    np.testing.assert_array_equal(cg, gold[p + "counts_global"])
+    np.testing.assert_array_equal(cf, gold[p + "counts_fam"])
+    np.testing.assert_array_equal(data.network["adj_mat"].indices, gold[name + "_adj_indices"])
+
+
+def test_experiment_config_errors(tmp_path):
+    from contact_zones_amd import experiment
+    c = tmp_path / "c.json"
+    c.write_text(json.dumps({"model": {"N_AREAS": 2}, "data": {"FEATURES": "f.csv", "FEATURE_STATES": "s.csv"}}))
+    with pytest.raises(NameError):  # INHERITANCE is required
+        experiment.load_config(c)
+    c.write_text(json.dumps({"model": {"N_AREAS": 2, "INHERITANCE": False},
+                             "mcmc": {"N_STEPS": 10, "N_SAMPLES": 3},
+                             "data": {"FEATURES": "f.csv", "FEATURE_STATES": "s.csv"}}))
+    with pytest.raises(ValueError):  # uneven sample spacing
+        experiment.load_config(c)
+    c.write_text(json.dumps({"simulation": {}, "model": {}}))
+    with pytest.raises(NotImplementedError):
+        experiment.load_config(c)
