@@ -156,6 +156,7 @@ int sbz_open(int device, const sbz_dims *dims, const int8_t *obs, const uint8_t 
         ctx->lik_kernel = strcmp(v, "zoned") == 0 ? 2 : strcmp(v, "db") == 0 ? 3 : strcmp(v, "ws") == 0 ? 4 : 1;
     if (const char *v = getenv("SBZ_WS_NG")) ctx->ws_ng = std::min(2, std::max(1, atoi(v)));
     if (const char *v = getenv("SBZ_WS_NB")) ctx->ws_nb = std::min(2, std::max(1, atoi(v)));
+    if (const char *v = getenv("SBZ_SRC_HBM")) ctx->src_hbm = atoi(v) != 0;
     if (const char *v = getenv("SBZ_LIK_TASKS")) ctx->tasks_per_cu = std::max(1, atoi(v));
     if (const char *v = getenv("SBZ_LIK_ZSPL")) {
         const int z = atoi(v);
@@ -231,6 +232,7 @@ void sbz_close(sbz_ctx *ctx) {
     free_buf(ctx->nzs);
     free_buf(ctx->partial);
     free_buf(ctx->src_t);
+    free_buf(ctx->src_cand);
     free_buf(ctx->ticket);
     free_buf(ctx->stage);
     free_buf(ctx->out);

@@ -719,9 +719,12 @@ __global__ __launch_bounds__(WAVE *(NB + NG), SBZ_WS_WAVES) void lik_mixture_ws_
         lds_barrier();  // the gatherers' partials
     };
     if (wv < NB) {
-        if (NB == 1) builder(std::integral_constant<int, -1>());
-        else if (wv == 0) builder(std::integral_constant<int, 0>());
-        else builder(std::integral_constant<int, 1>());
+        if constexpr (NB == 1) {
+            builder(std::integral_constant<int, -1>());
+        } else {
+            if (wv == 0) builder(std::integral_constant<int, 0>());
+            else builder(std::integral_constant<int, 1>());
+        }
         return;
     }
 

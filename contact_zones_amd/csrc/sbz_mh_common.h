@@ -381,14 +381,16 @@ struct MhArgs {
     int size_prior;             // 0 none, 1 uniform, 2 quadratic
     const double *gc_g;         // [F][S] Gibbs prior counts of p_global (sbz_set_gibbs_counts) or null = 1
     const double *gc_f;         // [Fam][F][S] of p_families, or null = 1
+    uint8_t *src_scratch;       // [B][N][F] candidate sources when they live in HBM (source mode)
     sbz_chains ch;
 };
 
 // Normalised operator probabilities -> cumulative table (numpy choice(p), mcmc_generative.py:294).
 constexpr int MH_STAT_INTS = 2 * SBZ_N_OPS;  // LDS counters: proposed | accepted
 
-// SAMPLE_SOURCE = true sampler (sbz_mh_src.hip): LDS bytes per chain and the launch.
-size_t mh_src_lds_bytes(const sbz_dims &d, int C);
+// SAMPLE_SOURCE = true sampler (sbz_mh_src.hip): LDS bytes per chain (sources in LDS, or in
+// HBM: hbm_sources) and the launch.
+size_t mh_src_lds_bytes(const sbz_dims &d, int C, bool hbm_sources = false);
 int launch_mh_source(sbz_ctx *ctx, int B, const MhArgs &a);
 
 }  // namespace sbz

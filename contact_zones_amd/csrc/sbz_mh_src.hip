@@ -78,16 +78,21 @@ __device__ __forceinline__ int posterior_draw(const double (&l)[3], const double
 
 }  // namespace
 
-size_t mh_src_lds_bytes(const sbz_dims &d, int C) {
+size_t mh_src_lds_bytes(const sbz_dims &d, int C, bool hbm_sources) {
     const size_t N = d.n_sites, F = d.n_features, S = d.n_states, Z = d.n_zones;
     const size_t cnt = F * (S > (size_t)C ? S : (size_t)C);
     return cnt * 4 + ((Z + 1) & ~(size_t)1) * 4 + MH_STAT_INTS * 4 + ((N + 1) & ~(size_t)1) * 2 +
-           ((N * F + 15) & ~(size_t)15) * 2 + ((N + 15) & ~(size_t)15) + ((F + 15) & ~(size_t)15);
+           (hbm_sources ? 0 : ((N * F + 15) & ~(size_t)15) * 2) + ((N + 15) & ~(size_t)15) +
+           ((F + 15) & ~(size_t)15);
 }
 
 namespace {
 
-template <int C>
+// GS: the current sources are the chain's own array in HBM (updated in place) and the candidate
+// sources a per-chain scratch row, for N * F too large for LDS.  Only this chain's wave touches
+// them; its lanes exchange cells through agent-scope (sc1, L1-bypassing) byte accesses and a
+// vmcnt(0) wait at every sync point.
+template <int C, bool GS>
 __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int lane = threadIdx.x;
@@ -103,12 +108,33 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
     int *stat = zsize + ((Z + 1) & ~1);                               // [MH_STAT_INTS]
     uint16_t *nb = reinterpret_cast<uint16_t *>(stat + MH_STAT_INTS);  // [N] neighbour stamps
     uint8_t *src = reinterpret_cast<uint8_t *>(nb + ((N + 1) & ~1));   // [N][F] current sources
-    uint8_t *srcb = src + ((NF + 15) & ~15);                         // [N][F] candidate sources
-    uint8_t *zos = srcb + ((NF + 15) & ~15);                         // [N] zone of site
+    uint8_t *srcb = src + (GS ? 0 : ((NF + 15) & ~15));              // [N][F] candidate sources
+    uint8_t *zos = srcb + (GS ? 0 : ((NF + 15) & ~15));              // [N] zone of site
     uint8_t *sub = zos + ((N + 15) & ~15);                           // [F] feature subset
 
     uint8_t *gzos = ch.zone_of_site + (size_t)b * N;
     uint8_t *gsrc = ch.source + (size_t)b * NF;
+    if (GS) {
+        src = gsrc;
+        srcb = a.src_scratch + (size_t)b * NF;
+    }
+    // source cell access and the sync points (LDS: wave-local lgkmcnt wait; HBM: also vmcnt)
+    auto rsrc = [&](const uint8_t *p, int c) -> int {
+        if constexpr (GS) return __hip_atomic_load(p + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else return p[c];
+    };
+    auto wsrc = [&](uint8_t *p, int c, int v) {
+        if constexpr (GS) __hip_atomic_store(p + c, (uint8_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else p[c] = (uint8_t)v;
+    };
+    auto sync = [&]() {
+        if constexpr (GS) {
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+        } else {
+            wsync();
+        }
+    };
     double *w = ch.w + (size_t)b * F * C;
     double *pg = ch.p_global + (size_t)b * F * S;
     double *pz = Z > 0 ? ch.p_zones + (size_t)b * Z * F * S : pg;
@@ -119,8 +145,9 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
     for (int z = lane; z < Z; z += WAVE) zsize[z] = 0;
     if (lane < MH_STAT_INTS) stat[lane] = 0;
     for (int s = lane; s < N; s += WAVE) nb[s] = 0;
-    for (int c = lane; c < NF; c += WAVE) src[c] = gsrc[c];
-    wsync();
+    if (!GS)
+        for (int c = lane; c < NF; c += WAVE) src[c] = gsrc[c];
+    sync();
     int occ = 0;
     for (int s = lane; s < N; s += WAVE) {
         const int z = gzos[s];
@@ -131,7 +158,7 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
         }
     }
     int occupied = uni(wave_sum_i(occ));
-    wsync();
+    sync();
 
     Rng rng;
     rng.tape = ch.tape ? ch.tape + (size_t)b * ch.tape_stride : nullptr;
@@ -155,14 +182,14 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
         stamp++;
         if (stamp == 0) {
             for (int s = lane; s < N; s += WAVE) nb[s] = 0;
-            wsync();
+            sync();
             stamp = 1;
         }
         for (int s = lane; s < N; s += WAVE)
             if (zos[s] == z)
                 for (int e = a.adj_ptr[s]; e < a.adj_ptr[s + 1]; e++)
                     nb[MH_IDX(a.adj_idx[MH_IDX(e, a.nnz, 1)], N, 2)] = stamp;
-        wsync();
+        sync();
     };
     auto is_nb = [&](int s) { return nb[s] == stamp && zos[s] == NONE; };
     enum { SEL_NB = 0, SEL_FREE = 1, SEL_ZONE = 2 };
@@ -206,7 +233,7 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
             double l[3], wn[3], p[3];
             obs_terms<C>(a, w, pg, pz, pf, s, f, zos[s], C == 3 ? a.fam_site[s] : 0, l, wn);
             posterior_draw<C>(l, wn, 2.0, p);
-            acc += log(p[src[c]]);
+            acc += log(p[rsrc(src, c)]);
         }
         return uni(wave_sum(acc));
     };
@@ -219,7 +246,7 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
             const int s = c / F, f = c - s * F;
             double l[3], wn[3];
             obs_terms<C>(a, w, pg, pz, pf, s, f, zos[s], C == 3 ? a.fam_site[s] : 0, l, wn);
-            const int k = sv[c];
+            const int k = rsrc(sv, c);
             zero_w |= wn[k] == 0.0;
             acc += log(wn[k] * l[k]);
         }
@@ -241,7 +268,7 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
             obs_terms<C>(a, w, pg, pz, pf, s, f, zos[s], C == 3 ? a.fam_site[s] : 0, l, wn);
             const double u = rng.tape ? (have ? rng.tape[pos0 + c] : 0.0) : lr.u();
             const int k = posterior_draw<C>(l, wn, u, p);
-            srcb[c] = (uint8_t)k;
+            wsrc(srcb, c, k);
             acc_q += log(p[k]);
             zero_w |= wn[k] == 0.0;
             acc_l += log(wn[k] * l[k]);
@@ -252,19 +279,19 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
         } else {
             rng.ctr++;
         }
-        wsync();
+        sync();
         log_q_s = uni(wave_sum(acc_q));
         const double v = uni(wave_sum(acc_l));
         ll_new = __ballot(zero_w) ? -INFINITY : v;
     };
     auto commit_sources = [&]() {
-        for (int c = lane; c < NF; c += WAVE) src[c] = srcb[c];
-        wsync();
+        for (int c = lane; c < NF; c += WAVE) wsrc(src, c, rsrc(srcb, c));
+        sync();
     };
     // per-feature counts of sources / states into cnt
     auto clear_cnt = [&]() {
         for (int i = lane; i < ncnt; i += WAVE) cnt[i] = 0;
-        wsync();
+        sync();
     };
     // F uniforms -> sub[f] = u < fraction (np.random.random(n_features) < 0.4, :335, :383)
     auto draw_subset = [&]() {
@@ -282,7 +309,7 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
         } else {
             rng.ctr++;
         }
-        wsync();
+        sync();
     };
     // p_row[idx] = np.random.dirichlet(alpha) over feature f's applicable states, alpha_x =
     // base(x) + cnt[f][x]; the new values come from the tape (in idx order) or per-lane gammas.
@@ -382,17 +409,17 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
                     broken = true;
                     break;
                 }
-                wsync();
+                sync();
                 if (lane == 0) zos[site] = NONE;
-                wsync();
+                sync();
                 mark(z);
                 const int n_back = count_sel(SEL_NB, 0);
                 q_back = (1.0 - p_grow) * (1.0 / (double)(n_free + 1));
                 if (is_nb(site)) q_back += p_grow * (1.0 / (double)n_back);
                 if (a.warmup) q_back = 1.0 / (double)(size + 1);  // zone_sampling.py:1561
-                wsync();
+                sync();
                 if (lane == 0) zos[site] = (uint8_t)z;
-                wsync();
+                sync();
                 q = 1.0 / (double)size;
                 dprior = uni(size_prior_delta(a.size_prior, N, size, size - 1));
                 sa = site;
@@ -401,12 +428,12 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
             }
             if (sa >= 0) {
                 // the new zones (tentatively, undone on rejection), then every source redrawn
-                wsync();
+                sync();
                 if (lane == 0) {
                     zos[sa] = (uint8_t)zna;
                     if (sb >= 0) zos[sb] = NONE;
                 }
-                wsync();
+                sync();
                 double log_q_s;
                 pass_resample(log_q_s, ll_new);
                 new_sources = true;
@@ -428,9 +455,9 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
             for (int c = lane; c < NF; c += WAVE) {
                 const int s = c / F, f = c - s * F;
                 const bool in = (C == 2 || fixed == 0) ? zos[s] < Z : a.fam_site[s] > 0;
-                if (in) atomicAdd(&cnt[f * C + src[c]], 1);
+                if (in) atomicAdd(&cnt[f * C + rsrc(src, c)], 1);
             }
-            wsync();
+            sync();
             LaneRng lr;
             lr.init(rng, lane);
             const int64_t pos0 = rng.pos;
@@ -475,7 +502,7 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
             } else {
                 rng.ctr++;
             }
-            wsync();
+            sync();
             ll_new = pass_ll(src);
         } else {
             // ---- gibbs_sample_p_global / p_zones / p_families
@@ -488,7 +515,7 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
             }
             if (op == G_P_ZONES) {
                 for (int f = lane; f < F; f += WAVE) sub[f] = 1;
-                wsync();
+                sync();
             } else {
                 draw_subset();
             }
@@ -497,12 +524,12 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
             for (int c = lane; c < NF; c += WAVE) {
                 const int s = c / F, f = c - s * F;
                 const int x = a.obs_sm[c];
-                bool in = sub[f] && src[c] == comp && x < S;
+                bool in = sub[f] && rsrc(src, c) == comp && x < S;
                 if (comp == 1) in = in && zos[s] == row;
                 if (comp == 2) in = in && a.fam_site[s] == row + 1;
                 if (in) atomicAdd(&cnt[f * S + x], 1);
             }
-            wsync();
+            sync();
             double *base = comp == 0 ? pg : (comp == 1 ? pz + (size_t)row * F * S : pf + (size_t)row * F * S);
             const double *gc = comp == 0 ? a.gc_g : (comp == 2 && a.gc_f ? a.gc_f + (size_t)row * F * S : nullptr);
             const double *al = comp == 0 ? a.alpha_g : (comp == 2 && a.alpha_f ? a.alpha_f + (size_t)row * F * S : nullptr);
@@ -511,7 +538,7 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
                 dprior += redraw_row(base + (size_t)f * S, f, gc, 1.0, al);
             }
             dprior = uni(dprior);
-            wsync();
+            sync();
             ll_new = pass_ll(src);
         }
 
@@ -533,15 +560,15 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
                     if (sb >= 0) zsize[zna]--;
                 }
                 occupied += (zna < Z ? 1 : -1) + (sb >= 0 ? -1 : 0);
-                wsync();
+                sync();
             }
         } else if (sa >= 0) {
-            wsync();
+            sync();
             if (lane == 0) {  // undo the tentative zone change
                 zos[sa] = (uint8_t)zoa;
                 if (sb >= 0) zos[sb] = (uint8_t)zna;
             }
-            wsync();
+            sync();
         }
         if (alias && accept && op != G_SOURCES && op != G_P_GLOBAL && op != G_P_ZONES &&
             op != G_P_FAMILIES) {
@@ -568,9 +595,10 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
         }
     }
 
-    wsync();
+    sync();
     for (int s = lane; s < N; s += WAVE) gzos[s] = zos[s];
-    for (int c = lane; c < NF; c += WAVE) gsrc[c] = src[c];
+    if (!GS)
+        for (int c = lane; c < NF; c += WAVE) gsrc[c] = src[c];
     if (lane == 0) {
         ch.ll[b] = ll;
         if (ch.prior) ch.prior[b] = prior;
@@ -594,22 +622,38 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
 
 }  // namespace
 
-int launch_mh_source(sbz_ctx *ctx, int B, const MhArgs &a) {
-    const size_t lds = mh_src_lds_bytes(ctx->d, ctx->C);
-    if (lds > 160 * 1024)
+int launch_mh_source(sbz_ctx *ctx, int B, const MhArgs &a0) {
+    MhArgs a = a0;
+    constexpr size_t LDS_MAX = 160 * 1024;
+    const bool gs = ctx->src_hbm || mh_src_lds_bytes(ctx->d, ctx->C) > LDS_MAX;  // do not fit: HBM
+    const size_t lds = mh_src_lds_bytes(ctx->d, ctx->C, gs);
+    if (lds > LDS_MAX)
         return fail(ctx, SBZ_EINVAL, "SAMPLE_SOURCE sampler needs " + std::to_string(lds) +
-                                         " B of LDS per chain (> 160 KiB: too many sites x features)");
+                                         " B of LDS per chain even with the sources in HBM (> 160 KiB)");
+    if (gs) {
+        const size_t nf = (size_t)ctx->d.n_sites * ctx->d.n_features;
+        int rc = ensure(ctx, ctx->src_cand, (size_t)B * nf);
+        if (rc) return rc;
+        a.src_scratch = static_cast<uint8_t *>(ctx->src_cand.ptr);
+    }
     static bool configured = false;
     if (!configured) {
-        for (const void *fn : {reinterpret_cast<const void *>(&mh_src_kernel<2>),
-                               reinterpret_cast<const void *>(&mh_src_kernel<3>)}) {
-            hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        for (const void *fn : {reinterpret_cast<const void *>(&mh_src_kernel<2, false>),
+                               reinterpret_cast<const void *>(&mh_src_kernel<3, false>),
+                               reinterpret_cast<const void *>(&mh_src_kernel<2, true>),
+                               reinterpret_cast<const void *>(&mh_src_kernel<3, true>)}) {
+            hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX);
             if (e != hipSuccess) return hip_fail(ctx, e, "hipFuncSetAttribute(sampler LDS)");
         }
         configured = true;
     }
-    if (ctx->C == 3) mh_src_kernel<3><<<B, WAVE, lds, ctx->stream>>>(a);
-    else mh_src_kernel<2><<<B, WAVE, lds, ctx->stream>>>(a);
+    if (ctx->C == 3) {
+        if (gs) mh_src_kernel<3, true><<<B, WAVE, lds, ctx->stream>>>(a);
+        else mh_src_kernel<3, false><<<B, WAVE, lds, ctx->stream>>>(a);
+    } else {
+        if (gs) mh_src_kernel<2, true><<<B, WAVE, lds, ctx->stream>>>(a);
+        else mh_src_kernel<2, false><<<B, WAVE, lds, ctx->stream>>>(a);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(ctx, e, "source-mode sampler launch");
     return SBZ_OK;

@@ -14,6 +14,14 @@ SRC_CASES = mh_cases(source=True)
 REL_TOL = 1e-9
 
 
+@pytest.fixture(params=["lds", "hbm"])
+def src_home(request, monkeypatch):
+    """Where the sampler keeps the sources: LDS (when they fit) or HBM (SBZ_SRC_HBM=1, the path
+    every N x F too large for LDS takes); read when the context opens."""
+    monkeypatch.setenv("SBZ_SRC_HBM", "1" if request.param == "hbm" else "0")
+    return request.param
+
+
 def _setup(fx):
     from contact_zones_amd.likelihood import LikelihoodEngine
     from contact_zones_amd.priors import PriorSpec
@@ -45,7 +53,7 @@ def _check_final(fx, st, inh):
 
 
 @pytest.mark.parametrize("case", SRC_CASES)
-def test_source_tape_replay_matches_reference(gpu_available, case):
+def test_source_tape_replay_matches_reference(gpu_available, case, src_home):
     import torch
     fx = load_golden(case)
     inh = bool(fx["inheritance"])
@@ -92,7 +100,7 @@ def test_source_tape_replay_in_chunks(gpu_available):
     _check_final(fx, st, bool(fx["inheritance"]))
 
 
-def test_source_philox_chains_are_valid(gpu_available):
+def test_source_philox_chains_are_valid(gpu_available, src_home):
     """Philox draws: every observation's source is a component it can come from (zone only inside
     a zone, inheritance only inside a family), the parameters stay normalised, the tracked ll
     equals a fresh evaluation and the carried prior the full prior; the run is reproducible."""
@@ -125,3 +133,47 @@ def test_source_philox_chains_are_valid(gpu_available):
     torch.cuda.synchronize()
     np.testing.assert_array_equal(st2.source.cpu().numpy(), src)
     np.testing.assert_array_equal(st2.zone_of_site.cpu().numpy(), s["zone_of_site"])
+
+
+def test_source_sampler_large_sources_in_hbm(gpu_available):
+    """N x F = 100k observations (200 KB of sources per chain, beyond LDS): the sampler keeps the
+    sources in HBM; Philox steps keep every invariant and the tracked ll equals a fresh
+    evaluation."""
+    import torch
+    from scipy.spatial import Delaunay
+
+    from contact_zones_amd.likelihood import LikelihoodEngine
+    from contact_zones_amd.sampler import ChainState, Sampler
+    fx = load_golden("mh_src_small")
+    rng = np.random.default_rng(4)
+    N, F, S, Z, Fam, B = 400, 250, 4, 2, 2, 4
+    obs = rng.integers(0, S, size=(N, F)).astype(np.int8)
+    obs[rng.random((N, F)) < 0.02] = -1
+    fam = rng.integers(0, Fam, size=N).astype(np.uint8)
+    fam[rng.random(N) < 0.3] = 255
+    states = np.ones((F, S), bool)
+    indptr, indices = Delaunay(rng.random((N, 2))).vertex_neighbor_vertices
+    eng = LikelihoodEngine(obs, fam, S, Z, Fam, True)
+    assert eng.lds_bytes() >= 0
+    smp = Sampler(eng, states, indptr, indices, fx["op_probs"], fx["precision"], 3, sample_source=True)
+    zos = np.full((B, N), 255, np.uint8)
+    for b in range(B):
+        p = rng.permutation(N)
+        zos[b, p[:10]], zos[b, p[10:20]] = 0, 1
+    w = rng.dirichlet(np.ones(3), size=(B, F))
+    pg = rng.dirichlet(np.ones(S), size=(B, F))
+    pz = rng.dirichlet(np.ones(S), size=(B, Z, F))
+    pf = rng.dirichlet(np.ones(S), size=(B, Fam, F))
+    st = ChainState(eng, zos, w, pg, pz, pf, source=np.zeros((B, N, F), np.uint8))
+    out = smp.run(st, 60, np.full(B, 50), np.full(B, 0.85), seed=5)
+    torch.cuda.synchronize()
+    assert out["status"].cpu().numpy().tolist() == [0] * B
+    s = st.to_numpy()
+    src = s["source"]
+    assert not np.any((src == 1) & (s["zone_of_site"] == 255)[:, :, None])
+    assert not np.any((src == 2) & (fam == 255)[None, :, None])
+    assert np.any(src == 1) and np.any(src == 2)  # the Gibbs source draws ran
+    np.testing.assert_allclose(s["p_global"].sum(-1), 1.0, rtol=1e-12)
+    fresh = st.refresh_ll().cpu().numpy()
+    assert np.all(np.isfinite(fresh))
+    assert np.max(np.abs(s["ll"] - fresh) / np.abs(fresh)) <= REL_TOL
