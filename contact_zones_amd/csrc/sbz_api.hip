@@ -157,6 +157,7 @@ int sbz_open(int device, const sbz_dims *dims, const int8_t *obs, const uint8_t 
     if (const char *v = getenv("SBZ_WS_NG")) ctx->ws_ng = std::min(2, std::max(1, atoi(v)));
     if (const char *v = getenv("SBZ_WS_NB")) ctx->ws_nb = std::min(2, std::max(1, atoi(v)));
     if (const char *v = getenv("SBZ_SRC_HBM")) ctx->src_hbm = atoi(v) != 0;
+    if (const char *v = getenv("SBZ_SRC_WAVES")) ctx->src_waves = atoi(v);
     if (const char *v = getenv("SBZ_LIK_TASKS")) ctx->tasks_per_cu = std::max(1, atoi(v));
     if (const char *v = getenv("SBZ_LIK_ZSPL")) {
         const int z = atoi(v);

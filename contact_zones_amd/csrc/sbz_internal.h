@@ -75,6 +75,7 @@ struct sbz_ctx {
     int tasks_per_cu = 0;  // SBZ_LIK_TASKS: single-wave tasks per CU per launch (0: occupancy)
     int mix_occ = 0;       // resident mixture-kernel waves per CU (queried at first launch)
     int n_cu = 256;        // compute units of the device
+    int src_waves = 0;     // SBZ_SRC_WAVES: waves per chain of the source-mode sampler (0: by N x F)
     int src_hbm = 0;       // SBZ_SRC_HBM=1: source-mode sampler keeps sources in HBM even when they fit LDS
     sbz::DevBuf partial, ticket, src_t, zl, nzs, stage, out, src_cand;
     std::string err;

@@ -203,6 +203,21 @@ struct LaneRng {
         c3 = (uint32_t)(r.chain >> 32) ^ ((uint32_t)(lane + 1) << 24);
         j = 0;
     }
+    // as init, from the key / chain / counter values themselves
+    __device__ __forceinline__ void initk(uint32_t key0, uint32_t key1, uint64_t chain, uint64_t ctr,
+                                          int lane) {
+        k0 = key0;
+        k1 = key1;
+        base = (uint32_t)ctr;
+        c2 = (uint32_t)chain;
+        c3 = (uint32_t)(chain >> 32) ^ ((uint32_t)(lane + 1) << 24);
+        j = 0;
+    }
+    // a stream per thread of a multi-wave workgroup (id < 2048)
+    __device__ __forceinline__ void initw(const Rng &r, int id) {
+        init(r, 0);
+        c3 = (uint32_t)(r.chain >> 32) ^ ((uint32_t)(id + 1) << 20);
+    }
     __device__ __forceinline__ double u() {
         uint32_t c[4] = {j++, base, c2, c3};
         philox4x32_10(c, k0, k1);
@@ -387,6 +402,7 @@ struct MhArgs {
 
 // Normalised operator probabilities -> cumulative table (numpy choice(p), mcmc_generative.py:294).
 constexpr int MH_STAT_INTS = 2 * SBZ_N_OPS;  // LDS counters: proposed | accepted
+constexpr int MH_SRC_MAX_WAVES = 16;         // waves per chain of the source-mode sampler (max)
 
 // SAMPLE_SOURCE = true sampler (sbz_mh_src.hip): LDS bytes per chain (sources in LDS, or in
 // HBM: hbm_sources) and the launch.

@@ -27,6 +27,7 @@
 // stream, per-observation / per-feature draws from per-lane streams.
 #include <cmath>
 #include <cstdint>
+#include <type_traits>
 
 #include "sbz_mh_common.h"
 
@@ -81,29 +82,40 @@ __device__ __forceinline__ int posterior_draw(const double (&l)[3], const double
 size_t mh_src_lds_bytes(const sbz_dims &d, int C, bool hbm_sources) {
     const size_t N = d.n_sites, F = d.n_features, S = d.n_states, Z = d.n_zones;
     const size_t cnt = F * (S > (size_t)C ? S : (size_t)C);
-    return cnt * 4 + ((Z + 1) & ~(size_t)1) * 4 + MH_STAT_INTS * 4 + ((N + 1) & ~(size_t)1) * 2 +
+    return MH_SRC_MAX_WAVES * 2 * (8 + 4) + cnt * 4 + ((Z + 1) & ~(size_t)1) * 4 + MH_STAT_INTS * 4 +
+           ((N + 1) & ~(size_t)1) * 2 +
            (hbm_sources ? 0 : ((N * F + 15) & ~(size_t)15) * 2) + ((N + 15) & ~(size_t)15) +
            ((F + 15) & ~(size_t)15);
 }
 
 namespace {
 
+// One workgroup of NW waves runs one chain.  Every decision is uniform across the workgroup:
+// all waves draw the same values from identical RNG states and take the same branches; the
+// NW * 64 threads share the N * F passes (block reductions through LDS, summed in wave order)
+// and the per-feature Gibbs draws.  Shared LDS state (zone assignment, counters) is written by
+// thread 0 and published by a barrier.
 // GS: the current sources are the chain's own array in HBM (updated in place) and the candidate
-// sources a per-chain scratch row, for N * F too large for LDS.  Only this chain's wave touches
-// them; its lanes exchange cells through agent-scope (sc1, L1-bypassing) byte accesses and a
-// vmcnt(0) wait at every sync point.
-template <int C, bool GS>
-__global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
+// sources a per-chain scratch row, for N * F too large for LDS.  Only this chain's threads touch
+// them; they exchange cells through agent-scope (sc1, L1-bypassing) byte accesses and a
+// vmcnt(0) wait at every barrier.
+template <int C, bool GS, int NW>
+__global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
+    constexpr int NT = NW * WAVE;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x;
+    const int lane = tid % WAVE;
+    const int wv = uni(tid / WAVE);
     const int b = blockIdx.x;
     const int N = a.N, F = a.F, S = a.S, Z = a.Z, Fam = (C == 3) ? a.Fam : 0;
     const int NF = N * F;
     const sbz_chains &ch = a.ch;
 
-    // LDS carve-up (ints first, then u16, then bytes)
+    // LDS carve-up (reduction slots, then ints, then u16, then bytes)
+    double *red = reinterpret_cast<double *>(lds);                    // [2][MH_SRC_MAX_WAVES]
+    int *redi = reinterpret_cast<int *>(red + 2 * MH_SRC_MAX_WAVES);   // [2][MH_SRC_MAX_WAVES]
     const int ncnt = F * (S > C ? S : C);
-    int *cnt = reinterpret_cast<int *>(lds);                          // [F][max(S, C)] counts
+    int *cnt = redi + 2 * MH_SRC_MAX_WAVES;                           // [F][max(S, C)] counts
     int *zsize = cnt + ncnt;                                          // [Z]
     int *stat = zsize + ((Z + 1) & ~1);                               // [MH_STAT_INTS]
     uint16_t *nb = reinterpret_cast<uint16_t *>(stat + MH_STAT_INTS);  // [N] neighbour stamps
@@ -118,7 +130,7 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
         src = gsrc;
         srcb = a.src_scratch + (size_t)b * NF;
     }
-    // source cell access and the sync points (LDS: wave-local lgkmcnt wait; HBM: also vmcnt)
+    // source cell access
     auto rsrc = [&](const uint8_t *p, int c) -> int {
         if constexpr (GS) return __hip_atomic_load(p + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         else return p[c];
@@ -127,13 +139,37 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
         if constexpr (GS) __hip_atomic_store(p + c, (uint8_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         else p[c] = (uint8_t)v;
     };
+    // workgroup barrier after this thread's LDS (and, GS / parameter stores, global) accesses
+    // completed; a compiler memory barrier on both sides
     auto sync = [&]() {
-        if constexpr (GS) {
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_wave_barrier();
-        } else {
-            wsync();
-        }
+        if constexpr (GS) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    };
+    auto gsync = [&]() { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+    // block reductions (deterministic: wave partials summed in wave order); uniform results
+    int rslot = 0;
+    auto bsum = [&](double v) -> double {
+        v = wave_sum(v);
+        double *r = red + rslot * MH_SRC_MAX_WAVES;
+        rslot ^= 1;
+        if (lane == 0) r[wv] = v;
+        sync();
+        double t = r[0];
+#pragma unroll
+        for (int i = 1; i < NW; i++) t += r[i];
+        return uni(t);
+    };
+    int islot = 0;
+    auto bor = [&](int v) -> int {
+        const int wvv = __ballot(v != 0) ? 1 : 0;
+        int *r = redi + islot * MH_SRC_MAX_WAVES;
+        islot ^= 1;
+        if (lane == 0) r[wv] = wvv;
+        sync();
+        int t = 0;
+#pragma unroll
+        for (int i = 0; i < NW; i++) t |= r[i];
+        return uni(t);
     };
     double *w = ch.w + (size_t)b * F * C;
     double *pg = ch.p_global + (size_t)b * F * S;
@@ -142,14 +178,14 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
     const int max_size = ch.max_size[b];
     const double p_grow = ch.p_grow_connected[b];
 
-    for (int z = lane; z < Z; z += WAVE) zsize[z] = 0;
-    if (lane < MH_STAT_INTS) stat[lane] = 0;
-    for (int s = lane; s < N; s += WAVE) nb[s] = 0;
+    for (int z = tid; z < Z; z += NT) zsize[z] = 0;
+    if (tid < MH_STAT_INTS) stat[tid] = 0;
+    for (int s = tid; s < N; s += NT) nb[s] = 0;
     if (!GS)
-        for (int c = lane; c < NF; c += WAVE) src[c] = gsrc[c];
+        for (int c = tid; c < NF; c += NT) src[c] = gsrc[c];
     sync();
     int occ = 0;
-    for (int s = lane; s < N; s += WAVE) {
+    for (int s = tid; s < N; s += NT) {
         const int z = gzos[s];
         zos[s] = (uint8_t)z;
         if (z < Z) {
@@ -157,7 +193,7 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
             occ++;
         }
     }
-    int occupied = uni(wave_sum_i(occ));
+    int occupied = (int)bsum((double)occ);
     sync();
 
     Rng rng;
@@ -177,15 +213,16 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
     long long err_val = 0;
     uint16_t stamp = 0;
 
-    // ---- zone-move helpers (as the SAMPLE_SOURCE = false kernel, sbz_mh.hip)
+    // ---- zone-move helpers (as the SAMPLE_SOURCE = false kernel, sbz_mh.hip).  The scans over
+    // the sites run in every wave (identical results); the stamps are written by all threads.
     auto mark = [&](int z) {
         stamp++;
         if (stamp == 0) {
-            for (int s = lane; s < N; s += WAVE) nb[s] = 0;
+            for (int s = tid; s < N; s += NT) nb[s] = 0;
             sync();
             stamp = 1;
         }
-        for (int s = lane; s < N; s += WAVE)
+        for (int s = tid; s < N; s += NT)
             if (zos[s] == z)
                 for (int e = a.adj_ptr[s]; e < a.adj_ptr[s + 1]; e++)
                     nb[MH_IDX(a.adj_idx[MH_IDX(e, a.nnz, 1)], N, 2)] = stamp;
@@ -228,21 +265,21 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
     // sum over observations of log posterior[src] for the current sample (zone_sampling.py:718-722)
     auto pass_logq = [&]() -> double {
         double acc = 0.0;
-        for (int c = lane; c < NF; c += WAVE) {
+        for (int c = tid; c < NF; c += NT) {
             const int s = c / F, f = c - s * F;
             double l[3], wn[3], p[3];
             obs_terms<C>(a, w, pg, pz, pf, s, f, zos[s], C == 3 ? a.fam_site[s] : 0, l, wn);
             posterior_draw<C>(l, wn, 2.0, p);
             acc += log(p[rsrc(src, c)]);
         }
-        return uni(wave_sum(acc));
+        return bsum(acc);
     };
     // log-likelihood of the current sample with sources `sv` (combine_lh source branch,
     // model.py:177-184): sum log(w_src * lh_src), -inf if a selected weight is 0
     auto pass_ll = [&](const uint8_t *sv) -> double {
         double acc = 0.0;
         int zero_w = 0;
-        for (int c = lane; c < NF; c += WAVE) {
+        for (int c = tid; c < NF; c += NT) {
             const int s = c / F, f = c - s * F;
             double l[3], wn[3];
             obs_terms<C>(a, w, pg, pz, pf, s, f, zos[s], C == 3 ? a.fam_site[s] : 0, l, wn);
@@ -250,19 +287,19 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
             zero_w |= wn[k] == 0.0;
             acc += log(wn[k] * l[k]);
         }
-        const double v = uni(wave_sum(acc));
-        return __ballot(zero_w) ? -INFINITY : v;
+        const double v = bsum(acc);
+        return bor(zero_w) ? -INFINITY : v;
     };
     // redraw every source from the current sample's posterior into srcb; returns log q (sum log
     // posterior[new source]) and the new log-likelihood
     auto pass_resample = [&](double &log_q_s, double &ll_new) {
         LaneRng lr;
-        lr.init(rng, lane);
+        lr.initw(rng, tid);
         double acc_q = 0.0, acc_l = 0.0;
         int zero_w = 0;
         const int64_t pos0 = rng.pos;
         const bool have = !rng.tape || pos0 + NF <= rng.len;
-        for (int c = lane; c < NF; c += WAVE) {
+        for (int c = tid; c < NF; c += NT) {
             const int s = c / F, f = c - s * F;
             double l[3], wn[3], p[3];
             obs_terms<C>(a, w, pg, pz, pf, s, f, zos[s], C == 3 ? a.fam_site[s] : 0, l, wn);
@@ -279,27 +316,26 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
         } else {
             rng.ctr++;
         }
-        sync();
-        log_q_s = uni(wave_sum(acc_q));
-        const double v = uni(wave_sum(acc_l));
-        ll_new = __ballot(zero_w) ? -INFINITY : v;
+        log_q_s = bsum(acc_q);
+        const double v = bsum(acc_l);
+        ll_new = bor(zero_w) ? -INFINITY : v;
     };
     auto commit_sources = [&]() {
-        for (int c = lane; c < NF; c += WAVE) wsrc(src, c, rsrc(srcb, c));
+        for (int c = tid; c < NF; c += NT) wsrc(src, c, rsrc(srcb, c));
         sync();
     };
     // per-feature counts of sources / states into cnt
     auto clear_cnt = [&]() {
-        for (int i = lane; i < ncnt; i += WAVE) cnt[i] = 0;
+        for (int i = tid; i < ncnt; i += NT) cnt[i] = 0;
         sync();
     };
     // F uniforms -> sub[f] = u < fraction (np.random.random(n_features) < 0.4, :335, :383)
     auto draw_subset = [&]() {
         LaneRng lr;
-        lr.init(rng, lane);
+        lr.initw(rng, tid);
         const int64_t pos0 = rng.pos;
         const bool have = !rng.tape || pos0 + F <= rng.len;
-        for (int f = lane; f < F; f += WAVE) {
+        for (int f = tid; f < F; f += NT) {
             const double u = rng.tape ? (have ? rng.tape[pos0 + f] : 1.0) : lr.u();
             sub[f] = u < 0.4 ? 1 : 0;
         }
@@ -311,44 +347,59 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
         }
         sync();
     };
-    // p_row[idx] = np.random.dirichlet(alpha) over feature f's applicable states, alpha_x =
-    // base(x) + cnt[f][x]; the new values come from the tape (in idx order) or per-lane gammas.
-    // Returns the change of the 'counts' prior (xlogy(alpha_prior - 1, p) terms) if al != null.
-    auto redraw_row = [&](double *row, int f, const double *gc, double gc_default, const double *al) -> double {
-        const int n = a.app_cnt[f];
-        const int x = lane < n ? a.app_list[(size_t)f * S + lane] : 0;
-        double g = 0.0;
-        if (rng.tape) {
-            const int64_t pos0 = rng.pos;
-            const bool have = pos0 + n <= rng.len;
-            g = (lane < n && have) ? rng.tape[pos0 + lane] : 0.0;
-            if (!have) rng.bad = 1;
-            rng.pos = uni64(pos0 + n);
-        } else {
-            LaneRng lr;
-            lr.init(rng, lane);
-            const double alpha = (gc ? ldp(gc + (size_t)f * S + x) : gc_default) + (double)cnt[f * S + x];
-            g = lane < n ? lr.gamma(alpha) : 0.0;
-            rng.ctr++;
-            const double tot = uni(wave_sum(g));
-            g = g / tot;
-        }
+    // Every feature f with sub[f]: p_row(f)[idx] = np.random.dirichlet(alpha) over f's applicable
+    // states, alpha_x = base(x) + cnt[f][x]; the values come from the tape (in feature order, idx
+    // order) or from per-lane gammas.  Wave w draws the features f = w (mod NW); a running scan in
+    // feature order gives each feature its tape offset / Philox counter, so the draws do not
+    // depend on NW.  Returns the change of the 'counts' prior (xlogy(alpha_prior - 1, p) terms)
+    // if al != null.
+    // (the generator's fields come in as values and go out through pos / ctr / bad: the lambda
+    // does not touch `rng`, which keeps it in registers)
+    auto redraw_rows = [&](double *base, const double *gc, double gc_default, const double *al,
+                           const double *tape, int64_t len, uint32_t key0, uint32_t key1,
+                           uint64_t chain, int64_t &pos, uint64_t &ctr, int &bad) -> double {
         double dp = 0.0;
-        if (lane < n) {
-            const double old = ldp(row + x);
-            stp(row + x, g);
-            if (al) {
-                const double am1 = ldp(al + (size_t)f * S + x) - 1.0;
-                dp = xlogy(am1, g) - xlogy(am1, old);
+        for (int f = 0; f < F; f++) {
+            if (!sub[f]) continue;
+            const int n = a.app_cnt[f];
+            if (f % NW == wv) {
+                double *row = base + (size_t)f * S;
+                const int x = lane < n ? a.app_list[(size_t)f * S + lane] : 0;
+                double g = 0.0;
+                if (tape) {
+                    const bool have = pos + n <= len;
+                    g = (lane < n && have) ? tape[pos + lane] : 0.0;
+                    bad |= have ? 0 : 1;
+                } else {
+                    LaneRng lr;
+                    lr.initk(key0, key1, chain, ctr, lane);
+                    const double alpha = (gc ? ldp(gc + (size_t)f * S + x) : gc_default) + (double)cnt[f * S + x];
+                    g = lane < n ? lr.gamma(alpha) : 0.0;
+                    const double tot = uni(wave_sum(g));
+                    g = g / tot;
+                }
+                if (lane < n) {
+                    const double old = ldp(row + x);
+                    stp(row + x, g);
+                    if (al) {
+                        const double am1 = ldp(al + (size_t)f * S + x) - 1.0;
+                        dp += xlogy(am1, g) - xlogy(am1, old);
+                    }
+                }
             }
+            if (tape) pos = pos + n;
+            else ctr++;
         }
+        bad = bor(bad);
+        pos = uni64(pos);
+        ctr = (uint64_t)uni64((int64_t)ctr);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        return uni(wave_sum(dp));
+        return bsum(dp);
     };
 
     bool broken = false;
     for (int step = 0; step < a.n_steps; step++) {
-        if (rng.bad || broken || err) break;
+        if (rng.bad || broken) break;
         const int op = rng.op(a.op_cdf, a.nops);
         const bool zone_op = op <= SWAP;
         if (!(zone_op || (op >= G_SOURCES && op <= G_P_FAMILIES)) || (zone_op && Z == 0) ||
@@ -410,7 +461,7 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
                     break;
                 }
                 sync();
-                if (lane == 0) zos[site] = NONE;
+                if (tid == 0) zos[site] = NONE;
                 sync();
                 mark(z);
                 const int n_back = count_sel(SEL_NB, 0);
@@ -418,7 +469,7 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
                 if (is_nb(site)) q_back += p_grow * (1.0 / (double)n_back);
                 if (a.warmup) q_back = 1.0 / (double)(size + 1);  // zone_sampling.py:1561
                 sync();
-                if (lane == 0) zos[site] = (uint8_t)z;
+                if (tid == 0) zos[site] = (uint8_t)z;
                 sync();
                 q = 1.0 / (double)size;
                 dprior = uni(size_prior_delta(a.size_prior, N, size, size - 1));
@@ -429,7 +480,7 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
             if (sa >= 0) {
                 // the new zones (tentatively, undone on rejection), then every source redrawn
                 sync();
-                if (lane == 0) {
+                if (tid == 0) {
                     zos[sa] = (uint8_t)zna;
                     if (sb >= 0) zos[sb] = NONE;
                 }
@@ -452,18 +503,18 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
                 break;
             }
             clear_cnt();
-            for (int c = lane; c < NF; c += WAVE) {
+            for (int c = tid; c < NF; c += NT) {
                 const int s = c / F, f = c - s * F;
                 const bool in = (C == 2 || fixed == 0) ? zos[s] < Z : a.fam_site[s] > 0;
                 if (in) atomicAdd(&cnt[f * C + rsrc(src, c)], 1);
             }
             sync();
             LaneRng lr;
-            lr.init(rng, lane);
+            lr.initw(rng, tid);
             const int64_t pos0 = rng.pos;
-            const int64_t need = C == 2 ? 2LL * F : 2LL * F;  // C == 3: F beta draws + F uniforms
+            const int64_t need = 2LL * F;  // C == 2: F pairs; C == 3: F beta draws + F uniforms
             const bool have = !rng.tape || pos0 + need <= rng.len;
-            for (int f = lane; f < F; f += WAVE) {
+            for (int f = tid; f < F; f += NT) {
                 double *wf = w + (size_t)f * C;
                 if (C == 2) {
                     double d0, d1;
@@ -495,14 +546,13 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
                     stp(wf + 2, w2 / sum);
                 }
             }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (rng.tape) {
                 if (!have) rng.bad = 1;
                 rng.pos = uni64(pos0 + need);
             } else {
                 rng.ctr++;
             }
-            sync();
+            gsync();  // the new weights are visible to every thread
             ll_new = pass_ll(src);
         } else {
             // ---- gibbs_sample_p_global / p_zones / p_families
@@ -514,14 +564,14 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
                 break;
             }
             if (op == G_P_ZONES) {
-                for (int f = lane; f < F; f += WAVE) sub[f] = 1;
+                for (int f = tid; f < F; f += NT) sub[f] = 1;
                 sync();
             } else {
                 draw_subset();
             }
             const int comp = op == G_P_GLOBAL ? 0 : (op == G_P_ZONES ? 1 : 2);
             clear_cnt();
-            for (int c = lane; c < NF; c += WAVE) {
+            for (int c = tid; c < NF; c += NT) {
                 const int s = c / F, f = c - s * F;
                 const int x = a.obs_sm[c];
                 bool in = sub[f] && rsrc(src, c) == comp && x < S;
@@ -533,12 +583,15 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
             double *base = comp == 0 ? pg : (comp == 1 ? pz + (size_t)row * F * S : pf + (size_t)row * F * S);
             const double *gc = comp == 0 ? a.gc_g : (comp == 2 && a.gc_f ? a.gc_f + (size_t)row * F * S : nullptr);
             const double *al = comp == 0 ? a.alpha_g : (comp == 2 && a.alpha_f ? a.alpha_f + (size_t)row * F * S : nullptr);
-            for (int f = 0; f < F; f++) {
-                if (!sub[f]) continue;
-                dprior += redraw_row(base + (size_t)f * S, f, gc, 1.0, al);
-            }
-            dprior = uni(dprior);
-            sync();
+            int64_t rpos = rng.pos;
+            uint64_t rctr = rng.ctr;
+            int rbad = 0;
+            dprior = redraw_rows(base, gc, 1.0, al, rng.tape, rng.len, rng.key0, rng.key1, rng.chain,
+                                 rpos, rctr, rbad);
+            rng.pos = rpos;
+            rng.ctr = rctr;
+            if (rbad) rng.bad = 1;
+            gsync();  // the new rows are visible to every thread
             ll_new = pass_ll(src);
         }
 
@@ -547,14 +600,14 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
         if (log_q_back == -INFINITY) accept = false;
         else if (log_q == -INFINITY) accept = true;
         else accept = log(rng.real()) < ((ll_new - ll) * 1.0) - (log_q - log_q_back) + dprior;
-        if (lane == 0) stat[op]++;
+        if (tid == 0) stat[op]++;
         if (accept) {
-            if (lane == 0) stat[SBZ_N_OPS + op]++;
+            if (tid == 0) stat[SBZ_N_OPS + op]++;
             ll = ll_new;
             prior = prior + dprior;
             if (new_sources) commit_sources();
             if (sa >= 0) {
-                if (lane == 0) {
+                if (tid == 0) {
                     if (zoa < Z) zsize[zoa]--;
                     if (zna < Z) zsize[zna]++;
                     if (sb >= 0) zsize[zna]--;
@@ -564,7 +617,7 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
             }
         } else if (sa >= 0) {
             sync();
-            if (lane == 0) {  // undo the tentative zone change
+            if (tid == 0) {  // undo the tentative zone change
                 zos[sa] = (uint8_t)zoa;
                 if (sb >= 0) zos[sb] = (uint8_t)zna;
             }
@@ -575,15 +628,15 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
             // this accept replaces the reference's Sample object: the arrays of the logged
             // sample stop changing here (sbz.h, alias_pending)
             const size_t fs = (size_t)F * S;
-            for (size_t k = lane; k < fs; k += WAVE) ch.alias_p_global[b * fs + k] = ldp(pg + k);
-            for (size_t k = lane; k < (size_t)Z * fs; k += WAVE)
+            for (size_t k = tid; k < fs; k += NT) ch.alias_p_global[b * fs + k] = ldp(pg + k);
+            for (size_t k = tid; k < (size_t)Z * fs; k += NT)
                 ch.alias_p_zones[b * Z * fs + k] = ldp(pz + k);
             if (C == 3)
-                for (size_t k = lane; k < (size_t)Fam * fs; k += WAVE)
+                for (size_t k = tid; k < (size_t)Fam * fs; k += NT)
                     ch.alias_p_fam[b * Fam * fs + k] = ldp(pf + k);
             alias = 0;
         }
-        if (ch.trace_op && lane == 0) {
+        if (ch.trace_op && tid == 0) {
             const size_t t = (size_t)b * a.n_steps + step;
             ch.trace_op[t] = (int8_t)op;
             ch.trace_accept[t] = accept ? 1 : 0;
@@ -591,15 +644,16 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
         }
         if (ch.trace_zos) {
             uint8_t *tz = ch.trace_zos + ((size_t)b * a.n_steps + step) * N;
-            for (int s = lane; s < N; s += WAVE) tz[s] = zos[s];
+            for (int s = tid; s < N; s += NT) tz[s] = zos[s];
         }
+        if (bor(err)) break;  // an out-of-range index (reported below)
     }
 
     sync();
-    for (int s = lane; s < N; s += WAVE) gzos[s] = zos[s];
+    for (int s = tid; s < N; s += NT) gzos[s] = zos[s];
     if (!GS)
-        for (int c = lane; c < NF; c += WAVE) gsrc[c] = src[c];
-    if (lane == 0) {
+        for (int c = tid; c < NF; c += NT) gsrc[c] = src[c];
+    if (tid == 0) {
         ch.ll[b] = ll;
         if (ch.prior) ch.prior[b] = prior;
         if (ch.alias_pending) ch.alias_pending[b] = alias;
@@ -607,17 +661,17 @@ __global__ __launch_bounds__(WAVE) void mh_src_kernel(MhArgs a) {
         if (ch.counter) ch.counter[b] = rng.ctr;
         if (ch.status) ch.status[b] = broken ? 2 : (rng.bad ? 1 : 0);
     }
-    if (lane < SBZ_N_OPS) {  // per-operator counters, one lane each
-        if (ch.accepted) ch.accepted[(size_t)b * SBZ_N_OPS + lane] += stat[SBZ_N_OPS + lane];
-        if (ch.proposed) ch.proposed[(size_t)b * SBZ_N_OPS + lane] += stat[lane];
+    if (tid < SBZ_N_OPS) {  // per-operator counters, one thread each
+        if (ch.accepted) ch.accepted[(size_t)b * SBZ_N_OPS + tid] += stat[SBZ_N_OPS + tid];
+        if (ch.proposed) ch.proposed[(size_t)b * SBZ_N_OPS + tid] += stat[tid];
     }
-    {
-        const uint64_t bad = __ballot(err != 0);
-        if (bad) {
-            const int code = __shfl(err, (int)__builtin_ctzll(bad), 64);
-            if (lane == 0 && ch.status) ch.status[b] = 16 + code;
-        }
-    }
+    // an out-of-range index: the first faulting thread's code (status 16 + code)
+    sync();
+    if (tid == 0) redi[0] = 0;
+    sync();
+    if (err) atomicCAS(&redi[0], 0, err);
+    sync();
+    if (tid == 0 && redi[0] && ch.status) ch.status[b] = 16 + redi[0];
 }
 
 }  // namespace
@@ -630,30 +684,47 @@ int launch_mh_source(sbz_ctx *ctx, int B, const MhArgs &a0) {
     if (lds > LDS_MAX)
         return fail(ctx, SBZ_EINVAL, "SAMPLE_SOURCE sampler needs " + std::to_string(lds) +
                                          " B of LDS per chain even with the sources in HBM (> 160 KiB)");
+    const size_t nf = (size_t)ctx->d.n_sites * ctx->d.n_features;
     if (gs) {
-        const size_t nf = (size_t)ctx->d.n_sites * ctx->d.n_features;
         int rc = ensure(ctx, ctx->src_cand, (size_t)B * nf);
         if (rc) return rc;
         a.src_scratch = static_cast<uint8_t *>(ctx->src_cand.ptr);
     }
+    // waves per chain: 8 when the passes over the N * F observations dominate, else 4
+    // (SBZ_SRC_WAVES overrides: 1, 4 or 8).  8 waves = 2 per SIMD, so up to 256 VGPRs: no spills.
+    int nw = nf >= 16384 ? 8 : 4;
+    if (ctx->src_waves == 1 || ctx->src_waves == 4 || ctx->src_waves == 8) nw = ctx->src_waves;
     static bool configured = false;
     if (!configured) {
-        for (const void *fn : {reinterpret_cast<const void *>(&mh_src_kernel<2, false>),
-                               reinterpret_cast<const void *>(&mh_src_kernel<3, false>),
-                               reinterpret_cast<const void *>(&mh_src_kernel<2, true>),
-                               reinterpret_cast<const void *>(&mh_src_kernel<3, true>)}) {
+        const void *fns[] = {
+            reinterpret_cast<const void *>(&mh_src_kernel<2, false, 1>), reinterpret_cast<const void *>(&mh_src_kernel<3, false, 1>),
+            reinterpret_cast<const void *>(&mh_src_kernel<2, true, 1>), reinterpret_cast<const void *>(&mh_src_kernel<3, true, 1>),
+            reinterpret_cast<const void *>(&mh_src_kernel<2, false, 4>), reinterpret_cast<const void *>(&mh_src_kernel<3, false, 4>),
+            reinterpret_cast<const void *>(&mh_src_kernel<2, true, 4>), reinterpret_cast<const void *>(&mh_src_kernel<3, true, 4>),
+            reinterpret_cast<const void *>(&mh_src_kernel<2, false, 8>), reinterpret_cast<const void *>(&mh_src_kernel<3, false, 8>),
+            reinterpret_cast<const void *>(&mh_src_kernel<2, true, 8>), reinterpret_cast<const void *>(&mh_src_kernel<3, true, 8>)};
+        for (const void *fn : fns) {
             hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX);
             if (e != hipSuccess) return hip_fail(ctx, e, "hipFuncSetAttribute(sampler LDS)");
         }
         configured = true;
     }
-    if (ctx->C == 3) {
-        if (gs) mh_src_kernel<3, true><<<B, WAVE, lds, ctx->stream>>>(a);
-        else mh_src_kernel<3, false><<<B, WAVE, lds, ctx->stream>>>(a);
-    } else {
-        if (gs) mh_src_kernel<2, true><<<B, WAVE, lds, ctx->stream>>>(a);
-        else mh_src_kernel<2, false><<<B, WAVE, lds, ctx->stream>>>(a);
-    }
+    auto go = [&](auto cc, auto gsc, auto nwc) {
+        constexpr int CC = decltype(cc)::value, NWC = decltype(nwc)::value;
+        constexpr bool GSC = decltype(gsc)::value;
+        mh_src_kernel<CC, GSC, NWC><<<B, NWC * WAVE, lds, ctx->stream>>>(a);
+    };
+    auto by_nw = [&](auto cc, auto gsc) {
+        if (nw == 1) go(cc, gsc, std::integral_constant<int, 1>());
+        else if (nw == 4) go(cc, gsc, std::integral_constant<int, 4>());
+        else go(cc, gsc, std::integral_constant<int, 8>());
+    };
+    auto by_gs = [&](auto cc) {
+        if (gs) by_nw(cc, std::true_type());
+        else by_nw(cc, std::false_type());
+    };
+    if (ctx->C == 3) by_gs(std::integral_constant<int, 3>());
+    else by_gs(std::integral_constant<int, 2>());
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(ctx, e, "source-mode sampler launch");
     return SBZ_OK;
