@@ -49,6 +49,11 @@ def parse():
     p.add_argument("--mh-steps", type=int, default=50000,
                    help="sampler leg: timed MH steps per chain (0 disables the leg)")
     p.add_argument("--mh-burnin", type=int, default=200000, help="sampler leg: untimed MH steps")
+    p.add_argument("--src-steps", type=int, default=2000,
+                   help="source-mode sampler leg (cfg4 shape, SAMPLE_SOURCE = true): timed MH steps "
+                        "(0 = skip)")
+    p.add_argument("--src-burnin", type=int, default=2000, help="source-mode leg: untimed MH steps")
+    p.add_argument("--src-chains", type=int, default=128, help="source-mode leg: chains per GPU")
     return p.parse_args()
 
 
@@ -267,6 +272,103 @@ def sampler_leg(args, eng, obs, fam, dev, rank, world, stream):
     }
 
 
+# source-mode leg: config/default_config.json STEPS with SAMPLE_SOURCE = true (source 0.0: zone
+# moves resample the sources themselves), mcmc_setup.py:70-95
+SRC_STEPS_CFG = dict(MH_STEPS_CFG, source=0.0)
+CFG4 = {"sites": 100, "features": 36, "states": 5, "zones": 6, "families": 6}  # South America shape
+
+
+def src_operators(inh=True):
+    a = dict(SRC_STEPS_CFG)
+    if not inh:
+        a["inheritance"] = 0.0
+    ops = {"shrink_zone": a["area"] * 0.4, "grow_zone": a["area"] * 0.4, "swap_zone": a["area"] * 0.2,
+           "gibbsish_sample_zones": 0.0, "gibbs_sample_sources": a["source"],
+           "gibbs_sample_weights": a["weights"], "gibbs_sample_p_global": a["universal"],
+           "gibbs_sample_p_zones": a["contact"], "gibbs_sample_p_families": a["inheritance"]}
+    tot = sum(ops.values())
+    return {k: v / tot for k, v in ops.items()}
+
+
+def source_sampler_leg(shape, B, K, burnin, seed, rank=0, world=1, device=0):
+    """SAMPLE_SOURCE = true (the reference default) on synthetic data of `shape`: B chains per GPU
+    x K Philox MH steps in one launch after `burnin` untimed steps; steps/s and ESS/s of the
+    log-likelihood traces, max wall over ranks."""
+    import random
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from scipy.spatial import Delaunay
+    from contact_zones_amd import packing
+    from contact_zones_amd.diagnostics import ess
+    from contact_zones_amd.likelihood import LikelihoodEngine
+    from contact_zones_amd.mcmc import InitialSamples
+    from contact_zones_amd.sampler import ChainState, Sampler, precisions
+    from contact_zones_amd.sources import draw_sources, source_posterior
+    N, F, S, Z, Fam = (shape[k] for k in ("sites", "features", "states", "zones", "families"))
+    inh = Fam > 0
+    rng = np.random.default_rng(seed)  # same data and network on every rank
+    obs = rng.integers(0, S, size=(N, F)).astype(np.int8)
+    obs[rng.random((N, F)) < 0.02] = -1
+    fam = rng.integers(0, max(Fam, 1), size=N).astype(np.uint8)
+    fam[rng.random(N) < 0.2] = 255
+    if not inh:
+        fam[:] = 255
+    indptr, indices = Delaunay(rng.random((N, 2))).vertex_neighbor_vertices
+    states = np.ones((F, S), bool)
+    eng = LikelihoodEngine(obs, fam, S, Z, Fam, inh, device=device)
+    init = InitialSamples(packing.obs_to_features(obs, S), states, indptr, indices,
+                          packing.index_to_groups(fam, Fam) if inh else np.zeros((0, N), bool), Z,
+                          MH_M_INITIAL, inh, None, random.Random(seed * 1000003 + rank))
+    pg0, w0 = init.p_global()[0], init.weights()
+    pf0 = init.p_families() if inh else None
+    zos = np.empty((B, N), np.uint8)
+    pz = np.empty((B, Z, F, S))
+    src = np.empty((B, N, F), np.uint8)
+    draws = np.random.default_rng(seed + 31 * rank)
+    for b in range(B):  # generate_initial_sample per chain, with its initial source draw
+        zones = init.zones()
+        zos[b] = packing.zones_to_zone_of_site(zones, N)
+        pz[b] = init.p_zones(zones)
+        src[b] = draw_sources(source_posterior(obs, fam, zos[b], w0, pg0, pz[b], pf0, inh), draws.random)
+    rep = lambda x: np.broadcast_to(x, (B,) + x.shape).copy()  # noqa: E731
+    st = ChainState(eng, zos, rep(w0), rep(pg0), pz, rep(pf0) if inh else None, source=src)
+    smp = Sampler(eng, states, indptr, indices, src_operators(inh), precisions(MH_PRECISION), MH_MIN_M,
+                  sample_source=True)
+    if burnin:
+        smp.run(st, burnin, MH_MAX_M, MH_P_GROW, seed=seed * 7919, chain_id0=rank * B)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    out = smp.run(st, K, MH_MAX_M, MH_P_GROW, seed=seed * 7919, chain_id0=rank * B, trace=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    status = out["status"].cpu().numpy()
+    if np.any(status != 0):
+        raise SystemExit(f"source-mode leg: chain status {np.unique(status)}")
+    e = ess(out["ll"].cpu().numpy())
+    acc = out["accept"].float().mean().item()
+    t = torch.tensor([wall, float(e.sum()), acc], dtype=torch.float64, device=torch.device("cuda", device))
+    if world > 1:
+        mx, sm = t.clone(), t.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        t = torch.stack([mx[0], sm[1], sm[2] / world])
+    wall_max, ess_tot, acc_mean = (float(v) for v in t)
+    eng.close()
+    return {"workload": f"{N}x{F}x{S} Z{Z} Fam{Fam}, SAMPLE_SOURCE = true, {B} chains/GPU",
+            "mh_steps_per_sec": B * K * world / wall_max, "ess_per_sec": ess_tot / wall_max,
+            "ess_per_chain_mean": ess_tot / (B * world), "chains": B * world, "steps": K,
+            "burnin": burnin, "wall_s": wall_max, "us_per_step": wall_max / K * 1e6,
+            "acceptance": acc_mean,
+            "sources": "HBM" if 2 * N * F > 150 * 1024 else "LDS",
+            "operators": "default_config.json STEPS with source 0.0 (zone moves resample every "
+                         "source), Gibbs parameter operators; Philox draws"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -344,6 +446,10 @@ def main():
     sampler = None
     if args.mh_steps > 0 and args.mode == "mixture":
         sampler = sampler_leg(args, eng, obs, fam, dev, rank, world, stream)
+    sampler_src = None
+    if args.src_steps > 0:
+        sampler_src = source_sampler_leg(CFG4, args.src_chains, args.src_steps, args.src_burnin,
+                                         args.seed, rank, world, local_rank)
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -386,6 +492,8 @@ def main():
         }
         if sampler is not None:
             line["sampler"] = sampler
+        if sampler_src is not None:
+            line["sampler_source_mode"] = sampler_src
         if world == 1 and args.cpu_seconds > 0:
             line["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
             line["speedup_vs_cpu"] = value / line["cpu_baseline"]["value"]
