@@ -74,6 +74,7 @@ SIGNATURES = {
     "sbz_lik_lds_bytes": (ctypes.c_uint64, [ctypes.POINTER(sbz_dims), _I]),
     "sbz_set_network": (_I, [_P, _P, ctypes.c_int32, _P, _P]),
     "sbz_set_priors": (_I, [_P, _P, _P, ctypes.c_int32]),
+    "sbz_set_geo_prior": (_I, [_P, _P, ctypes.c_double]),
     "sbz_set_gibbs_counts": (_I, [_P, _P, _P]),
     "sbz_mh_run_device": (_I, [_P, _I, _I, ctypes.POINTER(sbz_mh_config), ctypes.POINTER(sbz_chains)]),
     "sbz_mh_lds_bytes": (ctypes.c_uint64, [ctypes.POINTER(sbz_dims)]),

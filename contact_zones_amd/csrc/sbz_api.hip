@@ -226,7 +226,7 @@ void sbz_close(sbz_ctx *ctx) {
     for (void *p : {(void *)ctx->d_obs_sm, (void *)ctx->d_fam_site, (void *)ctx->d_adj_ptr,
                     (void *)ctx->d_adj_idx, (void *)ctx->d_app_list, (void *)ctx->d_app_cnt,
                     (void *)ctx->d_alpha_g, (void *)ctx->d_alpha_f, (void *)ctx->d_gc_g,
-                    (void *)ctx->d_gc_f})
+                    (void *)ctx->d_gc_f, (void *)ctx->d_geo_cost})
         if (p) (void)hipFree(p);
     if (ctx->d_cnt) (void)hipFree(ctx->d_cnt);
     free_buf(ctx->zl);
@@ -385,6 +385,26 @@ int sbz_set_priors(sbz_ctx *ctx, const double *alpha_global, const double *alpha
     if (rc == SBZ_OK) rc = upload(alpha_fam, (size_t)ctx->d.n_families * fs, &ctx->d_alpha_f);
     if (rc == SBZ_OK) ctx->size_prior = size_prior;
     return rc;
+}
+
+int sbz_set_geo_prior(sbz_ctx *ctx, const double *cost, double scale) {
+    if (!ctx) return SBZ_EINVAL;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->d_geo_cost) (void)hipFree(ctx->d_geo_cost);
+    ctx->d_geo_cost = nullptr;
+    ctx->geo_scale = 0.0;
+    if (!cost) return SBZ_OK;
+    if (!(scale > 0.0) || std::isinf(scale)) return fail(ctx, SBZ_EINVAL, "geo prior scale must be finite and > 0");
+    const size_t n = (size_t)ctx->d.n_sites * ctx->d.n_sites;
+    for (size_t i = 0; i < n; i++)
+        if (!(cost[i] >= 0.0) || std::isnan(cost[i]))
+            return fail(ctx, SBZ_EINVAL, "geo prior costs must be >= 0 (inf: no edge)");
+    if (hipMalloc(&ctx->d_geo_cost, n * sizeof(double)) != hipSuccess)
+        return fail(ctx, SBZ_ENOMEM, "geo prior allocation failed");
+    hipError_t e = hipMemcpy(ctx->d_geo_cost, cost, n * sizeof(double), hipMemcpyHostToDevice);
+    if (e != hipSuccess) return hip_fail(ctx, e, "geo prior upload");
+    ctx->geo_scale = scale;
+    return SBZ_OK;
 }
 
 int sbz_set_gibbs_counts(sbz_ctx *ctx, const double *counts_global, const double *counts_fam) {

@@ -63,6 +63,8 @@ struct sbz_ctx {
     double *d_alpha_g = nullptr;  // [F][S] 'counts' prior on p_global (sbz_set_priors) or null
     double *d_alpha_f = nullptr;  // [Fam][F][S] 'counts' prior on p_families or null
     int size_prior = 0;           // 0 none, 1 uniform, 2 quadratic
+    double *d_geo_cost = nullptr; // [N][N] 'cost_based' geo prior costs (sbz_set_geo_prior) or null
+    double geo_scale = 0.0;
     double *d_gc_g = nullptr;     // [F][S] Gibbs prior counts of p_global (sbz_set_gibbs_counts)
     double *d_gc_f = nullptr;     // [Fam][F][S] of p_families
     int zspl = 8;          // zoned sites per lane and chunk of the zone-sparse kernel
@@ -102,7 +104,7 @@ inline int np_of(int n_sites) {
 }
 
 // Sampler (sbz_mh.hip)
-size_t mh_lds_bytes(const sbz_dims &d, int C);
+size_t mh_lds_bytes(const sbz_dims &d, int C, bool geo = false);
 int launch_mh(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg, const sbz_chains *chains);
 
 // Launch the likelihood kernels for B chains (all pointers device); out_ll device [B].

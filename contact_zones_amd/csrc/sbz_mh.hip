@@ -45,8 +45,9 @@ namespace {
 // c (CH = NT * KT sites per chunk, nsc chunks); zos / nb / lst are padded to NpS = nsc * CH.
 struct MhLayout {
     int KT, CH, nsc, NpS, nent, ncol;
-    size_t col, zsize, red, nb, zos, selc, lst, stat, tabo, tabn, nw, rowp, ipos, clsinfo, total;
-    __host__ __device__ MhLayout(int N, int Np, int S, int Z, int Fam, int C, int FamC, int NT) {
+    size_t col, zsize, red, nb, zos, selc, lst, stat, tabo, tabn, nw, rowp, ipos, clsinfo, geo, total;
+    __host__ __device__ MhLayout(int N, int Np, int S, int Z, int Fam, int C, int FamC, int NT,
+                                 bool with_geo = false) {
         KT = Np / NT;
         KT = KT < 4 ? 4 : (KT > 32 ? 32 : KT);
         CH = NT * KT;
@@ -74,6 +75,8 @@ struct MhLayout {
         rowp = take((size_t)Np * 4);
         ipos = take((size_t)N * 2);
         clsinfo = take((size_t)((Z + 1) * FamC + 1) * 2);
+        // geo prior scratch (geo_zone_prior): key [N] doubles, mem [N] u16, cnt + redd / redi [16]
+        geo = with_geo ? take(geo_scratch_bytes(N)) : o;
         total = o;
     }
 };
@@ -98,7 +101,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
     const int N = a.N, F = a.F, S = a.S, Z = a.Z, Fam = (C == 3) ? a.Fam : 0;
     const sbz_chains &ch = a.ch;
 
-    const MhLayout L(N, a.Np, S, Z, a.Fam, C, a.FamC, NT);
+    const MhLayout L(N, a.Np, S, Z, a.Fam, C, a.FamC, NT, a.geo_cost != nullptr);
     const int KT = L.KT, CH = L.CH, nsc = L.nsc, ncol = L.ncol;
     double *col = reinterpret_cast<double *>(lds + L.col);  // staged parameter column
     int *zsize = reinterpret_cast<int *>(lds + L.zsize);     // [Z]
@@ -199,6 +202,17 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
 
     double ll = ch.ll[b];
     double prior = ch.prior ? ch.prior[b] : 0.0;  // carried log prior (sbz_set_priors)
+    // 'cost_based' geo prior: only the last zone counts (model.py:1110-1139); its current value
+    double *geo_key = reinterpret_cast<double *>(lds + L.geo);
+    uint16_t *geo_mem = reinterpret_cast<uint16_t *>(geo_key + N);
+    int *geo_cnt = reinterpret_cast<int *>(geo_mem + ((N + 7) & ~7));
+    double *geo_rd = reinterpret_cast<double *>(geo_cnt + 4);
+    int *geo_ri = reinterpret_cast<int *>(geo_rd + 16);
+    auto geo_prior = [&](int add, int rm1, int rm2) -> double {
+        return geo_zone_prior<NWV>(a.geo_cost, a.geo_scale, N, zos, Z - 1, add, rm1, rm2, geo_key,
+                                   geo_mem, geo_cnt, geo_rd, geo_ri);
+    };
+    double geo_cur = (a.geo_cost && Z > 0) ? geo_prior(-1, -1, -1) : 0.0;
     int err = 0;             // first range-check failure of this thread (MH_IDX)
     long long err_val = 0;
     const long long nFS = (long long)F * S, nZFS = (long long)Z * F * S, nFamFS = (long long)Fam * F * S;
@@ -692,6 +706,14 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             }
         }
 
+        // the geo prior of the last zone, when the move changes it
+        double geo_new = geo_cur;
+        if (a.geo_cost && sa >= 0 && (zna == Z - 1 || zoa == Z - 1)) {
+            geo_new = geo_prior(zna == Z - 1 ? sa : -1, zoa == Z - 1 ? sa : -1,
+                                (sb >= 0 && zna == Z - 1) ? sb : -1);
+            dprior = uni(dprior + (geo_new - geo_cur));
+        }
+
         if (SBZ_MH_STAMP) tph[3] = __builtin_amdgcn_s_memtime();
         // ---- 4. metropolis_hastings_ratio (mcmc_generative.py:331-351, uniform priors)
         bool accept = false;
@@ -708,6 +730,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             if (tid == 0) stat[SBZ_N_OPS + op]++;
             ll = ll + delta;
             prior = prior + dprior;
+            geo_cur = geo_new;
             if (sa >= 0) {
                 if (tid == 0) {
                     const int fca = C == 3 ? (int)a.fam_site[sa] : 0;
@@ -776,10 +799,10 @@ constexpr int MH_WAVES = 4;  // waves per chain (one workgroup per chain)
 
 }  // namespace
 
-size_t mh_lds_bytes(const sbz_dims &d, int C) {
+size_t mh_lds_bytes(const sbz_dims &d, int C, bool geo) {
     const int FamC = C == 3 ? d.n_families + 1 : 1;
     return MhLayout(d.n_sites, np_of(d.n_sites), d.n_states, d.n_zones, d.n_families, C, FamC,
-                    MH_WAVES * WAVE).total;
+                    MH_WAVES * WAVE, geo).total;
 }
 
 int launch_mh(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg, const sbz_chains *chains) {
@@ -849,6 +872,8 @@ int launch_mh(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg, const 
     a.size_prior = ctx->size_prior;
     a.gc_g = ctx->d_gc_g;
     a.gc_f = ctx->C == 3 ? ctx->d_gc_f : nullptr;
+    a.geo_cost = d.n_zones > 0 ? ctx->d_geo_cost : nullptr;
+    a.geo_scale = ctx->geo_scale;
     a.ch = *chains;
     if (!a.ch.zone_of_site || !a.ch.w || !a.ch.p_global || !a.ch.ll || !a.ch.max_size ||
         !a.ch.p_grow_connected || (d.n_zones > 0 && !a.ch.p_zones) ||
@@ -862,7 +887,7 @@ int launch_mh(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg, const 
         return fail(ctx, SBZ_EINVAL, "tape mode needs tape_pos and tape_len");
     if (src) return launch_mh_source(ctx, B, a);
     if (d.n_sites > 65535) return fail(ctx, SBZ_EINVAL, "sampler supports at most 65535 sites");
-    const size_t lds = mh_lds_bytes(d, ctx->C);
+    const size_t lds = mh_lds_bytes(d, ctx->C, a.geo_cost != nullptr);
     if (lds > 64 * 1024) return fail(ctx, SBZ_EINVAL, "sampler state exceeds 64 KiB of LDS (too many sites)");
     if (ctx->C == 3) mh_kernel<3, MH_WAVES><<<B, MH_WAVES * WAVE, lds, ctx->stream>>>(a);
     else mh_kernel<2, MH_WAVES><<<B, MH_WAVES * WAVE, lds, ctx->stream>>>(a);

@@ -397,8 +397,103 @@ struct MhArgs {
     const double *gc_g;         // [F][S] Gibbs prior counts of p_global (sbz_set_gibbs_counts) or null = 1
     const double *gc_f;         // [Fam][F][S] of p_families, or null = 1
     uint8_t *src_scratch;       // [B][N][F] candidate sources when they live in HBM (source mode)
+    const double *geo_cost;     // [N][N] 'cost_based' geo prior costs (sbz_set_geo_prior), or null
+    double geo_scale;
     sbz_chains ch;
 };
+
+// GeoPrior 'cost_based' (geo_prior_distance, sbayes/model.py:1096-1139) of zone zt with the
+// tentative change (+add, -rm1, -rm2; -1 = none): the mean exponential(scale) log density
+// -(d / scale) - log(scale) over the positive-cost edges of the minimum spanning tree of the
+// zone's cost submatrix (scipy's sparse tree leaves zero-cost edges out; inf = no edge, a forest
+// then), -log(scale) when no edge is positive.  Prim's algorithm, block-cooperative: the members
+// are gathered into mem[], key[] holds each unused member's cheapest link (-1 once in the tree),
+// and one block argmin (ties: lowest index) per added vertex.  Every thread gets the same value.
+// LDS scratch: key [N] doubles, mem [N] u16, cnt 1 int, redd / redi [NW].
+__host__ __device__ constexpr size_t geo_scratch_bytes(int N) {
+    return (size_t)N * 8 + (size_t)((N + 7) & ~7) * 2 + 16 + 16 * 8 + 16 * 4;
+}
+
+template <int NW>
+__device__ double geo_zone_prior(const double *cost, double scale, int N, const uint8_t *zos, int zt,
+                                 int add, int rm1, int rm2, double *key, uint16_t *mem, int *cnt,
+                                 double *redd, int *redi) {
+    constexpr int NT = NW * 64;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    auto bar = [&]() { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+    if (tid == 0) *cnt = 0;
+    bar();
+    for (int s = tid; s < N; s += NT) {
+        const bool in = (zos[s] == zt && s != rm1 && s != rm2) || s == add;
+        if (in) mem[atomicAdd(cnt, 1)] = (uint16_t)s;
+    }
+    bar();
+    const int m = uni(*cnt);
+    const double lsc = log(scale);
+    if (m <= 1) {  // (the reference raises "Too few locations"; zones have >= MIN_M sites)
+        bar();
+        return -lsc;
+    }
+    for (int i = tid; i < m; i += NT) key[i] = i == 0 ? 0.0 : INFINITY;
+    bar();
+    double sum = 0.0;
+    int npos = 0;
+    for (int it = 0; it < m; it++) {
+        double bk = INFINITY;
+        int bi = 0x7fffffff;
+        for (int i = tid; i < m; i += NT) {
+            const double k = key[i];
+            if (k >= 0.0 && (k < bk || (k == bk && i < bi))) {
+                bk = k;
+                bi = i;
+            }
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const double ok = __shfl_xor(bk, off, 64);
+            const int oi = __shfl_xor(bi, off, 64);
+            if (ok < bk || (ok == bk && oi < bi)) {
+                bk = ok;
+                bi = oi;
+            }
+        }
+        if (lane == 0) {
+            redd[wv] = bk;
+            redi[wv] = bi;
+        }
+        bar();
+        bk = redd[0];
+        bi = redi[0];
+#pragma unroll
+        for (int w = 1; w < NW; w++)
+            if (redd[w] < bk || (redd[w] == bk && redi[w] < bi)) {
+                bk = redd[w];
+                bi = redi[w];
+            }
+        bi = uni(bi);
+        if (bk > 0.0 && bk < INFINITY) {  // a positive tree edge (bk == inf: a new component)
+            sum += -(bk / scale) - lsc;
+            npos++;
+        }
+        const double *row = cost + (size_t)mem[bi] * N;
+        for (int i = tid; i < m; i += NT) {
+            if (i == bi) {
+                key[i] = -1.0;
+            } else {
+                const double k = key[i];
+                if (k >= 0.0) {
+                    const double c = row[mem[i]];
+                    if (c < k) key[i] = c;
+                }
+            }
+        }
+        bar();
+    }
+    double r;
+    if (npos > 0) r = sum / (double)npos;
+    else r = -lsc;
+    return uni(r);
+}
 
 // Normalised operator probabilities -> cumulative table (numpy choice(p), mcmc_generative.py:294).
 constexpr int MH_STAT_INTS = 2 * SBZ_N_OPS;  // LDS counters: proposed | accepted
@@ -406,7 +501,7 @@ constexpr int MH_SRC_MAX_WAVES = 16;         // waves per chain of the source-mo
 
 // SAMPLE_SOURCE = true sampler (sbz_mh_src.hip): LDS bytes per chain (sources in LDS, or in
 // HBM: hbm_sources) and the launch.
-size_t mh_src_lds_bytes(const sbz_dims &d, int C, bool hbm_sources = false);
+size_t mh_src_lds_bytes(const sbz_dims &d, int C, bool hbm_sources = false, bool geo = false);
 int launch_mh_source(sbz_ctx *ctx, int B, const MhArgs &a);
 
 }  // namespace sbz

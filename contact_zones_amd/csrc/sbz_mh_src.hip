@@ -79,13 +79,13 @@ __device__ __forceinline__ int posterior_draw(const double (&l)[3], const double
 
 }  // namespace
 
-size_t mh_src_lds_bytes(const sbz_dims &d, int C, bool hbm_sources) {
+size_t mh_src_lds_bytes(const sbz_dims &d, int C, bool hbm_sources, bool geo) {
     const size_t N = d.n_sites, F = d.n_features, S = d.n_states, Z = d.n_zones;
     const size_t cnt = F * (S > (size_t)C ? S : (size_t)C);
     return MH_SRC_MAX_WAVES * 2 * (8 + 4) + cnt * 4 + ((Z + 1) & ~(size_t)1) * 4 + MH_STAT_INTS * 4 +
            ((N + 1) & ~(size_t)1) * 2 +
            (hbm_sources ? 0 : ((N * F + 15) & ~(size_t)15) * 2) + ((N + 15) & ~(size_t)15) +
-           ((F + 15) & ~(size_t)15);
+           ((F + 15) & ~(size_t)15) + (geo ? 16 + geo_scratch_bytes((int)N) : 0);
 }
 
 namespace {
@@ -123,6 +123,13 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     uint8_t *srcb = src + (GS ? 0 : ((NF + 15) & ~15));              // [N][F] candidate sources
     uint8_t *zos = srcb + (GS ? 0 : ((NF + 15) & ~15));              // [N] zone of site
     uint8_t *sub = zos + ((N + 15) & ~15);                           // [F] feature subset
+    // geo prior scratch (geo_zone_prior), 16-B aligned after the subset
+    const size_t geo_off = ((size_t)(sub + ((F + 15) & ~15) - lds) + 15) & ~(size_t)15;
+    double *geo_key = reinterpret_cast<double *>(lds + geo_off);
+    uint16_t *geo_mem = reinterpret_cast<uint16_t *>(geo_key + N);
+    int *geo_cnt = reinterpret_cast<int *>(geo_mem + ((N + 7) & ~7));
+    double *geo_rd = reinterpret_cast<double *>(geo_cnt + 4);
+    int *geo_ri = reinterpret_cast<int *>(geo_rd + 16);
 
     uint8_t *gzos = ch.zone_of_site + (size_t)b * N;
     uint8_t *gsrc = ch.source + (size_t)b * NF;
@@ -195,6 +202,12 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     }
     int occupied = (int)bsum((double)occ);
     sync();
+    // 'cost_based' geo prior: only the last zone counts (model.py:1110-1139); its current value
+    auto geo_prior = [&]() -> double {
+        return geo_zone_prior<NW>(a.geo_cost, a.geo_scale, N, zos, Z - 1, -1, -1, -1, geo_key, geo_mem,
+                                  geo_cnt, geo_rd, geo_ri);
+    };
+    double geo_cur = (a.geo_cost && Z > 0) ? geo_prior() : 0.0;
 
     Rng rng;
     rng.tape = ch.tape ? ch.tape + (size_t)b * ch.tape_stride : nullptr;
@@ -411,6 +424,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         double dprior = 0.0, ll_new = ll;
         int sa = -1, zoa = NONE, zna = NONE, sb = -1;
         bool new_sources = false;
+        double geo_new = geo_cur;
 
         if (zone_op) {
             // ---- zone move with source resampling
@@ -485,6 +499,10 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                     if (sb >= 0) zos[sb] = NONE;
                 }
                 sync();
+                if (a.geo_cost && (zna == Z - 1 || zoa == Z - 1)) {  // the last zone changed
+                    geo_new = geo_prior();
+                    dprior = uni(dprior + (geo_new - geo_cur));
+                }
                 double log_q_s;
                 pass_resample(log_q_s, ll_new);
                 new_sources = true;
@@ -605,6 +623,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             if (tid == 0) stat[SBZ_N_OPS + op]++;
             ll = ll_new;
             prior = prior + dprior;
+            geo_cur = geo_new;
             if (new_sources) commit_sources();
             if (sa >= 0) {
                 if (tid == 0) {
@@ -679,8 +698,9 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
 int launch_mh_source(sbz_ctx *ctx, int B, const MhArgs &a0) {
     MhArgs a = a0;
     constexpr size_t LDS_MAX = 160 * 1024;
-    const bool gs = ctx->src_hbm || mh_src_lds_bytes(ctx->d, ctx->C) > LDS_MAX;  // do not fit: HBM
-    const size_t lds = mh_src_lds_bytes(ctx->d, ctx->C, gs);
+    const bool geo = a.geo_cost != nullptr;
+    const bool gs = ctx->src_hbm || mh_src_lds_bytes(ctx->d, ctx->C, false, geo) > LDS_MAX;  // do not fit: HBM
+    const size_t lds = mh_src_lds_bytes(ctx->d, ctx->C, gs, geo);
     if (lds > LDS_MAX)
         return fail(ctx, SBZ_EINVAL, "SAMPLE_SOURCE sampler needs " + std::to_string(lds) +
                                          " B of LDS per chain even with the sources in HBM (> 160 KiB)");

@@ -30,7 +30,8 @@ def _type(obj):
 class PriorSpec:
     """The prior terms of the MH ratio (defaults: all zero)."""
 
-    def __init__(self, alpha_global=None, alpha_fam=None, size_prior="none"):
+    def __init__(self, alpha_global=None, alpha_fam=None, size_prior="none", geo_cost=None,
+                 geo_scale=None):
         self.alpha_global = None if alpha_global is None else np.ascontiguousarray(alpha_global, np.float64)
         self.alpha_fam = None if alpha_fam is None else np.ascontiguousarray(alpha_fam, np.float64)
         if isinstance(size_prior, str):
@@ -40,10 +41,14 @@ class PriorSpec:
         if size_prior not in (0, 1, 2):
             raise ValueError(f"size_prior must be 0, 1 or 2, got {size_prior}")
         self.size_prior = int(size_prior)
+        # 'cost_based' geo prior (GeoPrior, model.py:979-1139): cost matrix [N][N] and scale
+        self.geo_cost = None if geo_cost is None else np.ascontiguousarray(geo_cost, np.float64)
+        self.geo_scale = None if geo_cost is None else float(geo_scale)
 
     @property
     def is_zero(self):
-        return self.alpha_global is None and self.alpha_fam is None and self.size_prior == 0
+        return (self.alpha_global is None and self.alpha_fam is None and self.size_prior == 0
+                and self.geo_cost is None)
 
     @classmethod
     def from_model(cls, model, states):
@@ -55,7 +60,11 @@ class PriorSpec:
             return cls()
         states = np.asarray(states, bool)
         F, S = states.shape
-        for name, ok in (("geo_prior", ("uniform",)), ("prior_weights", ("uniform",)),
+        geo = getattr(prior, "geo_prior", None)
+        geo_cost = geo_scale = None
+        if _type(geo) == "cost_based":
+            geo_cost, geo_scale = geo.cost_matrix, geo.scale
+        for name, ok in (("geo_prior", ("uniform", "cost_based")), ("prior_weights", ("uniform",)),
                          ("prior_p_zones", ("uniform",))):
             t = _type(getattr(prior, name, None))
             if t is not None and t not in ok:
@@ -81,7 +90,7 @@ class PriorSpec:
                         af[fam, f, states[f]] = pf.dirichlet[fam][f]
             elif t not in (None, "uniform"):
                 raise NotImplementedError(f"inheritance prior of type '{t}' is not supported")
-        return cls(ag, af, size)
+        return cls(ag, af, size, geo_cost, geo_scale)
 
     def log_prior(self, zone_of_site, p_global, p_fam, states, n_zones, inheritance):
         """Log prior of B chain states: zone_of_site [B][N] (255 = none), p_global [B][F][S],
@@ -98,7 +107,11 @@ class PriorSpec:
             out = out + (-np.sum(np.log(sizes ** 2), axis=1))
         else:
             out = out + 0.
-        out = out + 0.  # geo
+        if self.geo_cost is not None and n_zones:
+            out = out + np.array([geo_prior_distance(zos[b] == n_zones - 1, self.geo_cost, self.geo_scale)
+                                  for b in range(B)])
+        else:
+            out = out + 0.  # geo
         out = out + 0.  # weights
         if self.alpha_global is not None:
             pg = np.asarray(p_global, np.float64).reshape(B, states.shape[0], states.shape[1])
@@ -129,3 +142,19 @@ def _dirichlet_logpdf_rows(p, alpha, states):
         lnB = np.sum(gammaln(a)) - gammaln(np.sum(a))
         out[:, f] = -lnB + np.sum(xlogy(a - 1, p[:, f, idx]), axis=1)
     return out
+
+
+def geo_prior_distance(zone, cost, scale):
+    """GeoPrior 'cost_based' (model.py:1096-1139) as the reference evaluates it: the log density of
+    an exponential(scale) at every edge of the minimum spanning tree of the zone's cost matrix
+    (scipy csgraph, zero-cost edges leave the sparse tree), averaged.  The reference's zone loop
+    overwrites the value, so only the LAST zone counts; callers pass that zone's mask."""
+    from scipy import stats
+    from scipy.sparse.csgraph import csgraph_from_dense, minimum_spanning_tree
+    zone = np.asarray(zone, bool)
+    cz = np.asarray(cost)[zone][:, zone]
+    if cz.shape[0] <= 1:
+        raise ValueError("Too few locations to compute distance.")
+    mst = minimum_spanning_tree(csgraph_from_dense(cz, null_value=np.inf))
+    distances = mst.tocsr()[mst.nonzero()] if mst.nnz > 0 else 0
+    return float(np.mean(stats.expon.logpdf(distances, loc=0, scale=scale)))

@@ -181,6 +181,14 @@ class Sampler:
         check(eng._lib.sbz_set_priors(eng.ctx, vp(ag.ctypes.data) if ag is not None else None,
                                       vp(af.ctypes.data) if af is not None else None,
                                       int(p.size_prior)), eng.ctx)
+        cost = None
+        if p.geo_cost is not None:
+            cost = np.ascontiguousarray(p.geo_cost, np.float64)
+            N = eng.n_sites
+            if cost.shape != (N, N):
+                raise ValueError(f"geo_cost: expected {(N, N)}, got {cost.shape}")
+        check(eng._lib.sbz_set_geo_prior(eng.ctx, vp(cost.ctypes.data) if cost is not None else None,
+                                         float(p.geo_scale) if cost is not None else 0.0), eng.ctx)
         self.priors = p
 
     def run(self, state, n_steps, max_size, p_grow_connected, seed=0, chain_id0=0, tape=None,

@@ -196,6 +196,16 @@ int sbz_set_network(sbz_ctx *ctx, const uint8_t *applicable, int32_t nnz, const 
 int sbz_set_priors(sbz_ctx *ctx, const double *alpha_global, const double *alpha_fam,
                    int32_t size_prior);
 
+/* 'cost_based' geo prior (GeoPrior, sbayes/model.py:979-1139; experiments/simulation/sim_exp2):
+ *   cost   double [N][N] row-major cost matrix between sites (load_data.py:106-121: a cost file,
+ *          or the distance matrix), or NULL to switch the geo prior off (uniform, 0);
+ *   scale  > 0, the exponential's scale.
+ * The geo prior is the mean exp(scale) log density over the edges of the minimum spanning tree
+ * of the LAST zone's cost submatrix (geo_prior_distance, model.py:1096-1139, overwrites its value
+ * in the zone loop, so zone n_zones - 1 alone counts; zero-cost edges are not counted, as in
+ * scipy's sparse tree).  Zone moves that change that zone add the difference to the MH ratio. */
+int sbz_set_geo_prior(sbz_ctx *ctx, const double *cost, double scale);
+
 /* Prior pseudo-counts of the source-mode Gibbs operators (SAMPLE_SOURCE = true): p_global is
  * redrawn from Dirichlet(counts_global[f] + source counts) (gibbs_sample_p_global,
  * zone_sampling.py:334-357; PGlobalPrior.counts, model.py:576-586), p_families from

@@ -57,6 +57,19 @@ class TapeReader:
         return np.asarray(v, np.float64)
 
 
+def geo_prior_distance(zone, cost, scale):
+    """geo_prior_distance (model.py:1096-1139) for one zone mask: scipy MST of the zone's cost
+    submatrix (csgraph_from_dense, null_value inf), mean exponential log density of its edges."""
+    from scipy import stats
+    from scipy.sparse.csgraph import csgraph_from_dense, minimum_spanning_tree
+    cz = np.asarray(cost)[zone][:, zone]
+    if cz.shape[0] <= 1:
+        raise ValueError("Too few locations to compute distance.")
+    mst = minimum_spanning_tree(csgraph_from_dense(cz, null_value=np.inf))
+    distances = mst.tocsr()[mst.nonzero()] if mst.nnz > 0 else 0
+    return float(np.mean(stats.expon.logpdf(distances, loc=0, scale=scale)))
+
+
 def dirichlet_logpdf(x, alpha):
     """scipy.stats.dirichlet._logpdf: -(sum gammaln(a) - gammaln(sum a)) + sum xlogy(a - 1, x)."""
     lnB = np.sum(gammaln(alpha)) - gammaln(np.sum(alpha))
@@ -103,6 +116,8 @@ class Model:
         self.size_prior = int(fx["prior_size"]) if "prior_size" in fx else 0
         self.alpha_global = fx.get("prior_alpha_global")
         self.alpha_fam = fx.get("prior_alpha_fam")
+        self.geo_cost = fx.get("prior_geo_cost")
+        self.geo_scale = float(fx["prior_geo_scale"]) if "prior_geo_scale" in fx else None
 
     def log_prior(self, st):
         """Prior.__call__ (model.py:484-505) for the supported types: zone size 'none' /
@@ -119,7 +134,10 @@ class Model:
             log_prior += -np.sum(np.log(sizes ** 2))
         else:
             log_prior += 0.
-        log_prior += 0.  # geo
+        if self.geo_cost is not None:  # GeoPrior 'cost_based': the last zone only (model.py:1110-1139)
+            log_prior += geo_prior_distance(zos == self.n_zones - 1, self.geo_cost, self.geo_scale)
+        else:
+            log_prior += 0.  # geo
         log_prior += 0.  # weights
         if self.alpha_global is not None:
             lp = np.zeros(self.states.shape[0])

@@ -42,3 +42,12 @@ def gpu_available():
     if n < 1:
         pytest.fail("gpu test selected but no HIP device is visible")
     return n
+
+
+def prior_spec(fx):
+    """The PriorSpec of a captured MH case (tests/golden/make_golden_mh.py): 'counts'
+    concentrations, zone-size prior and the 'cost_based' geo prior's cost matrix and scale."""
+    from contact_zones_amd.priors import PriorSpec
+    return PriorSpec(fx.get("prior_alpha_global"), fx.get("prior_alpha_fam"), int(fx["prior_size"]),
+                     fx.get("prior_geo_cost"),
+                     float(fx["prior_geo_scale"]) if "prior_geo_scale" in fx else None)

@@ -309,6 +309,9 @@ def run_case(name, data, model_cfg, mcmc_cfg, steps, seed, warmup, n_chains):
             for f in range(F):
                 af[fam, f, states[f]] = pr.prior_p_families.dirichlet[fam][f]
         out["prior_alpha_fam"] = af
+    if model_cfg["PRIOR"]["geo"]["type"] == "cost_based":  # GeoPrior (model.py:979-1139)
+        out["prior_geo_cost"] = np.asarray(data.geo_prior["cost_matrix"], np.float64)
+        out["prior_geo_scale"] = np.array(float(model_cfg["PRIOR"]["geo"]["scale"]))
     out["init_prior"] = np.array([init_prior[c] for c in range(n_chains)])
     if warmup:
         out["best_zone_of_site"] = packing.zones_to_zone_of_site(best.zones, N)
@@ -400,8 +403,9 @@ def small_data(seed=7, N=40, F=12, S=4, fam=2):
     return types.SimpleNamespace(features=x, states=states, network=net, families=fams)
 
 
-def model_cfg(Z, inheritance, min_m=3, max_m=50, counts=False, size="none", source=False):
-    prior = {"geo": {"type": "uniform"}, "area_size": {"type": size},
+def model_cfg(Z, inheritance, min_m=3, max_m=50, counts=False, size="none", source=False, geo=None):
+    prior = {"geo": {"type": "cost_based", "scale": geo} if geo else {"type": "uniform"},
+             "area_size": {"type": size},
              "weights": {"type": "uniform"}, "universal": {"type": "uniform"},
              "inheritance": {"type": "uniform"}, "contact": {"type": "uniform"}}
     if counts:  # as experiments/balkan/config.json:34-50
@@ -424,6 +428,13 @@ def with_counts(d, seed=11):
                                  prior_inheritance={"counts": ci})
 
 
+def with_geo(d, cost=None):
+    """Attach the geo prior's cost matrix (load_data.py:106-121: the network's distance matrix
+    when no cost file is given)."""
+    c = d.network["dist_mat"] if cost is None else cost
+    return types.SimpleNamespace(**{**vars(d), "geo_prior": {"cost_matrix": np.asarray(c, np.float64)}})
+
+
 def mcmc_cfg(area=0.4, m_initial=5, p_grow=0.85, inheritance=0.1, source=0.0):
     return {"P_GROW_CONNECTED": p_grow, "M_INITIAL": m_initial,
             "PROPOSAL_PRECISION": {"weights": 15, "universal": 40, "contact": 20, "inheritance": 20},
@@ -431,7 +442,29 @@ def mcmc_cfg(area=0.4, m_initial=5, p_grow=0.85, inheritance=0.1, source=0.0):
                       "inheritance": inheritance, "source": source}}
 
 
+def geo_cases():
+    """Cost-based geo prior (experiments/simulation/sim_exp2/config.json:50-53): only the last
+    zone's MST enters the prior (model.py:1110-1139 overwrites log_prior in its zone loop)."""
+    s = small_data()
+    run_case("small_geo", with_geo(s), model_cfg(2, True, min_m=3, max_m=8, geo=30.0),
+             mcmc_cfg(area=0.8, m_initial=4), steps=300, seed=15, warmup=False, n_chains=3)
+    # integer costs with ties and zeros (zero-cost edges leave the MST's nonzero count)
+    rng = np.random.default_rng(16)
+    n = s.features.shape[0]
+    c = rng.integers(0, 6, size=(n, n)).astype(float)
+    c = np.triu(c, 1)
+    c = c + c.T
+    run_case("small_geo_ties_warmup", with_geo(s, c), model_cfg(2, True, min_m=3, max_m=8, geo=2.0),
+             mcmc_cfg(area=0.8, m_initial=4), steps=200, seed=17, warmup=True, n_chains=4)
+    run_case("src_geo", with_geo(s), model_cfg(2, True, min_m=3, max_m=8, source=True, geo=30.0),
+             mcmc_cfg(area=0.4, m_initial=4, source=0.05), steps=150, seed=18, warmup=False,
+             n_chains=2)
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "geo":
+        geo_cases()
+        return
     d = sim_data()
     run_case("cfg1_sim", d, model_cfg(1, False), mcmc_cfg(inheritance=0.0), steps=300, seed=3,
              warmup=False, n_chains=2)

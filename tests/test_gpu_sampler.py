@@ -5,7 +5,7 @@ the GPU) stay within the north_star tolerance of 1e-9 relative of the reference'
 import numpy as np
 import pytest
 
-from conftest import golden_cases, load_golden, mh_cases
+from conftest import prior_spec, golden_cases, load_golden, mh_cases
 
 pytestmark = pytest.mark.gpu
 
@@ -22,7 +22,7 @@ def _setup(fx):
     Fam = fx["init_p_fam"].shape[1] if inh else 0
     eng = LikelihoodEngine(fx["obs"], fx["fam_of_site"], S, Z, Fam, inh)
     from contact_zones_amd.priors import PriorSpec
-    priors = PriorSpec(fx.get("prior_alpha_global"), fx.get("prior_alpha_fam"), int(fx["prior_size"]))
+    priors = prior_spec(fx)
     smp = Sampler(eng, fx["states"], fx["adj_indptr"], fx["adj_indices"], fx["op_probs"],
                   fx["precision"], int(fx["min_size"]), warmup=bool(fx["warmup"]), priors=priors)
     st = ChainState(eng, fx["init_zone_of_site"], fx["init_w"], fx["init_p_global"],
@@ -122,7 +122,7 @@ def test_philox_carried_prior_matches_full_prior(gpu_available):
     torch.cuda.synchronize()
     assert out["status"].cpu().numpy().tolist() == [0] * st.B
     s = st.to_numpy()
-    spec = PriorSpec(fx["prior_alpha_global"], fx["prior_alpha_fam"], int(fx["prior_size"]))
+    spec = prior_spec(fx)
     full = spec.log_prior(s["zone_of_site"], s["p_global"], s["p_fam"], fx["states"],
                           int(fx["n_zones"]), True)
     np.testing.assert_allclose(s["prior"], full, rtol=1e-12)

@@ -6,7 +6,7 @@ log-likelihoods within the north_star tolerance of 1e-9 relative."""
 import numpy as np
 import pytest
 
-from conftest import load_golden, mh_cases
+from conftest import prior_spec, load_golden, mh_cases
 
 pytestmark = pytest.mark.gpu
 
@@ -34,7 +34,7 @@ def _setup(fx):
     Z = int(fx["n_zones"])
     Fam = fx["init_p_fam"].shape[1] if inh else 0
     eng = LikelihoodEngine(fx["obs"], fx["fam_of_site"], S, Z, Fam, inh)
-    priors = PriorSpec(fx.get("prior_alpha_global"), fx.get("prior_alpha_fam"), int(fx["prior_size"]))
+    priors = prior_spec(fx)
     smp = Sampler(eng, fx["states"], fx["adj_indptr"], fx["adj_indices"], fx["op_probs"],
                   fx["precision"], int(fx["min_size"]), warmup=bool(fx["warmup"]), priors=priors,
                   sample_source=True,
@@ -126,7 +126,7 @@ def test_source_philox_chains_are_valid(gpu_available, src_home):
     np.testing.assert_allclose(s["p_zones"].sum(-1), 1.0, rtol=1e-12)
     fresh = st.refresh_ll().cpu().numpy()
     assert np.max(np.abs(s["ll"] - fresh) / np.abs(fresh)) <= REL_TOL
-    spec = PriorSpec(fx.get("prior_alpha_global"), fx.get("prior_alpha_fam"), int(fx["prior_size"]))
+    spec = prior_spec(fx)
     full = spec.log_prior(s["zone_of_site"], s["p_global"], s["p_fam"], fx["states"],
                           int(fx["n_zones"]), bool(fx["inheritance"]))
     np.testing.assert_allclose(s["prior"], full, rtol=1e-12, atol=1e-12)

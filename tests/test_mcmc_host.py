@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 import scipy.sparse as sp
 
-from conftest import golden_cases, load_golden, mh_cases
+from conftest import prior_spec, golden_cases, load_golden, mh_cases
 from contact_zones_amd import packing
 from contact_zones_amd.mcmc import (BatchedZoneMCMC, BatchedZoneMCMCWarmup, InitialSamples,
                                     check_model, get_max_size_list)
@@ -40,8 +40,7 @@ def objects_from_fixture(fx):
     kw = dict(model=model, data=data, operators=ops, n_chains=fx["init_w"].shape[0],
               var_proposal=var_proposal, p_grow_connected=float(fx["p_grow_base"]),
               initial_size=int(fx["initial_size"]),
-              priors=PriorSpec(fx.get("prior_alpha_global"), fx.get("prior_alpha_fam"),
-                               int(fx["prior_size"])))
+              priors=prior_spec(fx))
     if bool(fx.get("sample_source", False)):
         kw["gibbs_counts"] = (fx["gibbs_counts_global"], fx.get("gibbs_counts_fam"))
     return kw

@@ -7,14 +7,14 @@ from enum import Enum
 import numpy as np
 import pytest
 
-from conftest import golden_cases, load_golden
+from conftest import prior_spec, golden_cases, load_golden
 from contact_zones_amd.priors import PriorSpec
 
 MH_CASES = golden_cases("mh_", exclude=())
 
 
 def spec_from_fixture(fx):
-    return PriorSpec(fx.get("prior_alpha_global"), fx.get("prior_alpha_fam"), int(fx["prior_size"]))
+    return prior_spec(fx)
 
 
 @pytest.mark.parametrize("case", MH_CASES)
@@ -34,6 +34,7 @@ class T(Enum):
     NONE = "none"
     QUADRATIC = "quadratic"
     COST = "cost_based"
+    GAUSS = "gaussian"
 
 
 def fake_prior(pg="uniform", pf="uniform", size="none", geo="uniform", F=3, S=4, n_fam=2):
@@ -60,7 +61,7 @@ def test_spec_from_reference_prior_objects():
     assert PriorSpec.from_model(types.SimpleNamespace(inheritance=False), states).is_zero
 
 
-@pytest.mark.parametrize("kw", [dict(pg="universal"), dict(pf="universal"), dict(geo="cost_based")])
+@pytest.mark.parametrize("kw", [dict(pg="universal"), dict(pf="universal"), dict(geo="gaussian")])
 def test_unsupported_prior_types_raise(kw):
     model, states, _, _ = fake_prior(**kw)
     with pytest.raises(NotImplementedError):
@@ -79,3 +80,13 @@ def test_size_prior_values():
     assert np.isclose(q, -(log(4) + log(9)), rtol=1e-13)
     with pytest.raises(NotImplementedError):
         PriorSpec(size_prior="exponential")
+
+
+def test_geo_prior_from_reference_object():
+    """'cost_based' geo priors carry the reference GeoPrior's cost matrix and scale."""
+    model, states, _, _ = fake_prior(geo="cost_based")
+    cost = np.arange(16.0).reshape(4, 4)
+    model.prior.geo_prior.cost_matrix, model.prior.geo_prior.scale = cost, 7.0
+    s = PriorSpec.from_model(model, states)
+    assert s.geo_scale == 7.0 and not s.is_zero
+    np.testing.assert_array_equal(s.geo_cost, cost)
