@@ -9,7 +9,8 @@ reference package.
                 network, prior counts)
   operators     sbayes/mcmc_setup.py:70-95 (steps_per_operator)
   priors        sbayes/model.py:538-680: 'counts' priors on p_global / p_families
-                (initial count 1 + scale_counts), zone-size prior; geo / weights / contact
+                (initial count 1 + scale_counts), zone-size prior, 'cost_based' geo prior
+                (cost file or the distance matrix, model.py:979-1139); weights / contact
                 must be 'uniform' (NotImplementedError otherwise, as the batched sampler)
   sampling      warm-up: BatchedZoneMCMCWarmup, N_WARM_UP_CHAINS chains in one launch; main:
                 BatchedZoneMCMC from the warm-up's best sample (mcmc_setup.py:97-121, 174-187)
@@ -117,6 +118,11 @@ def load_config(config_file, custom_settings=None):
                 prior["file"] = fix(prior["file"])
             elif key == "inheritance":
                 prior["files"] = {fam: fix(p) for fam, p in prior["files"].items()}
+        if prior["type"] == "cost_based":
+            if "scale" not in prior:
+                raise NameError(f"scale for geo prior is not defined in {config_file}.")
+            if "file" in prior:
+                prior["file"] = fix(prior["file"])
     mcmc["N_CHAINS"] = 1  # MC3 is disabled in the reference (experiment_setup.py:200-206)
     if mcmc["N_STEPS"] % mcmc["N_SAMPLES"] != 0:
         raise ValueError("Non-consistent spacing between samples. Set N_STEPS to be a multiple of N_SAMPLES. ")
@@ -193,6 +199,13 @@ class ExperimentData:
             self.universal_counts, lg = io.read_universal_counts(
                 t, pri["universal"]["file"], pri["universal"]["file_type"], d["FEATURE_STATES"])
             self.log.append(lg)
+        self.geo_cost = None
+        if pri["geo"]["type"] == "cost_based":  # load_geo_cost_matrix (load_data.py:106-121)
+            if "file" in pri["geo"]:
+                self.geo_cost, lg = io.read_geo_cost_matrix([str(x) for x in t.site_ids], pri["geo"]["file"])
+                self.log.append(lg)
+            else:
+                self.geo_cost = dist
         if config["model"]["INHERITANCE"] and pri["inheritance"]["type"] == "counts":
             self.inheritance_counts, lg = io.read_inheritance_counts(
                 t, pri["inheritance"]["files"], pri["inheritance"]["file_type"], d["FEATURE_STATES"])
@@ -206,9 +219,11 @@ def build_priors(config, data):
     from .priors import PriorSpec
     model = config["model"]
     pri = model["PRIOR"]
-    for key in ("geo", "weights", "contact"):
+    for key in ("weights", "contact"):
         if pri[key]["type"] != "uniform":
             raise NotImplementedError(f"{key} prior of type '{pri[key]['type']}' is not supported")
+    if pri["geo"]["type"] not in ("uniform", "cost_based"):
+        raise NotImplementedError(f"geo prior of type '{pri['geo']['type']}' is not supported")
     F, S = data.states.shape
     Fam = data.families.shape[0]
     cg = np.ones((F, S))
@@ -234,7 +249,9 @@ def build_priors(config, data):
         elif t != "uniform":
             raise NotImplementedError(f"inheritance prior of type '{t}' is not supported")
     size = pri["area_size"]["type"]
-    return PriorSpec(ag, af, size), (cg, cf)
+    geo_cost = data.geo_cost if pri["geo"]["type"] == "cost_based" else None
+    geo_scale = pri["geo"]["scale"] if geo_cost is not None else None
+    return PriorSpec(ag, af, size, geo_cost, geo_scale), (cg, cf)
 
 
 def model_spec(config, n_zones):

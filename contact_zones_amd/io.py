@@ -255,6 +255,23 @@ def read_inheritance_counts(tab: FeatureTable, files, file_type, feature_states_
     return counts_all.astype(int), log
 
 
+def read_geo_cost_matrix(site_ids, file):
+    """read_geo_cost_matrix (preprocessing.py:677-700, read_costs_from_csv util.py:417-428): the
+    cost CSV (site ids as header and index) ordered by the features file's site ids, as float;
+    made symmetric by averaging when it is not.  Returns (cost [N][N], log)."""
+    import pandas as pd
+    costs = pd.read_csv(file, dtype=str, index_col=0)
+    costs.index = costs.index.astype(str)  # (numeric ids would otherwise index as integers)
+    log = f"Geographical cost matrix read from {file}."
+    assert set(costs.columns) == set(site_ids)
+    cost = np.asarray(costs.loc[list(site_ids), list(site_ids)]).astype(float)
+    if not np.allclose(cost, cost.T):
+        cost = (cost + cost.T) / 2
+        log += (".The cost matrix is not symmetric. It was made symmetric by averaging the original"
+                " costs along the upper and lower triangle.")
+    return cost, log
+
+
 def compute_network(locations):
     """The Delaunay graph of the sites (util.py:158-175, qhull options "QJ Pp") as the CSR
     arrays the sampler takes (indptr, indices), and the Euclidean distance matrix
@@ -376,7 +393,7 @@ def samples2file(samples, data, config, paths):
 
 __all__ = ["FeatureTable", "read_features_packed", "read_features_from_csv",
            "read_feature_occurrence_from_csv", "read_universal_counts", "read_inheritance_counts",
-           "compute_network", "format_area_columns", "stats_columns", "samples2file",
+           "compute_network", "read_geo_cost_matrix", "format_area_columns", "stats_columns", "samples2file",
            "extract_feature_states"]
 
 

@@ -56,3 +56,30 @@ def test_balkan_experiment_end_to_end(gpu_available, tmp_path, source):
                                    stats["sample_p_global"][s][0], stats["sample_p_zones"][s],
                                    stats["sample_p_families"][s], inheritance=True)
             assert ll[s] == pytest.approx(ref, rel=1e-9)
+
+
+def test_balkan_experiment_geo_prior(gpu_available, tmp_path):
+    """A 'cost_based' geo prior (the distance matrix as costs): every logged prior equals the host
+    restatement of the reference's Prior (PriorSpec.log_prior, scipy MST) on that sample."""
+    cfg, _ = experiment.load_config(CFG, {**_short(tmp_path, SAMPLE_SOURCE=False),
+                                          "model": {"N_AREAS": 2, "SAMPLE_SOURCE": False,
+                                                    "PRIOR": {"geo": {"type": "cost_based", "scale": 2.0}}}})
+    data = experiment.ExperimentData(cfg)
+    spec, _ = experiment.build_priors(cfg, data)
+    stats, _ = experiment.run_experiment(cfg, data, 2, name="g", seed=5)
+    t = data.table
+    # match_areas / rank_areas relabel the zones after sampling (the logged priors keep the
+    # sampling-time labels, as the reference's), and only the last zone enters the geo prior:
+    # the logged prior is the prior of one of the two labelings
+    n_geo = 0
+    for s in range(len(stats["sample_zones"])):
+        refs = []
+        for order in ((0, 1), (1, 0)):
+            zos = np.full((1, t.n_sites), 255, np.uint8)
+            for z in range(2):
+                zos[0, stats["sample_zones"][s][order[z]]] = z
+            refs.append(spec.log_prior(zos, stats["sample_p_global"][s][0][None],
+                                       stats["sample_p_families"][s][None], data.states, 2, True)[0])
+        assert any(stats["sample_prior"][s] == pytest.approx(r, rel=1e-9, abs=1e-9) for r in refs)
+        n_geo += refs[0] != refs[1]
+    assert n_geo > 0  # the geo term differs between the zones

@@ -159,3 +159,17 @@ def test_experiment_config_errors(tmp_path):
     c.write_text(json.dumps({"simulation": {}, "model": {}}))
     with pytest.raises(NotImplementedError):
         experiment.load_config(c)
+
+
+def test_geo_cost_matrix_reader(tmp_path):
+    """read_geo_cost_matrix (preprocessing.py:677-700): rows / columns ordered by the features
+    file's site ids, symmetrised by averaging when the file is not symmetric."""
+    import pandas as pd
+    ids = ["b", "a", "c"]
+    raw = pd.DataFrame([[0, 1, 4], [3, 0, 2], [4, 2, 0]], index=["a", "b", "c"], columns=["a", "b", "c"])
+    raw.to_csv(tmp_path / "cost.csv")
+    cost, log = io.read_geo_cost_matrix(ids, tmp_path / "cost.csv")
+    sym = (raw.values + raw.values.T) / 2
+    order = [1, 0, 2]
+    np.testing.assert_array_equal(cost, sym[np.ix_(order, order)])
+    assert "made symmetric" in log
