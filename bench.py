@@ -50,10 +50,11 @@ def parse():
                    help="sampler leg: timed MH steps per chain (0 disables the leg)")
     p.add_argument("--mh-burnin", type=int, default=200000, help="sampler leg: untimed MH steps")
     p.add_argument("--src-steps", type=int, default=2000,
-                   help="source-mode sampler leg (cfg4 shape, SAMPLE_SOURCE = true): timed MH steps "
-                        "(0 = skip)")
-    p.add_argument("--src-burnin", type=int, default=2000, help="source-mode leg: untimed MH steps")
-    p.add_argument("--src-chains", type=int, default=128, help="source-mode leg: chains per GPU")
+                   help="real-data sampler legs (the reference's Balkan / South America configs, "
+                        "SAMPLE_SOURCE = true): timed MH steps (0 = skip)")
+    p.add_argument("--src-burnin", type=int, default=2000, help="real-data legs: untimed MH steps")
+    p.add_argument("--src-chains", type=int, default=128,
+                   help="real-data legs: chains per GPU (South America; Balkan runs twice as many)")
     return p.parse_args()
 
 
@@ -369,6 +370,87 @@ def source_sampler_leg(shape, B, K, burnin, seed, rank=0, world=1, device=0):
                          "source), Gibbs parameter operators; Philox draws"}
 
 
+EXPERIMENTS = os.path.join(ROOT, "tests", "golden", "io", "data", "experiments")  # the reference's data
+
+
+def real_data_leg(name, n_zones_list, B, K, burnin, seed, rank=0, world=1, device=0):
+    """The reference's own experiment configs on their real data (experiments/<name>/config.json:
+    features, counts priors, STEPS, PROPOSAL_PRECISION, MIN_M / MAX_M / M_INITIAL, SAMPLE_SOURCE
+    default true), B chains per GPU from generate_initial_sample, K Philox MH steps after `burnin`,
+    for each number of zones: steps/s and ESS/s of the log-likelihood traces (max wall over
+    ranks, ESS summed over ranks)."""
+    import random
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from contact_zones_amd import experiment, packing
+    from contact_zones_amd.diagnostics import ess
+    from contact_zones_amd.likelihood import LikelihoodEngine
+    from contact_zones_amd.mcmc import InitialSamples
+    from contact_zones_amd.sampler import ChainState, Sampler, precisions
+    path = os.path.join(EXPERIMENTS, name, "config.json")
+    cfg0, _ = experiment.load_config(path, {"model": {"N_AREAS": int(n_zones_list[0])}})
+    data = experiment.ExperimentData(cfg0)
+    t = data.table
+    m, mc = cfg0["model"], cfg0["mcmc"]
+    inh, src_mode = bool(m["INHERITANCE"]), bool(m["SAMPLE_SOURCE"])
+    Fam = len(t.family_names) if inh else 0
+    indptr, indices = data.network["adj_mat"].indptr, data.network["adj_mat"].indices
+    out = {"data": f"{name}: {t.n_sites} sites x {t.n_features} features x {t.n_states} states, "
+                   f"{Fam} families, SAMPLE_SOURCE = {src_mode}, {B} chains/GPU",
+           "runs": {}}
+    for Z in n_zones_list:
+        cfg, _ = experiment.load_config(path, {"model": {"N_AREAS": int(Z)}})
+        spec, gibbs = experiment.build_priors(cfg, data)
+        eng = LikelihoodEngine(t.obs, t.fam_of_site, t.n_states, Z, Fam, inh, device=device)
+        smp = Sampler(eng, t.applicable, indptr, indices, experiment.operators(cfg),
+                      precisions(mc["PROPOSAL_PRECISION"]), int(m["MIN_M"]), priors=spec,
+                      sample_source=src_mode, gibbs_counts=gibbs if src_mode else None)
+        init = InitialSamples(data.features, t.applicable, indptr, indices, data.families, Z,
+                              mc["M_INITIAL"], inh, None, random.Random(seed * 1000003 + 7919 * rank + Z),
+                              sample_source=src_mode)
+        np.random.seed(seed + 31 * rank + Z)  # the initial source draws (np.random, as the reference)
+        samples = [init(b) for b in range(B)]
+        zos = np.stack([packing.zones_to_zone_of_site(x.zones, t.n_sites) for x in samples])
+        w = np.stack([x.weights for x in samples])
+        pg = np.stack([np.asarray(x.p_global)[0] for x in samples])
+        pz = np.stack([x.p_zones for x in samples])
+        pf = np.stack([x.p_families for x in samples]) if inh else None
+        src = np.stack([packing.source_to_index(x.source) for x in samples]) if src_mode else None
+        prior = spec.log_prior(zos, pg, pf, t.applicable, Z, inh)
+        st = ChainState(eng, zos, w, pg, pz, pf, prior=prior, source=src)
+        max_m, p_grow = int(m["MAX_M"]), float(mc["P_GROW_CONNECTED"])
+        if burnin:
+            smp.run(st, burnin, max_m, p_grow, seed=seed * 7919 + Z, chain_id0=rank * B)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        res = smp.run(st, K, max_m, p_grow, seed=seed * 7919 + Z, chain_id0=rank * B, trace=True)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        wall = time.perf_counter() - t0
+        status = res["status"].cpu().numpy()
+        if np.any(status != 0):
+            raise SystemExit(f"{name} leg: chain status {np.unique(status)}")
+        e = ess(res["ll"].cpu().numpy())
+        tt = torch.tensor([wall, float(e.sum()), res["accept"].float().mean().item()],
+                          dtype=torch.float64, device=torch.device("cuda", device))
+        if world > 1:
+            mx, sm = tt.clone(), tt.clone()
+            dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+            dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+            tt = torch.stack([mx[0], sm[1], sm[2] / world])
+        wall_max, ess_tot, acc = (float(v) for v in tt)
+        out["runs"][f"Z={Z}"] = {"chains": B * world, "steps": K, "burnin": burnin,
+                                 "mh_steps_per_sec": B * K * world / wall_max,
+                                 "ess_per_sec": ess_tot / wall_max, "us_per_step": wall_max / K * 1e6,
+                                 "acceptance": acc}
+        eng.close()
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -446,10 +528,15 @@ def main():
     sampler = None
     if args.mh_steps > 0 and args.mode == "mixture":
         sampler = sampler_leg(args, eng, obs, fam, dev, rank, world, stream)
-    sampler_src = None
+    real = None
     if args.src_steps > 0:
-        sampler_src = source_sampler_leg(CFG4, args.src_chains, args.src_steps, args.src_burnin,
-                                         args.seed, rank, world, local_rank)
+        # configs[2] (Balkan, 3 zones, 256 chains) and configs[3] (South America, K = 1..6 zone
+        # sweep, 128 chains per GPU = 512 over 4 GPUs) on the reference's own data
+        real = {"cfg3_balkan": real_data_leg("balkan", [3], args.src_chains * 2, args.src_steps,
+                                             args.src_burnin, args.seed, rank, world, local_rank),
+                "cfg4_south_america": real_data_leg("south_america", [1, 2, 3, 4, 5, 6], args.src_chains,
+                                                    args.src_steps, args.src_burnin, args.seed, rank,
+                                                    world, local_rank)}
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -492,8 +579,8 @@ def main():
         }
         if sampler is not None:
             line["sampler"] = sampler
-        if sampler_src is not None:
-            line["sampler_source_mode"] = sampler_src
+        if real is not None:
+            line["sampler_real_data"] = real
         if world == 1 and args.cpu_seconds > 0:
             line["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
             line["speedup_vs_cpu"] = value / line["cpu_baseline"]["value"]
