@@ -63,8 +63,10 @@ def make_shared(args, rng):
     N, F, S, Fam = args.sites, args.features, args.states, args.families
     obs = rng.integers(0, S, size=(N, F)).astype(np.int8)
     obs[rng.random((N, F)) < 0.02] = -1
-    fam = rng.integers(0, Fam, size=N).astype(np.uint8)
+    fam = rng.integers(0, max(Fam, 1), size=N).astype(np.uint8)
     fam[rng.random(N) < 0.2] = 255
+    if Fam == 0:  # no families: the model without inheritance (C = 2)
+        fam[:] = 255
     return obs, fam
 
 
@@ -72,7 +74,7 @@ def make_chains_torch(args, n_chains, gen, dev):
     """Chain states on the device: disjoint zones of --zone-size sites, Dirichlet(1) parameters."""
     import torch
     N, F, S, Z, Fam = args.sites, args.features, args.states, args.zones, args.families
-    C = 3
+    C = 3 if Fam > 0 else 2
 
     zone_size = min(args.zone_size, N // max(Z, 1))
     perm = torch.argsort(torch.rand(n_chains, N, generator=gen, device=dev), dim=1)
@@ -89,22 +91,23 @@ def make_chains_torch(args, n_chains, gen, dev):
 
     pg = probs(n_chains, F)
     pz = probs(n_chains, Z, F)
-    pf = probs(n_chains, Fam, F)
+    pf = probs(n_chains, Fam, F) if Fam > 0 else None
     src = None
     if args.mode == "source":  # allowed components only: global, zone where zoned, family where present
         r = torch.rand(n_chains, N, F, generator=gen, device=dev)
         src = torch.zeros(n_chains, N, F, dtype=torch.uint8, device=dev)
         src[(zos[:, :, None] != 255) & (r > 0.5)] = 1
         fam_t = torch.as_tensor(args._fam, device=dev)
-        src[(fam_t[None, :, None] != 255) & (r < 0.25)] = 2
+        if C == 3:
+            src[(fam_t[None, :, None] != 255) & (r < 0.25)] = 2
     return dict(zos=zos.contiguous(), w=w.contiguous(), pg=pg.contiguous(), pz=pz.contiguous(),
-                pf=pf.contiguous(), src=src)
+                pf=pf.contiguous() if pf is not None else None, src=src)
 
 
 def algorithmic_bytes(args, B, source=False):
     """bytes/eval = P + D/B; a launch of B chains moves B*P + D bytes."""
     N, F, S, Z, Fam = args.sites, args.features, args.states, args.zones, args.families
-    C = 3
+    C = 3 if Fam > 0 else 2
     P = 8 * F * S * (1 + Z + Fam) + 8 * F * C + N + (N * F if source else 0)
     D = N * F + N
     return P, D, B * P + D
@@ -143,14 +146,15 @@ def cpu_baseline(args, seconds):
     zs = min(args.zone_size, N // max(Z, 1))
     for z in range(Z):
         zos[perm[z * zs:(z + 1) * zs]] = z
-    w = rng.dirichlet(np.ones(3), size=F)
+    inh = Fam > 0
+    w = rng.dirichlet(np.ones(3 if inh else 2), size=F)
     pg = rng.dirichlet(np.ones(S), size=F)
     pz = rng.dirichlet(np.ones(S), size=(Z, F))
-    pf = rng.dirichlet(np.ones(S), size=(Fam, F))
+    pf = rng.dirichlet(np.ones(S), size=(Fam, F)) if inh else None
     n = 0
     t0 = time.perf_counter()
     while True:
-        lik_numpy.loglik(obs, fam, zos, w, pg, pz, pf, inheritance=True)
+        lik_numpy.loglik(obs, fam, zos, w, pg, pz, pf, inheritance=inh)
         n += 1
         el = time.perf_counter() - t0
         if el >= seconds:
@@ -474,7 +478,8 @@ def main():
     rng = np.random.default_rng(args.seed)
     obs, fam = make_shared(args, rng)  # replicated on every rank (1 MB)
     args._fam = fam
-    eng = LikelihoodEngine(obs, fam, args.states, args.zones, args.families, True, device=local_rank)
+    eng = LikelihoodEngine(obs, fam, args.states, args.zones, args.families, args.families > 0,
+                           device=local_rank)
     stream = torch.cuda.current_stream()
     eng.set_stream(stream.cuda_stream)
 
@@ -488,7 +493,7 @@ def main():
     def step(i):
         c = pool[i % args.pool]
         eng.loglik_device(B, c["zos"].data_ptr(), c["w"].data_ptr(), c["pg"].data_ptr(),
-                          c["pz"].data_ptr(), c["pf"].data_ptr(),
+                          c["pz"].data_ptr(), c["pf"].data_ptr() if c["pf"] is not None else 0,
                           c["src"].data_ptr() if src_mode else 0, out[i % args.pool].data_ptr())
 
     for i in range(args.warmup):
@@ -526,7 +531,7 @@ def main():
 
     traffic, traffic_src = pmc_traffic(args, B)
     sampler = None
-    if args.mh_steps > 0 and args.mode == "mixture":
+    if args.mh_steps > 0 and args.mode == "mixture" and args.families > 0:
         sampler = sampler_leg(args, eng, obs, fam, dev, rank, world, stream)
     real = None
     if args.src_steps > 0:

@@ -1211,17 +1211,58 @@ __global__ __launch_bounds__(WAVE) void lik_source_kernel(LikArgs a) {
 }
 
 // Row-major source [B][N][F] -> feature-major [B][F][Np] in the family-sorted site order
-// (padded sites -> component 0).
-__global__ void repack_source_kernel(int B, int N, int F, int Np, const int *perm, const uint8_t *src,
-                                     uint8_t *dst) {
-    const size_t total = (size_t)B * F * Np;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-         i += (size_t)gridDim.x * blockDim.x) {
-        const int s = (int)(i % Np);
-        const size_t r = i / Np;
-        const int f = (int)(r % F);
-        const int b = (int)(r / F);
-        dst[i] = s < N ? src[((size_t)b * N + perm[s]) * F + f] : 0;
+// (padded sites -> component 0).  One workgroup transposes a tile of 64 positions x 64 features
+// through LDS: each site's 64 feature bytes are read as one contiguous run (4-byte words when F
+// is a multiple of 4), each feature's 64 position bytes written as 16-byte stores.
+constexpr int RP_T = 64;
+__global__ __launch_bounds__(256) void repack_source_kernel(int N, int F, int Np, const int *perm,
+                                                            const uint8_t *src, uint8_t *dst) {
+    __shared__ uint8_t tile[RP_T][RP_T + 4];  // [position][feature]
+    const int tid = threadIdx.x;
+    const int p0 = blockIdx.x * RP_T, f0 = blockIdx.y * RP_T;
+    const size_t b = blockIdx.z;
+    {
+        const int r = tid >> 2, q = tid & 3;  // row (position) r, 16 features from f0 + 16 q
+        const int p = p0 + r;
+        const int fq = f0 + 16 * q;
+        uint8_t v[16];
+        if (p < N) {
+            const uint8_t *row = src + (b * N + perm[p]) * F;
+            if ((F & 3) == 0 && fq + 16 <= F) {
+                const uint32_t *w = reinterpret_cast<const uint32_t *>(row + fq);
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t x = w[k];
+#pragma unroll
+                    for (int j = 0; j < 4; j++) v[4 * k + j] = (uint8_t)(x >> (8 * j));
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 16; j++) v[j] = fq + j < F ? row[fq + j] : 0;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 16; j++) v[j] = 0;
+        }
+#pragma unroll
+        for (int j = 0; j < 16; j++) tile[r][16 * q + j] = v[j];
+    }
+    __syncthreads();
+    {
+        const int fr = tid >> 2, q = tid & 3;  // feature f0 + fr, positions p0 + 16 q ..
+        const int f = f0 + fr;
+        if (f < F) {
+            uint32_t w[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                uint32_t x = 0;
+#pragma unroll
+                for (int j = 0; j < 4; j++) x |= (uint32_t)tile[16 * q + 4 * k + j][fr] << (8 * j);
+                w[k] = x;
+            }
+            // Np is a multiple of 64, so the 16 bytes are 16-byte aligned and inside the row
+            *reinterpret_cast<uint4 *>(dst + (b * F + f) * Np + p0 + 16 * q) = make_uint4(w[0], w[1], w[2], w[3]);
+        }
     }
 }
 
@@ -1520,9 +1561,9 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
         const size_t bytes = (size_t)B * F * ctx->Np;
         rc = ensure(ctx, ctx->src_t, bytes);
         if (rc) return rc;
-        const int blocks = (int)std::min<size_t>((bytes + 255) / 256, 8192);
-        repack_source_kernel<<<blocks, 256, 0, ctx->stream>>>(B, d.n_sites, F, ctx->Np, ctx->d_perm, source,
-                                                             static_cast<uint8_t *>(ctx->src_t.ptr));
+        const dim3 rgrid(ctx->Np / RP_T, (F + RP_T - 1) / RP_T, B);
+        repack_source_kernel<<<rgrid, 256, 0, ctx->stream>>>(d.n_sites, F, ctx->Np, ctx->d_perm, source,
+                                                            static_cast<uint8_t *>(ctx->src_t.ptr));
         a.src_fm = static_cast<const uint8_t *>(ctx->src_t.ptr);
     }
 
