@@ -162,6 +162,52 @@ class GpuLikelihood:
         self.everything_updated(sample)
         return float(ll)
 
+    # ---- the arrays the reference's own CPU operators read from the likelihood object
+    # (zone_sampling.py:193-199, 239-240, 283, 305-306, 716-719, 801-804, 878-881), so that this
+    # object can also replace Likelihood under the reference's sampler in SAMPLE_SOURCE mode.
+    # They are host arrays by contract; the GPU sampler (BatchedZoneMCMC) never calls them.
+    # Sites that left a zone get a zone likelihood of 0 here where the reference's cache keeps
+    # a stale value; both are masked by a zone weight of 0.
+    def _packed(self, sample):
+        zone_of_site, w, pg, pz, pf, _ = pack_sample(sample, self.n_sites)
+        return zone_of_site, w, pg, pz, pf
+
+    def get_zone_assignment(self, sample):
+        """model.py:248-252: has_zone per site."""
+        return np.any(np.asarray(sample.zones, bool), axis=0)
+
+    def update_weights(self, sample):
+        """model.py:251-294: normalised weights (n_sites, n_features, C)."""
+        from .sources import normalized_weights
+        zone_of_site, w, _, _, _ = self._packed(sample)
+        return normalized_weights(self._fam, zone_of_site, w, self.inheritance)
+
+    def update_component_likelihoods(self, sample, caching=True):
+        """model.py:230-249: component likelihoods (n_sites, n_features, C), NA cells 1."""
+        from .sources import component_likelihoods
+        zone_of_site, _, pg, pz, pf = self._packed(sample)
+        return component_likelihoods(self._obs, self._fam, zone_of_site, pg, pz, pf, self.inheritance)
+
+    def get_global_lh(self, sample):
+        """model.py:190-202: p_global gathered at every observation (0 at NA cells)."""
+        lh = self.update_component_likelihoods(sample)[..., 0].copy()
+        lh[self.na_features] = 0.0
+        return lh
+
+    def get_family_lh(self, sample):
+        """model.py:204-217 (None without inheritance)."""
+        if not self.inheritance:
+            return None
+        lh = self.update_component_likelihoods(sample)[..., 2].copy()
+        lh[self.na_features] = 0.0
+        return lh
+
+    def get_zone_lh(self, sample):
+        """model.py:219-228."""
+        lh = self.update_component_likelihoods(sample)[..., 1].copy()
+        lh[self.na_features] = 0.0
+        return lh
+
     def everything_updated(self, sample):
         """Clear the 'lh' dirty flags exactly as the reference does (model.py:186-192)."""
         wc = getattr(sample, "what_changed", None)

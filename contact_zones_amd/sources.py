@@ -12,10 +12,10 @@ import numpy as np
 from .packing import NONE
 
 
-def source_posterior(obs, fam_of_site, zone_of_site, w, p_global, p_zones, p_fam, inheritance):
-    """(N, F, C) normalize(lh * weights) for one chain in packed form (obs int8 [N][F], -1 = NA):
-    lh per component as update_component_likelihoods (model.py:224-247; NA -> 1, a site outside
-    every zone / family -> 0), weights as update_weights -> normalize_weights (:284-292, 436-452)."""
+def component_likelihoods(obs, fam_of_site, zone_of_site, p_global, p_zones, p_fam, inheritance):
+    """(N, F, C) lh per component as update_component_likelihoods (model.py:224-247): the one-hot
+    gathers of p_global / p_zones / p_families (0 for a site outside every zone / family), every
+    component 1 at NA cells."""
     N, F = obs.shape
     na = obs < 0
     x = np.where(na, 0, obs).astype(np.intp)
@@ -26,18 +26,33 @@ def source_posterior(obs, fam_of_site, zone_of_site, w, p_global, p_zones, p_fam
     if iz.any():
         lz[iz] = p_zones[zone_of_site[iz].astype(np.intp)[:, None], fi[iz], x[iz]]
     comps.append(lz)
-    has = [np.ones(N, bool), iz]
     if inheritance:
         lf = np.zeros((N, F))
         ifm = fam_of_site != NONE
         if ifm.any():
             lf[ifm] = p_fam[fam_of_site[ifm].astype(np.intp)[:, None], fi[ifm], x[ifm]]
         comps.append(lf)
-        has.append(ifm)
     lh = np.ascontiguousarray(np.array(comps).transpose((1, 2, 0)))
     lh[na] = 1.0
+    return lh
+
+
+def normalized_weights(fam_of_site, zone_of_site, w, inheritance):
+    """(N, F, C) update_weights -> normalize_weights (model.py:251-294, 436-452): w * has / sum."""
+    N = zone_of_site.shape[0]
+    has = [np.ones(N, bool), zone_of_site != NONE]
+    if inheritance:
+        has.append(fam_of_site != NONE)
     wps = w[None, :, :] * np.stack(has, axis=1)[:, None, :]
-    wn = wps / wps.sum(axis=2, keepdims=True)
+    return wps / wps.sum(axis=2, keepdims=True)
+
+
+def source_posterior(obs, fam_of_site, zone_of_site, w, p_global, p_zones, p_fam, inheritance):
+    """(N, F, C) normalize(lh * weights) for one chain in packed form (obs int8 [N][F], -1 = NA):
+    lh per component as update_component_likelihoods (model.py:224-247; NA -> 1, a site outside
+    every zone / family -> 0), weights as update_weights -> normalize_weights (:284-292, 436-452)."""
+    lh = component_likelihoods(obs, fam_of_site, zone_of_site, p_global, p_zones, p_fam, inheritance)
+    wn = normalized_weights(fam_of_site, zone_of_site, w, inheritance)
     p = lh * wn
     return p / np.sum(p, axis=-1, keepdims=True)
 

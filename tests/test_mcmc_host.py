@@ -122,3 +122,37 @@ def test_unsupported_options_raise():
     kw2 = dict(kw, operators={"grow_zone": 1.0, "gibbs_sample_sources": 0.5})
     with pytest.raises(ValueError):
         BatchedZoneMCMC(**kw2)
+
+
+@pytest.mark.parametrize("case", ["lik_cfg3_balkan", "lik_cfg4_sa_z6", "lik_cfg2", "lik_edge_na"])
+def test_gpu_likelihood_host_component_arrays(case):
+    """GpuLikelihood's update_component_likelihoods / update_weights (the arrays the reference's
+    own CPU operators read, model.py:230-294) reproduce the reference's likelihood:
+    sum log sum_c lh * w equals the captured Likelihood(..., caching=False) value, and the source
+    branch with the captured sources too (host only, no GPU)."""
+    from contact_zones_amd.likelihood import GpuLikelihood
+    fx = load_golden(case)
+    inh = bool(fx["inheritance"])
+    S = fx["p_global"].shape[-1]
+    obs, fam = fx["obs"], fx["fam_of_site"]
+    n_fam = fx["p_fam"].shape[1] if inh else 0
+    data = types.SimpleNamespace(features=packing.obs_to_features(obs, S),
+                                 families=packing.index_to_groups(fam, n_fam) if inh else np.zeros((0, obs.shape[0]), bool))
+    lik = GpuLikelihood(data, inh)
+    for b in range(fx["w"].shape[0]):
+        Z = fx["p_zones"].shape[1]
+        zones = packing.index_to_groups(fx["zone_of_site"][b], Z)
+        sample = types.SimpleNamespace(
+            zones=zones, weights=fx["w"][b], p_global=fx["p_global"][b][None], p_zones=fx["p_zones"][b],
+            p_families=fx["p_fam"][b] if inh else None, source=None)
+        lh = lik.update_component_likelihoods(sample, caching=False)
+        w = lik.update_weights(sample)
+        ll = np.sum(np.log(np.sum(lh * w, axis=-1)))
+        assert ll == pytest.approx(float(fx["ll_mixture"][b]), rel=1e-12)
+        src = fx["source"][b]
+        sel = np.take_along_axis(lh * w, src[..., None].astype(np.intp), axis=-1)[..., 0]
+        with np.errstate(divide="ignore"):
+            lls = np.sum(np.log(sel))
+        ref = float(fx["ll_source"][b])
+        assert (lls == ref) if np.isinf(ref) else lls == pytest.approx(ref, rel=1e-12)
+        np.testing.assert_array_equal(lik.get_zone_assignment(sample), fx["zone_of_site"][b] != 255)
