@@ -36,6 +36,9 @@ struct LikArgs {
     const int *cnt;         // [F][128]   sites per (family class, x): fc * (S+1) + x (zone-sparse)
     const uint32_t *zl;     // [B][N]     zoned sites: site | class << 24, first nzs[b] valid
     const int *nzs;         // [B]        zoned sites per chain
+    const uint8_t *obs8;    // [N + 1][F4] x*8 by site (NA: S*8; row N all NA), rows padded to F4
+    const double *ones;     // [F*S + 8]  1.0: constant entries of the zone-sparse direct kernel
+    int F4;
     double *partial;        // [B][W]     task partial sums
     unsigned *ticket;       // [B]        finished tasks per chain (0 between launches)
     double *out;            // [B]        log-likelihood per chain
@@ -57,6 +60,10 @@ struct sbz_ctx {
     // sampler data (sbz_open / sbz_set_network)
     uint8_t *d_obs_sm = nullptr;    // [N][F] x by site (S = NA)
     uint8_t *d_fam_site = nullptr;  // [N] family class by site
+    uint8_t *d_obs8 = nullptr;      // [N + 1][F4] x*8 by site, zone-sparse direct kernel (xs8 only)
+    double *d_ones = nullptr;       // [F*S + 8] ones, same kernel
+    int F4 = 0;
+    int hfm = 0;  // family presence over the sites: 0 none (or C = 2), 1 every site, 2 mixed
     int *d_adj_ptr = nullptr, *d_adj_idx = nullptr;  // CSR network
     int adj_nnz = 0;
     int *d_app_list = nullptr, *d_app_cnt = nullptr; // [F][S] applicable states, [F] counts
@@ -70,7 +77,8 @@ struct sbz_ctx {
     int zspl = 8;          // zoned sites per lane and chunk of the zone-sparse kernel
     int lik_kernel = 1;    // SBZ_LIK_KERNEL: 1 dense (default), 2 zone-sparse ("zoned"),
                            // 3 dense double-buffered ("db", where the table fits 4 KiB),
-                           // 4 wave-specialised builder + gatherers ("ws", same condition)
+                           // 4 wave-specialised builder + gatherers ("ws", same condition),
+                           // 5 zone-sparse direct ("zd")
     int ws_ng = 2;         // SBZ_WS_NG: gatherer waves of the wave-specialised kernel (1 or 2)
     int ws_nb = 2;         // SBZ_WS_NB: its builder waves (1 or 2; 2 split the zone-class slots)
     const void *mix_occ_fn = nullptr;  // the kernel mix_occ was queried for

@@ -1004,6 +1004,326 @@ __global__ __launch_bounds__(WAVE, SBZ_ZS_WAVES) void lik_zoned_kernel(LikArgs a
     finish_chain(a, b, tot);
 }
 
+// ---------------------------------------------------------------------------------------
+// Zone-sparse mixture kernel, direct (SBZ_LIK_KERNEL=zd).  Same decomposition as
+// lik_zoned_kernel,
+//   ll_f = sum_{fc,x} n_all[f][fc][x] log T0[fc][x] + log prod_zoned T - log prod_zoned T0,
+// but without a class table: the feature's parameter column (p_global, p_zones, a row of
+// ones for "no family", p_fam; the NA column is 1.0) is staged in ~1 KB of LDS and a zoned
+// cell gathers its three l_c and forms T = (n0 l0 + n1 l1) + n2 l2 and T0 = n0' l0 + n2' l2 in
+// registers (reference operation order; a +0 term of a tame input is left out, x + 0 == x).
+// One lane per (fc, x) count entry takes the log of T0.  Zoned observations come as one dword
+// (4 features) per site from the site-major obs8 rows.  The no-zone sites, 80 % at the bench's
+// cfg5, cost no gathers at all.
+// Features whose inputs are not all tame, or with a zero / non-finite T0 entry that has a
+// non-zero count, take the exact slow path (every site of the feature, one log per cell).
+// Requires: xs8, 2 (Z + 2 + Fam)(S + 1) <= 320, FamC * (S + 1) <= 64 (host check at launch).
+// HFM: 0 no zoned site has a family (C == 2 or no families), 1 all sites have one, 2 mixed.
+// ---------------------------------------------------------------------------------------
+#ifndef SBZ_ZD_WAVES
+#define SBZ_ZD_WAVES 2
+#endif
+constexpr int ZD_NT = 5;  // LDS-DMA dword loads per column image: 2 (Z + 2 + Fam)(S + 1) <= 320
+constexpr int ZD_FB = 4;  // features per batch (one observation dword)
+
+__device__ __forceinline__ double uniform_f64(double v) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
+template <int C, int ZSPL, int HFM>
+__global__ __launch_bounds__(WAVE, SBZ_ZD_WAVES) void lik_zdirect_kernel(LikArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int lane = threadIdx.x;
+    const int b = blockIdx.y;
+    const int fa = blockIdx.x * a.fpw;  // fpw % 4 == 0
+    const int fb = min(a.F, fa + a.fpw);
+    const int S = a.S, S1 = S + 1, Z = a.Z, Fam = C == 3 ? a.Fam : 0, FamC = a.FamC;
+    const int RL = Z + 2 + Fam;                      // rows: pg, pz[0..Z), ones, pf[0..Fam)
+    const int NT = (2 * RL * S1 + WAVE - 1) / WAVE;  // LDS-DMA dword loads per column (<= ZD_NT)
+    const int RLS = NT * (WAVE / 2);                 // one column image, doubles
+    double *stg = reinterpret_cast<double *>(lds);   // [2][ZD_FB][RLS] column images
+    double *nwt = stg + 2 * ZD_FB * RLS;
+    const int NC = FamC * S1;
+    const int nz = a.nzs[b];
+    const uint32_t zfs = (uint32_t)(a.F * S);
+
+    // weights: NWC features at a time, layout as MixTable::prep
+    int nwf0 = -(1 << 30);
+    uint64_t nwbad = 0;
+    const double *wb = a.w + (size_t)b * a.F * C;
+    auto prep = [&](int f0) {
+        const int k = lane >> 1, hp = lane & 1;
+        const uint32_t f = (uint32_t)min(f0 + k, fb - 1);
+        const double w0r = wb[f * C], w1r = wb[f * C + 1], w2r = C == 3 ? wb[f * C + 2] : 0.0;
+        int ok = 1;
+        double n[2][3];
+#pragma unroll
+        for (int hz = 0; hz < 2; hz++) {
+            const double hzf = hz ? 1.0 : 0.0, hff = hp ? 1.0 : 0.0;
+            const double w0 = w0r * 1.0, w1 = w1r * hzf;
+            double sum = w0 + w1, w2 = 0.0;
+            if (C == 3) {
+                w2 = w2r * hff;
+                sum = sum + w2;
+            }
+            n[hz][0] = w0 / sum;
+            n[hz][1] = w1 / sum;
+            n[hz][2] = C == 3 ? w2 / sum : 0.0;
+            ok &= (int)tame(n[hz][0]) & (int)tame(n[hz][1]) & (int)tame(n[hz][2]);
+        }
+        wave_lds_sync();
+        double *o = nwt + k * NW_PER_F;
+#pragma unroll
+        for (int hz = 0; hz < 2; hz++) {
+            o[2 * (2 * hp + hz)] = n[hz][0];
+            o[2 * (2 * hp + hz) + 1] = n[hz][1];
+            o[8 + 2 * hz + hp] = n[hz][2];
+        }
+        nwbad = __ballot(!ok);
+        nwf0 = f0;
+        wave_lds_sync();
+    };
+
+    // LDS-DMA sources: dword t*64 + lane of a column image is double (r, x) = ((t*64 + lane) / 2
+    // as r * S1 + x), half (lane & 1).  NA column, "no family" row and padding read a.ones,
+    // which advances with the feature like a parameter row (F * S + 8 ones).
+    const char *dsrc[ZD_NT];
+#pragma unroll
+    for (int t = 0; t < ZD_NT; t++) {
+        const int i = t * WAVE + lane, dr = i >> 1, r = dr / S1, x = dr - r * S1;
+        const double *p;
+        if (r >= RL || x == S || r == Z + 1) p = a.ones;
+        else if (r == 0) p = a.pg + (size_t)b * zfs + x;
+        else if (r <= Z) p = a.pz + ((size_t)b * Z + (r - 1)) * zfs + x;
+        else p = a.pf + ((size_t)b * Fam + (r - Z - 2)) * zfs + x;
+        dsrc[t] = reinterpret_cast<const char *>(p) + 4 * (i & 1);
+    }
+    auto dma_column = [&](int f, double *img) {
+        const size_t fo = (size_t)f * S * 8;
+#pragma unroll
+        for (int t = 0; t < ZD_NT; t++)
+            if (t < NT)  // uniform
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void *)(dsrc[t] + fo),
+                    (__attribute__((address_space(3))) void *)(img + t * (WAVE / 2)), 4, 0, 0);
+    };
+    auto dma = [&](int fg, int buf) {
+#pragma unroll
+        for (int j = 0; j < ZD_FB; j++) dma_column(min(fg + j, fb - 1), stg + (buf * ZD_FB + j) * RLS);
+    };
+    // count lane: entry (fc, x) = (lane / S1, lane % S1)
+    const int cfc = min(lane, NC - 1) / S1, cx = min(lane, NC - 1) - cfc * S1;
+    const uint32_t c_l2 = (uint32_t)((Z + 1 + cfc) * S1 + cx);
+    const bool c_hf = C == 3 && cfc > 0;
+
+    double m1[2] = {1.0, 1.0}, m0[2] = {1.0, 1.0};
+    int e = 0;
+    double acc = 0.0;
+    uint64_t slowm = 0;  // features [fa, fb) for the exact slow path (fpw <= 64)
+    uint32_t desc[ZSPL], obase[ZSPL];
+    uint32_t hfm = 0;  // HFM == 2: bit q = the lane's slot-q site has a family
+
+    auto load_c = [&](int fg, int (&c)[ZD_FB]) {
+#pragma unroll
+        for (int j = 0; j < ZD_FB; j++) c[j] = a.cnt[(size_t)min(fg + j, fb - 1) * CP + min(lane, NC - 1)];
+    };
+    auto load_o = [&](int fg, uint32_t (&o)[ZSPL]) {
+#pragma unroll
+        for (int k = 0; k < ZSPL; k++)
+            o[k] = *reinterpret_cast<const uint32_t *>(a.obs8 + obase[k] + (uint32_t)fg);
+    };
+    auto at = [&](uint32_t byte) { return *reinterpret_cast<const double *>(lds + byte); };
+    // cc[j] with a loop-variable j, without a dynamically indexed register array
+    auto ccj = [](const int (&c)[ZD_FB], int j) { return j == 0 ? c[0] : j == 1 ? c[1] : j == 2 ? c[2] : c[3]; };
+
+    // One batch of ZD_FB = 4 features (one observation dword per zoned site): the batch's four
+    // column images landed in buffer buf during the previous batch; issue the next batch's DMA
+    // into the other buffer, then count terms and zoned cells.
+    auto batch = [&](int fg, int buf, bool first, int zb0, const int (&cc)[ZD_FB], const uint32_t (&ob)[ZSPL],
+                     int (&cfill)[ZD_FB], uint32_t (&ofill)[ZSPL]) {
+        if (fg + ZD_FB - 1 >= nwf0 + NWC) prep(fg);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this batch's images have landed
+        wave_lds_sync();  // and the previous batch's reads of the other buffer are done
+        dma(fg + ZD_FB, buf ^ 1);
+        load_c(fg + ZD_FB, cfill);
+        load_o(min(fg + ZD_FB, fb - 1) & ~3, ofill);
+        const double *sbuf = stg + buf * ZD_FB * RLS;
+        uint32_t slowb = 0;  // bit j: feature fg + j takes the slow path (or is padding)
+        double cl = 0.0;
+#pragma unroll 1
+        for (int j = 0; j < ZD_FB; j++) {
+            const double *sj = sbuf + j * RLS;
+            int ok = 1;
+#pragma unroll
+            for (int k = 0; k < (ZD_NT + 1) / 2; k++) ok &= (int)tame(sj[min(lane + WAVE * k, RLS - 1)]);
+            const bool wide = ((nwbad >> (2 * (fg + j - nwf0))) & 3ull) != 0 || __ballot(!ok) != 0;
+            const double *nk = static_cast<const double *>(
+                __builtin_assume_aligned(nwt + (fg + j - nwf0) * NW_PER_F, 16));
+            const double2 n0p = *reinterpret_cast<const double2 *>(nk + 0);
+            const double2 n2p = *reinterpret_cast<const double2 *>(nk + 4);
+            const double2 c2p = *reinterpret_cast<const double2 *>(nk + 8);
+            double t0 = (c_hf ? n2p.x : n0p.x) * sj[cx];
+            if (C == 3) t0 = t0 + (c_hf ? c2p.y * sj[c_l2] : 0.0);
+            const bool use = lane < NC && ccj(cc, j) > 0;
+            const bool bad = use && !(t0 > 0.0 && t0 < __builtin_huge_val());
+            const bool sl = fg + j >= fb || wide || __ballot(bad) != 0;
+            slowb |= sl ? 1u << j : 0u;
+            if (first && use && !sl) cl += (double)ccj(cc, j) * log(t0);
+            __builtin_amdgcn_sched_barrier(0);  // one log's temporaries at a time
+        }
+        acc += cl;
+#pragma unroll 1
+        for (int j = 0; j < ZD_FB; j++) {
+            if ((slowb >> j) & 1u) {
+                if (first && fg + j < fb) slowm |= 1ull << (fg + j - fa);  // after the main loop
+                continue;
+            }
+            const double *nk = static_cast<const double *>(
+                __builtin_assume_aligned(nwt + (fg + j - nwf0) * NW_PER_F, 16));
+            // the weights are wave-uniform: into SGPRs
+            auto pair = [&](int i) {
+                const double2 v = *reinterpret_cast<const double2 *>(nk + i);
+                return make_double2(uniform_f64(v.x), uniform_f64(v.y));
+            };
+            const double2 n0p = pair(0), n2p = pair(4), c2p = pair(8);  // h = 0, 2; c2 of (0, 2)
+            const double2 z1 = pair(2), z3 = pair(6), c2z = pair(10);   // h = 1, 3; c2 of (1, 3)
+            const uint32_t sb = (uint32_t)((buf * ZD_FB + j) * RLS * 8);
+            const int sh = 8 * j;
+            // groups of 4 slots: every gather of the group is issued before the arithmetic
+#pragma unroll
+            for (int g = 0; g < ZSPL; g += 4) {
+                if (zb0 + WAVE * g >= nz) break;  // uniform
+                double L0[4], L1[4], L2[4];
+#pragma unroll
+                for (int q = g; q < g + 4; q++) {
+                    if (zb0 + WAVE * q >= nz) break;  // uniform
+                    const uint32_t x8 = sb + ((ob[q] >> sh) & 0xffu);
+                    const uint32_t d = desc[q];
+                    L0[q - g] = at(x8);
+                    L1[q - g] = at((d & 0xffffu) + x8);
+                    if (HFM != 0) L2[q - g] = at((d >> 16) + x8);
+                }
+#pragma unroll
+                for (int q = g; q < g + 4; q++) {
+                    if (zb0 + WAVE * q >= nz) break;  // uniform
+                    const double l0 = L0[q - g], l1 = L1[q - g];
+                    double T, T0;
+                    if (HFM == 0) {
+                        T = z1.x * l0 + z1.y * l1;
+                        T0 = n0p.x * l0;
+                    } else if (HFM == 1) {
+                        const double l2 = L2[q - g];
+                        T = (z3.x * l0 + z3.y * l1) + c2z.y * l2;
+                        T0 = n2p.x * l0 + c2p.y * l2;
+                    } else {
+                        const double l2 = L2[q - g];
+                        const bool h = (hfm >> q) & 1u;
+                        T = (h ? z3.x : z1.x) * l0 + (h ? z3.y : z1.y) * l1;
+                        T0 = (h ? n2p.x : n0p.x) * l0;
+                        if (h) {
+                            T = T + c2z.y * l2;
+                            T0 = T0 + c2p.y * l2;
+                        }
+                    }
+                    m1[q & 1] *= T;
+                    m0[q & 1] *= T0;
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            int e1a, e1b, e0a, e0b;
+            e1a = __builtin_amdgcn_frexp_exp(m1[0]);
+            m1[0] = __builtin_amdgcn_frexp_mant(m1[0]);
+            e1b = __builtin_amdgcn_frexp_exp(m1[1]);
+            m1[1] = __builtin_amdgcn_frexp_mant(m1[1]);
+            e0a = __builtin_amdgcn_frexp_exp(m0[0]);
+            m0[0] = __builtin_amdgcn_frexp_mant(m0[0]);
+            e0b = __builtin_amdgcn_frexp_exp(m0[1]);
+            m0[1] = __builtin_amdgcn_frexp_mant(m0[1]);
+            e += (e1a + e1b) - (e0a + e0b);
+        }
+    };
+
+    const int nchunk = max(1, (nz + WAVE * ZSPL - 1) / (WAVE * ZSPL));
+    const uint32_t *zlb = a.zl + (size_t)b * a.N;
+    for (int ch = 0; ch < nchunk; ch++) {
+        const int zb0 = ch * WAVE * ZSPL;
+        hfm = 0;
+#pragma unroll
+        for (int q = 0; q < ZSPL; q++) {
+            const int jj = zb0 + lane + WAVE * q;
+            const uint32_t ent = jj < nz ? zlb[min(jj, a.N - 1)] : 0u;  // beyond nz: stale
+            const uint32_t cls = ent >> 24;
+            const uint32_t zc = cls / (uint32_t)FamC;
+            const uint32_t fc = cls - zc * (uint32_t)FamC;
+            if (HFM == 2) hfm = fc > 0 ? (hfm | (1u << q)) : hfm;
+            // a slot beyond nz reads the all-NA row N of obs8: l0 = l1 = l2 = 1, so its factor
+            // T / T0 is (sum of normalised weights) / (sum of normalised weights) = 1 +- 1 ulp
+            const int site = jj < nz ? a.perm[ent & 0xffffffu] : a.N;
+            obase[q] = (uint32_t)site * (uint32_t)a.F4;
+            desc[q] = (uint32_t)(zc * S1 * 8) | ((uint32_t)((Z + 1 + fc) * S1 * 8) << 16);
+        }
+        if (fa < nwf0 || fa + ZD_FB - 1 >= nwf0 + NWC) prep(fa);
+        int Cc[ZD_FB], Cn[ZD_FB];
+        uint32_t Oc[ZSPL], On[ZSPL];
+        wave_lds_sync();
+        dma(fa, 0);
+        load_c(fa, Cc);
+        load_o(fa, Oc);
+        int buf = 0;
+#pragma unroll 1
+        for (int fg = fa; fg < fb; fg += ZD_FB) {
+            batch(fg, buf, ch == 0, zb0, Cc, Oc, Cn, On);
+#pragma unroll
+            for (int j = 0; j < ZD_FB; j++) Cc[j] = Cn[j];
+#pragma unroll
+            for (int q = 0; q < ZSPL; q++) Oc[q] = On[q];
+            buf ^= 1;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last (unused) prefetch
+    }
+    // exact slow path (rare: untamed inputs, or a zero T0 entry with a non-zero count): every
+    // site of the feature, the reference cell, one log each
+    while (slowm) {
+        const int f = fa + __builtin_ctzll(slowm);
+        slowm &= slowm - 1;
+        if (f < nwf0 || f >= nwf0 + NWC) prep(f);
+        wave_lds_sync();
+        dma_column(f, stg);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        wave_lds_sync();
+        const double *nk = nwt + (f - nwf0) * NW_PER_F;
+        const uint8_t *zb = a.zone + (size_t)b * a.N;
+        const uint8_t *op = a.obs_fm + (size_t)f * a.Np;
+        double sacc = 0.0;
+        for (int p = lane; p < a.N; p += WAVE) {
+            const int z = zb[a.perm[p]];
+            const int fc = C == 3 ? a.famc[p] : 0;
+            const uint32_t x8 = op[p];  // xs8
+            const bool na = x8 == (uint32_t)(S * 8);
+            const int hz = z < Z ? 1 : 0, hf = fc > 0 ? 1 : 0;
+            const int h = hz | (hf << 1);
+            const double n0 = nk[2 * h], n1 = nk[2 * h + 1];
+            const double l0 = at(x8);
+            const double l1 = hz ? at((uint32_t)((1 + z) * S1 * 8) + x8) : (na ? 1.0 : 0.0);
+            double v = n0 * l0 + n1 * l1;
+            if (C == 3) {
+                const double l2 = hf ? at((uint32_t)((Z + 1 + fc) * S1 * 8) + x8) : (na ? 1.0 : 0.0);
+                v = v + nk[8 + 2 * hz + hf] * l2;
+            }
+            sacc += log(v);
+        }
+        acc += sacc;
+    }
+    double v = (log(m1[0]) + log(m1[1])) - (log(m0[0]) + log(m0[1]));
+    v = v + (double)e * LN2;
+    v = v + acc;
+    const double tot = wave_sum(v);
+    finish_chain(a, b, tot);
+}
+
 // Per-chain ordered list of zoned sites for lik_zoned_kernel: zl[b][j] = position | cls << 24
 // (position in the family-sorted site order, cls = (z+1)*FamC + fc), j < nzs[b].  One wave per
 // chain.
@@ -1330,6 +1650,28 @@ const void *mix_kernel(int C, int fr, bool xs8, bool zoned, int spl, int zspl) {
     return xs8 ? mix_kernel_x<2, 4, true>(zoned, spl, zspl) : mix_kernel_x<2, 4, false>(zoned, spl, zspl);
 }
 
+const void *zd_kernel(int C, int zspl, int hfm) {
+    if (C == 3) {
+        if (zspl == 4)
+            return hfm == 0 ? reinterpret_cast<const void *>(&lik_zdirect_kernel<3, 4, 0>)
+                 : hfm == 1 ? reinterpret_cast<const void *>(&lik_zdirect_kernel<3, 4, 1>)
+                            : reinterpret_cast<const void *>(&lik_zdirect_kernel<3, 4, 2>);
+        return hfm == 0 ? reinterpret_cast<const void *>(&lik_zdirect_kernel<3, 8, 0>)
+             : hfm == 1 ? reinterpret_cast<const void *>(&lik_zdirect_kernel<3, 8, 1>)
+                        : reinterpret_cast<const void *>(&lik_zdirect_kernel<3, 8, 2>);
+    }
+    return zspl == 4 ? reinterpret_cast<const void *>(&lik_zdirect_kernel<2, 4, 0>)
+                     : reinterpret_cast<const void *>(&lik_zdirect_kernel<2, 8, 0>);
+}
+
+// LDS of lik_zdirect_kernel: staged rows, 16-B pad, normalised weights
+size_t zd_lds_bytes(const sbz_dims &d, int C) {
+    const size_t S1 = (size_t)d.n_states + 1;
+    const size_t Fam = C == 3 ? (size_t)d.n_families : 0;
+    const size_t nt = (2 * ((size_t)d.n_zones + 2 + Fam) * S1 + WAVE - 1) / WAVE;
+    return (2 * (size_t)ZD_FB * nt * (WAVE / 2) + (size_t)NWC * NW_PER_F) * 8;
+}
+
 template <int C>
 void launch_source(int spl, dim3 grid, size_t lds, hipStream_t st, const LikArgs &a) {
     switch (spl) {
@@ -1367,6 +1709,13 @@ void configure_mix(std::vector<const void *> &v) {
     if (C == 3) {
         configure_mix_x<C, 8, true>(v);
         configure_mix_x<C, 8, false>(v);
+    }
+}
+
+void configure_zd(std::vector<const void *> &v) {
+    for (int zspl = 4; zspl <= 8; zspl *= 2) {
+        v.push_back(zd_kernel(2, zspl, 0));
+        for (int hfm = 0; hfm < 3; hfm++) v.push_back(zd_kernel(3, zspl, hfm));
     }
 }
 
@@ -1447,6 +1796,7 @@ int lik_configure(sbz_ctx *ctx) {
     configure_mix<3>(fns);
     configure_source<2>(fns);
     configure_source<3>(fns);
+    configure_zd(fns);
     for (const void *fn : fns) {
         hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
         if (e != hipSuccess) return hip_fail(ctx, e, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
@@ -1484,7 +1834,7 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
     a.pf = pf;
 
     MixPlan plan;
-    bool zoned = false, ws = false;
+    bool zoned = false, ws = false, zd = false;
     int block = WAVE;
     const void *mix_fn = nullptr;
     size_t lds = 0;
@@ -1493,6 +1843,12 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
         plan = plan_mixture(d, ctx->C, ctx->xs8 != 0);
         if (plan.fr) {
             zoned = ctx->d_cnt != nullptr && ctx->lik_kernel == 2;
+            {
+                const int Fam = ctx->C == 3 ? d.n_families : 0;
+                zd = ctx->d_cnt != nullptr && ctx->d_obs8 != nullptr && ctx->lik_kernel == 5 &&
+                     2 * (d.n_zones + 2 + Fam) * (d.n_states + 1) <= WAVE * ZD_NT &&
+                     ctx->FamC * (d.n_states + 1) <= WAVE;
+            }
             // (the <C=3, SPL=32, FR=8> instantiation of the double-buffered kernel spills)
             const bool db = plan.db && !zoned && ctx->lik_kernel == 3 &&
                             !(ctx->C == 3 && plan.fr == 8 && ctx->spl == 32);
@@ -1500,7 +1856,7 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
             int ng = ctx->ws_ng;
             while (ng > 1 && ctx->spl / ng < 4) ng--;
             ws = plan.db && !zoned && ctx->lik_kernel == 4;
-            if (zoned) {
+            if (zoned || zd) {
                 rc = ensure(ctx, ctx->zl, (size_t)B * d.n_sites * sizeof(uint32_t));
                 if (rc) return rc;
                 rc = ensure(ctx, ctx->nzs, (size_t)B * sizeof(int));
@@ -1512,8 +1868,14 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
                 a.nzs = static_cast<const int *>(ctx->nzs.ptr);
                 a.cnt = ctx->d_cnt;
             }
-            lds = ws ? mix_ws_lds_bytes() : db ? mix_db_lds_bytes() : mix_lds_bytes(d, ctx->C);
-            if (ws) {
+            lds = zd ? zd_lds_bytes(d, ctx->C) : ws ? mix_ws_lds_bytes() : db ? mix_db_lds_bytes()
+                                                                             : mix_lds_bytes(d, ctx->C);
+            if (zd) {
+                a.obs8 = ctx->d_obs8;
+                a.F4 = ctx->F4;
+                a.ones = ctx->d_ones;
+                mix_fn = zd_kernel(ctx->C, ctx->zspl, ctx->C == 3 ? ctx->hfm : 0);
+            } else if (ws) {
                 block = WAVE * (ctx->ws_nb + ng);
                 mix_fn = mix_ws_kernel(ctx->C, plan.fr, ctx->spl / ng, ng, ctx->ws_nb);
             } else {
@@ -1531,6 +1893,10 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
             const int per_cu = ctx->tasks_per_cu > 0 ? ctx->tasks_per_cu : ctx->mix_occ;
             const int W = std::max(1, std::min((F + 1) / 2, (ctx->n_cu * per_cu + B - 1) / B));
             a.fpw = (F + W - 1) / W;
+            if (zd) {
+                // dword observation groups; <= 64 features per task (the slow-path feature mask)
+                a.fpw = std::min(64, (a.fpw + 3) / 4 * 4);
+            }
         }
     } else {
         lds = lik_lds_bytes(d, true);

@@ -37,9 +37,10 @@ def _assert_close(got, ref, tol=REL_TOL):
 # Mixture-mode kernels: "dense" = every site gathered from the table (default), "db" = the
 # double-buffered dense kernel (where the table fits 4 KiB), "ws" / "ws1" = the wave-specialised
 # kernel (a builder wave + 2 / 1 gatherer waves, same condition), "zoned" = zone-sparse counts
-# kernel (SBZ_LIK_KERNEL and SBZ_WS_NG are read when a context opens).
+# kernel, "zd" = zone-sparse direct kernel (no class table) (SBZ_LIK_KERNEL and SBZ_WS_NG are
+# read when a context opens).
 MODES = [("mixture", "dense"), ("mixture", "db"), ("mixture", "ws"), ("mixture", "ws1"),
-         ("mixture", "zoned"), ("source", "dense")]
+         ("mixture", "zoned"), ("mixture", "zd"), ("source", "dense")]
 
 
 @pytest.fixture
@@ -75,11 +76,11 @@ def test_known_answer(gpu_available):
     assert lf == pytest.approx(float(d["lh_direct"]), rel=1e-12)
 
 
-def _random_batch(rng, N, F, S, Z, Fam, B, inheritance, zone_size, na=0.02):
+def _random_batch(rng, N, F, S, Z, Fam, B, inheritance, zone_size, na=0.02, nofam=0.2):
     obs = rng.integers(0, S, size=(N, F)).astype(np.int8)
     obs[rng.random((N, F)) < na] = -1
     fam = rng.integers(0, max(Fam, 1), size=N).astype(np.uint8)
-    fam[rng.random(N) < 0.2] = 255
+    fam[rng.random(N) < nofam] = 255
     if Fam == 0:
         fam[:] = 255
     zos = np.full((B, N), 255, np.uint8)
@@ -182,14 +183,15 @@ def test_drop_in_likelihood_interface(gpu_available):
         assert lik(Sample(b, True)) == pytest.approx(d["ll_source"][b], rel=1e-12)
 
 
-@pytest.mark.parametrize("zspl", ["4", "8", "16"])
-def test_zone_sparse_paths(gpu_available, monkeypatch, zspl):
-    """Zone-sparse kernel: several chunks of zoned sites, no zoned sites, all sites zoned,
+@pytest.mark.parametrize("kernel,zspl", [("zoned", "4"), ("zoned", "8"), ("zoned", "16"),
+                                         ("zd", "4"), ("zd", "8")])
+def test_zone_sparse_paths(gpu_available, monkeypatch, kernel, zspl):
+    """Zone-sparse kernels: several chunks of zoned sites, no zoned sites, all sites zoned,
     zero no-zone table entries (exact slow path, finite and -inf) and untamed inputs."""
     from contact_zones_amd.likelihood import LikelihoodEngine
     from oracle import oracle_c
     monkeypatch.setenv("SBZ_LIK_ZSPL", zspl)
-    monkeypatch.setenv("SBZ_LIK_KERNEL", "zoned")
+    monkeypatch.setenv("SBZ_LIK_KERNEL", kernel)
     N, F, S, Z, Fam, B = 1500, 40, 6, 4, 3, 7
     rng = np.random.default_rng(11)
     obs, fam, zos, w, pg, pz, pf, _ = _random_batch(rng, N, F, S, Z, Fam, B, True, 100)
@@ -216,6 +218,27 @@ def test_zone_sparse_paths(gpu_available, monkeypatch, zspl):
     got = eng.loglik(zos, w, pg, pz, pf)
     ref = oracle_c.loglik_batch(obs, fam, zos, w, pg, pz, pf, inheritance=True)
     assert np.isfinite(ref[3]) and ref[4] == -np.inf
+    _assert_close(got, ref, tol=1e-12)
+
+
+@pytest.mark.parametrize("nofam,Fam,inh", [(0.0, 4, True), (1.0, 4, True), (0.3, 4, True),
+                                           (0.0, 0, False), (0.0, 0, True)])
+@pytest.mark.parametrize("zspl", ["4", "8"])
+def test_zd_family_layouts(gpu_available, monkeypatch, nofam, Fam, inh, zspl):
+    """Zone-sparse direct kernel, every family-presence instantiation (every site with a family,
+    none, mixed; no inheritance; inheritance without families), partial slots, ragged F."""
+    from contact_zones_amd.likelihood import LikelihoodEngine
+    from oracle import oracle_c
+    monkeypatch.setenv("SBZ_LIK_ZSPL", zspl)
+    monkeypatch.setenv("SBZ_LIK_KERNEL", "zd")
+    N, F, S, Z, B = 900, 61, 7, 5, 9
+    rng = np.random.default_rng(int(nofam * 10) + Fam + 100 * inh + int(zspl))
+    obs, fam, zos, w, pg, pz, pf, _ = _random_batch(rng, N, F, S, Z, Fam, B, inh, 37, nofam=nofam)
+    zos[1] = 255
+    zos[2, :300] = rng.integers(0, Z, size=300)
+    eng = LikelihoodEngine(obs, fam, S, Z, Fam, inh)
+    got = eng.loglik(zos, w, pg, pz, pf)
+    ref = oracle_c.loglik_batch(obs, fam, zos, w, pg, pz, pf, inheritance=inh)
     _assert_close(got, ref, tol=1e-12)
 
 
