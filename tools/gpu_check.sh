@@ -4,7 +4,7 @@
 set -u
 mkdir -p gpurun_out
 STEPS=${STEPS:-200}
-run() { echo "== $*"; "$@"; rc=$?; if [ $rc -ne 0 ]; then echo "FAILED rc=$rc: $*"; exit $rc; fi; }
+run() { echo "== $*" >&2; "$@"; rc=$?; if [ $rc -ne 0 ]; then echo "FAILED rc=$rc: $*"; exit $rc; fi; }
 run timeout -k 10 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
 tail -3 gpurun_out/pytest_gpu.log
 run timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()"
