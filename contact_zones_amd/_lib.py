@@ -67,6 +67,7 @@ SIGNATURES = {
     "sbz_synchronize": (_I, [_P]),
     "sbz_loglik_batch": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P]),
     "sbz_loglik_batch_device": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "sbz_check_indices_device": (_I, [_P, _I, _P, _P]),
     "sbz_device_alloc": (_I, [_P, ctypes.c_uint64, ctypes.POINTER(_P)]),
     "sbz_device_free": (_I, [_P, _P]),
     "sbz_memcpy_h2d": (_I, [_P, _P, _P, ctypes.c_uint64]),

@@ -265,6 +265,7 @@ void sbz_close(sbz_ctx *ctx) {
     free_buf(ctx->ticket);
     free_buf(ctx->stage);
     free_buf(ctx->out);
+    free_buf(ctx->flags);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;
 }
@@ -296,6 +297,53 @@ int sbz_loglik_batch_device(sbz_ctx *ctx, int B, const uint8_t *zone_of_site, co
         return fail(ctx, SBZ_EINVAL, "null argument or negative B");
     (void)hipSetDevice(ctx->device);
     return launch_loglik(ctx, B, zone_of_site, w, p_global, p_zones, p_fam, source, out_ll);
+}
+
+namespace {
+// bit 0: a zone byte >= n_zones (and != SBZ_NONE); bit 1: a source byte >= C
+__global__ void check_indices_kernel(size_t nz, const uint8_t *zone, int Z, size_t ns,
+                                     const uint8_t *src, int C, unsigned *flags) {
+    unsigned bad = 0;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nz; i += stride) {
+        const unsigned z = zone[i];
+        bad |= (z != SBZ_NONE && z >= (unsigned)Z) ? 1u : 0u;
+    }
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += stride)
+        bad |= src[i] >= (unsigned)C ? 2u : 0u;
+    if (__any(bad != 0)) {
+        const unsigned m = bad;
+        atomicOr(flags, m);
+    }
+}
+}  // namespace
+
+int sbz_check_indices_device(sbz_ctx *ctx, int B, const uint8_t *zone_of_site,
+                             const uint8_t *source) {
+    if (!ctx) return SBZ_EINVAL;
+    if (B < 0 || (B > 0 && !zone_of_site)) return fail(ctx, SBZ_EINVAL, "null argument or negative B");
+    if (B == 0) return SBZ_OK;
+    (void)hipSetDevice(ctx->device);
+    int rc = ensure(ctx, ctx->flags, sizeof(unsigned));
+    if (rc) return rc;
+    unsigned *flags = static_cast<unsigned *>(ctx->flags.ptr);
+    hipError_t e = hipMemsetAsync(flags, 0, sizeof(unsigned), ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipMemsetAsync(flags)");
+    const size_t nz = (size_t)B * ctx->d.n_sites;
+    const size_t ns = source ? nz * (size_t)ctx->d.n_features : 0;
+    const size_t work = std::max(nz, ns);
+    const int grid = (int)std::min<size_t>(2048, (work + 255) / 256);
+    check_indices_kernel<<<grid, 256, 0, ctx->stream>>>(nz, zone_of_site, ctx->d.n_zones, ns, source,
+                                                        ctx->C, flags);
+    e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(ctx, e, "check_indices_kernel launch");
+    unsigned h = 0;
+    e = hipMemcpyAsync(&h, flags, sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "check_indices (read flags)");
+    if (h & 1u) return fail(ctx, SBZ_EINVAL, "zone_of_site holds an index >= n_zones");
+    if (h & 2u) return fail(ctx, SBZ_EINVAL, "source holds a component index >= C");
+    return SBZ_OK;
 }
 
 int sbz_loglik_batch(sbz_ctx *ctx, int B, const uint8_t *zone_of_site, const double *w,

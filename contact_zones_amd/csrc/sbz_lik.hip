@@ -70,11 +70,21 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 // Store a task's partial sum; the chain's last task to finish adds the W partials in task order
 // (deterministic, independent of which task finishes last) into out[b] and re-arms the chain's
-// ticket for the next launch.  Hand-off without cache maintenance (MI355X_MICROARCH.md,
-// cross-workgroup hand-offs, first row): the partial is an sc1 store (relaxed agent-scope atomic
-// store), the storing lane waits vmcnt(0), then adds to the chain's ticket (agent atomic); the
-// lane whose add returned W-1 reads every partial with sc1 loads.  An agent-scope acq_rel fence
-// here would write back / invalidate caches once per task and cost ~2x the kernel.
+// ticket for the next launch.
+//
+// Memory ordering.  This is NOT the HIP/LLVM memory model's release/acquire pattern: it is the
+// hand-off MI355X_MICROARCH.md ("Hand-offs measured with sc1 loads in place of the acquire",
+// first row) lists as measured-valid on gfx950 / ROCm 7.2, and which that guide states is not an
+// architectural guarantee.  Every condition of that row holds here: (1) every load of the
+// handed-off bytes is a global sc1 load (relaxed agent-scope atomic load, L1 bypassed), (2) the
+// producer stores every byte sc1 (relaxed agent-scope atomic store, 8 B), (3) the storing lane
+// (the only lane that stores) runs s_waitcnt vmcnt(0) before its agent-scope atomic add to the
+// chain's one unsharded counter, (4) the consumer is the task whose add returned W-1, and it loads
+// only after that add has returned; buffers come from hipMalloc, one single-wave task per
+// workgroup.  The release/acquire form (a release on every ticket add, an acquire on the winner)
+// writes back the XCD's L2 once per task: ~1.7 us per fence, measured ~2x the kernel here.
+// tests/test_gpu_likelihood.py::test_partials_handoff_stress re-checks the hand-off under uneven
+// load across all XCDs; the host re-zeroes the tickets when a launch fails (launch_loglik).
 __device__ __forceinline__ void finish_chain(const LikArgs &a, int b, double tot,
                                              bool leader = threadIdx.x == 0) {
     if (!leader) return;
@@ -1935,6 +1945,12 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
 
     dim3 grid(a.W, B);
     hipStream_t st = ctx->stream;
+    // A launch that never ran leaves no ticket armed, but one that failed after some tasks
+    // finished would leave the chains' tickets non-zero and corrupt every later sum: re-zero them.
+    auto launch_failed = [&](hipError_t e, const char *what) {
+        (void)hipMemsetAsync(ctx->ticket.ptr, 0, ctx->ticket.bytes, st);
+        return hip_fail(ctx, e, what);
+    };
     if (src_mode) {
         if (ctx->C == 3) launch_source<3>(ctx->spl, grid, lds, st, a);
         else launch_source<2>(ctx->spl, grid, lds, st, a);
@@ -1944,10 +1960,10 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
     } else {
         void *args[] = {&a};
         hipError_t e = hipLaunchKernel(mix_fn, grid, dim3(block), args, lds, st);
-        if (e != hipSuccess) return hip_fail(ctx, e, "mixture kernel launch");
+        if (e != hipSuccess) return launch_failed(e, "mixture kernel launch");
     }
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return hip_fail(ctx, e, "likelihood launch");
+    if (e != hipSuccess) return launch_failed(e, "likelihood launch");
     return SBZ_OK;
 }
 

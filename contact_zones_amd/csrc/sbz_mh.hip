@@ -809,6 +809,9 @@ int launch_mh(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg, const 
     const sbz_dims &d = ctx->d;
     if (!ctx->d_adj_ptr) return fail(ctx, SBZ_ESTATE, "sbz_set_network must be called before sbz_mh_run_device");
     if (B <= 0 || n_steps <= 0) return SBZ_OK;
+    // Philox blocks carry the global chain id in one 32-bit word (LaneRng, sbz_mh_common.h)
+    if (chains->chain_id0 > 0xffffffffull - (uint64_t)B)
+        return fail(ctx, SBZ_EINVAL, "global chain ids must stay below 2^32");
     const bool src = cfg->sample_source != 0;
     MhArgs a{};
     a.N = d.n_sites;

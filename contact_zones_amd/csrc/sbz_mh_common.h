@@ -190,9 +190,11 @@ struct Rng {
     __device__ __forceinline__ void dirichlet2(double a0, double a1, double &x0, double &x1);
 };
 
-// Per-lane Philox stream: block (j, base, chain lo, chain hi ^ (lane + 1) << 24), key = seed.
-// `base` is the wave's counter when the phase started (the wave then advances it by one), j
-// counts the lane's draws in the phase.
+// Per-lane Philox stream: block (j, base lo, chain, base hi ^ (lane + 1) << 24), key = seed.
+// `base` is the wave's 64-bit counter when the phase started (the wave then advances it by one),
+// j counts the lane's draws in the phase.  The counter's high word goes into c3 (bits 0..19; a
+// counter stays far below 2^52), so a chain's lane streams never repeat when its counter passes
+// 2^32; the host keeps global chain ids below 2^32 (c2).
 struct LaneRng {
     uint32_t k0, k1, base, c2, c3, j;
     __device__ __forceinline__ void init(const Rng &r, int lane) {
@@ -200,7 +202,7 @@ struct LaneRng {
         k1 = r.key1;
         base = (uint32_t)r.ctr;
         c2 = (uint32_t)r.chain;
-        c3 = (uint32_t)(r.chain >> 32) ^ ((uint32_t)(lane + 1) << 24);
+        c3 = (uint32_t)(r.ctr >> 32) ^ ((uint32_t)(lane + 1) << 24);
         j = 0;
     }
     // as init, from the key / chain / counter values themselves
@@ -210,13 +212,13 @@ struct LaneRng {
         k1 = key1;
         base = (uint32_t)ctr;
         c2 = (uint32_t)chain;
-        c3 = (uint32_t)(chain >> 32) ^ ((uint32_t)(lane + 1) << 24);
+        c3 = (uint32_t)(ctr >> 32) ^ ((uint32_t)(lane + 1) << 24);
         j = 0;
     }
     // a stream per thread of a multi-wave workgroup (id < 2048)
     __device__ __forceinline__ void initw(const Rng &r, int id) {
         init(r, 0);
-        c3 = (uint32_t)(r.chain >> 32) ^ ((uint32_t)(id + 1) << 20);
+        c3 = (uint32_t)(r.ctr >> 32) ^ ((uint32_t)(id + 1) << 20);
     }
     __device__ __forceinline__ double u() {
         uint32_t c[4] = {j++, base, c2, c3};

@@ -260,10 +260,36 @@ def model_spec(config, n_zones):
                                  inheritance=bool(m["INHERITANCE"]), sample_source=bool(m["SAMPLE_SOURCE"]))
 
 
+def derive_seeds(seed, run, n_zones):
+    """Independent seeds for the phases of one (run, n_zones) job from the experiment seed.
+
+    The reference draws everything from the global `random` / `np.random` streams, so its warm-up,
+    main run and every N_RUNS / N_AREAS job consume different draws.  The GPU sampler keys its
+    Philox streams by (seed, global chain id) with the counter starting at 0 in every ChainState,
+    so reusing one seed would hand each main chain exactly the uniforms its warm-up chain used, and
+    make every replicate of N_RUNS bit-identical.  SeedSequence([seed, run, n_zones]).spawn(3)
+    gives the host draws (initial samples, initial sources), the warm-up Philox key and the
+    main-run Philox key, pairwise independent and reproducible from `seed`."""
+    ss = np.random.SeedSequence([int(seed) & (2**63 - 1), int(run), int(n_zones)])
+    host, warm, main = (int(c.generate_state(1, np.uint64)[0]) & (2**63 - 1) for c in ss.spawn(3))
+    return {"host": host, "warmup": warm, "sample": main}
+
+
+def agree_seed(seed=None):
+    """The experiment seed every rank uses: `seed` if given, else one drawn from OS entropy on
+    rank 0; broadcast from rank 0 when torch.distributed is initialised, so that all ranks build
+    the same initial samples (the chains are sharded, their initial states are not)."""
+    from .parallel import broadcast_seed
+    if seed is None:
+        seed = int(np.random.SeedSequence().entropy) & (2**63 - 1)
+    return broadcast_seed(int(seed))
+
+
 def run_experiment(config, data, n_zones, run=0, name="experiment", seed=None, device=None,
                    logger=None, warmup_chains=None):
     """One run for one number of zones (cli.py:13-27): warm-up, sampling, results files.
-    Returns (statistics, paths)."""
+    Returns (statistics, paths).  `seed` is the experiment seed (None: fresh entropy, agreed
+    across ranks); the phases draw from independent streams derived from (seed, run, n_zones)."""
     from . import io
     from .mcmc import BatchedZoneMCMC, BatchedZoneMCMCWarmup
     from .postprocessing import contribution_per_area, match_areas, rank_areas
@@ -274,21 +300,25 @@ def run_experiment(config, data, n_zones, run=0, name="experiment", seed=None, d
     priors, gibbs = build_priors(cfg, data)
     model = model_spec(cfg, n_zones)
     ops = operators(cfg)
-    rng = random.Random(seed)
-    if seed is not None:
-        np.random.seed(seed)
+    seeds = derive_seeds(agree_seed(seed), run, n_zones)
+    rng = random.Random(seeds["host"])
+    np.random.seed(seeds["host"] % 2**32)  # the initial sources' draws (np.random, as the reference)
     common = dict(model=model, data=data, operators=ops, var_proposal=mc["PROPOSAL_PRECISION"],
                   p_grow_connected=mc["P_GROW_CONNECTED"], initial_size=mc["M_INITIAL"],
-                  logger=logger, rng=rng, seed=seed, device=device, priors=priors,
+                  logger=logger, rng=rng, device=device, priors=priors,
                   gibbs_counts=gibbs if model.sample_source else None)
     t0 = time.time()
-    warm = BatchedZoneMCMCWarmup(n_chains=warmup_chains or mc["WARM_UP"]["N_WARM_UP_CHAINS"], **common)
+    warm = BatchedZoneMCMCWarmup(n_chains=warmup_chains or mc["WARM_UP"]["N_WARM_UP_CHAINS"],
+                                 seed=seeds["warmup"], **common)
     best = warm.generate_samples(n_steps=0, n_samples=0, warm_up=True,
                                  warm_up_steps=mc["WARM_UP"]["N_WARM_UP_STEPS"])
     logger.info("warm-up: %d chains x %d steps in %.2f s", warm.n_chains, mc["WARM_UP"]["N_WARM_UP_STEPS"],
                 time.time() - t0)
-    smp = BatchedZoneMCMC(n_chains=mc["N_CHAINS"], initial_sample=best, **common)
+    smp = BatchedZoneMCMC(n_chains=mc["N_CHAINS"], initial_sample=best, seed=seeds["sample"], **common)
     smp.generate_samples(mc["N_STEPS"], mc["N_SAMPLES"])
+    if getattr(smp, "rank", 0) != 0:
+        # chain_idx[0] (the logged chain) lives on rank 0: the other ranks have nothing to write
+        return smp.statistics, None
     contribution_per_area(smp)
     stats = rank_areas(match_areas(smp.statistics))
     fi = {"n": f"n{n_zones}", "i": f"i{int(cfg['model']['INHERITANCE'])}",
@@ -300,9 +330,7 @@ def run_experiment(config, data, n_zones, run=0, name="experiment", seed=None, d
     os.makedirs(pth, exist_ok=True)
     paths = {"parameters": os.path.join(pth, f"stats_{fi}_{run}.txt"),
              "areas": os.path.join(pth, f"areas_{fi}_{run}.txt")}
-    rank = getattr(smp, "rank", 0)
-    if rank == 0:
-        io.samples2file(stats, data, cfg, paths)
+    io.samples2file(stats, data, cfg, paths)
     logger.info("sampling: %d steps, acceptance %.3f, %.2f s; results in %s", mc["N_STEPS"],
                 stats["acceptance_ratio"], stats["sampling_time"], pth)
     return stats, paths
@@ -317,7 +345,8 @@ def main(argv=None):
     p.add_argument("--device", type=int, default=None)
     p.add_argument("--set", default=None, help="JSON object merged into the config (custom settings)")
     a = p.parse_args(argv)
-    logging.basicConfig(level=logging.INFO, format="%(message)s")
+    rank, device = init_distributed(a.device)
+    logging.basicConfig(level=logging.INFO if rank == 0 else logging.WARNING, format="%(message)s")
     logger = logging.getLogger("sbz")
     config, _ = load_config(a.config, json.loads(a.set) if a.set else None)
     name = a.name or time.strftime("%Y%m%d-%H%M%S")
@@ -329,8 +358,54 @@ def main(argv=None):
     if not all(isinstance(n, int) for n in sweep):
         raise ValueError(f"N_AREAS must be an integer or a list of integers, got {n_areas!r} "
                          "(set it with --set '{\"model\": {\"N_AREAS\": 3}}')")
-    for run in range(config["mcmc"]["N_RUNS"]):
-        for n in sweep:
-            run_experiment(config, data, int(n), run=run, name=name, seed=a.seed, device=a.device,
-                           logger=logger)
+    name = _broadcast_name(name)
+    seed = agree_seed(a.seed)
+    try:
+        for run in range(config["mcmc"]["N_RUNS"]):
+            for n in sweep:
+                run_experiment(config, data, int(n), run=run, name=name, seed=seed, device=device,
+                               logger=logger)
+    finally:
+        _finish_distributed()
     return 0
+
+
+def init_distributed(device=None):
+    """One process per GPU under torchrun (WORLD_SIZE > 1): bind this rank's GPU from LOCAL_RANK
+    and join the process group (nccl = RCCL over xGMI; gloo when no GPU is visible) before any GPU
+    call.  The batched samplers then shard the chains over the ranks.  Returns (rank, device)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world <= 1:
+        return 0, device
+    import torch
+    import torch.distributed as dist
+    gpu = torch.cuda.is_available()
+    # more ranks than GPUs (a rehearsal on a one-GPU box) share the GPUs round-robin; RCCL
+    # refuses two ranks on one device, so such a run sets SBZ_DIST_BACKEND=gloo
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count() if gpu else 1)
+    if device is None:
+        device = local
+    if not dist.is_initialized():
+        if gpu:
+            torch.cuda.set_device(device)
+        dist.init_process_group(os.environ.get("SBZ_DIST_BACKEND", "nccl" if gpu else "gloo"))
+    return dist.get_rank(), device
+
+
+def _broadcast_name(name):
+    """Rank 0's experiment name (the default is a timestamp, which ranks may disagree on)."""
+    from .parallel import _dist
+    d = _dist()
+    if d is None or d.get_world_size() == 1:
+        return name
+    box = [name]
+    d.broadcast_object_list(box, src=0)
+    return box[0]
+
+
+def _finish_distributed():
+    from .parallel import _dist
+    d = _dist()
+    if d is not None and int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        d.barrier()
+        d.destroy_process_group()

@@ -102,8 +102,21 @@ class LikelihoodEngine:
               self.ctx)
         return out
 
-    def loglik_device(self, B, zone_of_site, w, p_global, p_zones, p_fam, source, out_ll):
-        """Device-pointer variant (ints = device addresses, 0 for None); async on the stream."""
+    def check_indices_device(self, B, zone_of_site, source=0):
+        """Range-check device index arrays (zone bytes < n_zones or 255, source bytes < C);
+        raises SbzError (SBZ_EINVAL) otherwise.  Synchronises the engine's stream."""
+        v = ctypes.c_void_p
+        check(self._lib.sbz_check_indices_device(self.ctx, int(B), v(zone_of_site), v(source or 0)),
+              self.ctx)
+
+    def loglik_device(self, B, zone_of_site, w, p_global, p_zones, p_fam, source, out_ll,
+                      validate=True):
+        """Device-pointer variant (ints = device addresses, 0 for None); async on the stream.
+        The kernels trust the index bytes (include/sbz.h), so by default they are range-checked
+        first (one extra pass and a stream sync); callers whose arrays the sampler itself
+        maintains pass validate=False."""
+        if validate:
+            self.check_indices_device(B, zone_of_site, source)
         v = ctypes.c_void_p
         check(self._lib.sbz_loglik_batch_device(self.ctx, int(B), v(zone_of_site), v(w), v(p_global),
                                                 v(p_zones), v(p_fam or 0), v(source or 0),

@@ -30,6 +30,7 @@ contiguously by rank; the only collectives are the per-operator counter sum at t
 the warm-up arg-max (value, chain id) and the broadcast of the best sample (``parallel.py``).
 """
 import math
+import os
 import random as _random_module
 import time
 from collections import defaultdict
@@ -385,7 +386,14 @@ class BatchedZoneMCMC:
             import torch
             from .likelihood import LikelihoodEngine
             from .sampler import Sampler
-            dev = torch.cuda.current_device() if self._device is None else int(self._device)
+            dev = self._device
+            if dev is None:
+                # under torchrun each rank owns GPU LOCAL_RANK (one process per GPU), whether or
+                # not the caller bound it with torch.cuda.set_device
+                lr = os.environ.get("LOCAL_RANK")
+                dev = (int(lr) % torch.cuda.device_count() if _dist() is not None and lr is not None
+                       else torch.cuda.current_device())
+            dev = int(dev)
             self._device = dev
             obs = packing.features_to_obs(self.features)
             fam = packing.families_to_fam_of_site(self.families if self.inheritance and
@@ -438,6 +446,14 @@ class BatchedZoneMCMC:
         samples = [self.generate_initial_sample(c) for c in self.chain_idx]
         seed = self.seed if self.seed is not None else self.rng.getrandbits(63)
         self._philox_seed = broadcast_seed(int(seed), self._group)
+        self._tape_pos = None
+        self._alias = None
+        self._alias_logged = []  # logged samples whose p_* still alias chain 0's (source mode)
+        if self.hi == self.lo:
+            # more ranks than chains: this rank holds no chain but joins every collective
+            self._state = None
+            self._sync_host_ll()
+            return samples
         eng = self._get_engine()
         mine = samples[self.lo:self.hi]
         packed = [self._pack(s) for s in mine]
@@ -449,9 +465,6 @@ class BatchedZoneMCMC:
                                  source=stack(5) if self.sample_source else None)
         self._acc0 = self._state.accepted.clone()
         self._prop0 = self._state.proposed.clone()
-        self._tape_pos = None
-        self._alias = None
-        self._alias_logged = []  # logged samples whose p_* still alias chain 0's (source mode)
         if self.sample_source and self.lo == 0 and self.hi > 0:
             import torch
             st = self._state
@@ -466,6 +479,10 @@ class BatchedZoneMCMC:
         return samples
 
     def _sync_host_ll(self):
+        if self._state is None:
+            self._ll[:] = -np.inf
+            self._prior[:] = -np.inf
+            return
         ll = self._state.ll.cpu().numpy()
         self._ll[:] = -np.inf
         self._ll[self.lo:self.hi] = ll
@@ -474,7 +491,7 @@ class BatchedZoneMCMC:
 
     def _advance(self, n):
         """n MH steps on every chain of this rank (one launch)."""
-        if n <= 0:
+        if n <= 0 or self._state is None:
             return
         st = self._state
         kw = {}
@@ -511,10 +528,14 @@ class BatchedZoneMCMC:
 
     def _operator_counts(self):
         from .parallel import all_reduce_sum
-        acc = (self._state.accepted - self._acc0).sum(0)
-        prop = (self._state.proposed - self._prop0).sum(0)
         import torch
-        t = torch.stack([acc, prop]).to(torch.int64)
+        if self._state is None:
+            from .sampler import N_OPS_MAX
+            t = torch.zeros((2, N_OPS_MAX), dtype=torch.int64)
+        else:
+            acc = (self._state.accepted - self._acc0).sum(0)
+            prop = (self._state.proposed - self._prop0).sum(0)
+            t = torch.stack([acc, prop]).to(torch.int64)
         t = all_reduce_sum(t, self._group)
         return t[0].cpu().numpy(), t[1].cpu().numpy()
 

@@ -87,6 +87,9 @@ class ChainState:
                                  f"got {src.shape}")
             self.source = torch.as_tensor(src, device=dev)
         self.counter = torch.zeros(self.B, dtype=torch.int64, device=dev)
+        # the kernels trust the index bytes (include/sbz.h): range-check them once here
+        engine.check_indices_device(self.B, self.zone_of_site.data_ptr(),
+                                    self.source.data_ptr() if self.source is not None else 0)
         self.refresh_ll()
 
     def refresh_ll(self):
@@ -99,7 +102,7 @@ class ChainState:
                           self.p_global.data_ptr(), self.p_zones.data_ptr(),
                           self.p_fam.data_ptr() if self.p_fam is not None else 0,
                           self.source.data_ptr() if self.source is not None else 0,
-                          self.ll.data_ptr())
+                          self.ll.data_ptr(), validate=False)  # checked at construction
         return self.ll
 
     def to_numpy(self):

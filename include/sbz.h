@@ -99,10 +99,21 @@ int sbz_loglik_batch(sbz_ctx *ctx, int B, const uint8_t *zone_of_site, const dou
                      const double *p_global, const double *p_zones, const double *p_fam,
                      const uint8_t *source, double *out_ll);
 
-/* Same, all pointers on the device (out_ll: double[B] device); asynchronous on ctx's stream. */
+/* Same, all pointers on the device (out_ll: double[B] device); asynchronous on ctx's stream.
+ * The device entry points (this one and sbz_mh_run_device) TRUST their index bytes: they do
+ * not re-check zone_of_site < n_zones (or SBZ_NONE) and source < C, which sbz_loglik_batch
+ * checks on the host.  A caller holding device buffers of unknown origin calls
+ * sbz_check_indices_device first. */
 int sbz_loglik_batch_device(sbz_ctx *ctx, int B, const uint8_t *zone_of_site, const double *w,
                             const double *p_global, const double *p_zones, const double *p_fam,
                             const uint8_t *source, double *out_ll);
+
+/* Validate device index arrays (zone_of_site [B][N]: < n_zones or SBZ_NONE; source
+ * [B][N][F] or NULL: < C) with one kernel pass; synchronises ctx's stream.  SBZ_EINVAL with
+ * a message naming the first offending array, SBZ_OK otherwise.  No reference counterpart:
+ * the reference's arrays are host numpy arrays whose shapes/values it builds itself. */
+int sbz_check_indices_device(sbz_ctx *ctx, int B, const uint8_t *zone_of_site,
+                             const uint8_t *source);
 
 /* Device memory helpers (so a host without torch can stage device buffers). */
 int sbz_device_alloc(sbz_ctx *ctx, uint64_t bytes, void **out);

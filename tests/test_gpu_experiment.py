@@ -83,3 +83,16 @@ def test_balkan_experiment_geo_prior(gpu_available, tmp_path):
         assert any(stats["sample_prior"][s] == pytest.approx(r, rel=1e-9, abs=1e-9) for r in refs)
         n_geo += refs[0] != refs[1]
     assert n_geo > 0  # the geo term differs between the zones
+
+
+def test_runs_are_independent_and_reproducible(gpu_available, tmp_path):
+    """With --seed, the N_RUNS replicates draw from different streams (run index in the seed
+    derivation) and the main run's draws differ from its warm-up's; the same (seed, run) is
+    reproducible."""
+    cfg, _ = experiment.load_config(CFG, _short(tmp_path, SAMPLE_SOURCE=False))
+    data = experiment.ExperimentData(cfg)
+    a, _ = experiment.run_experiment(cfg, data, 2, run=0, name="r", seed=11)
+    b, _ = experiment.run_experiment(cfg, data, 2, run=1, name="r", seed=11)
+    c, _ = experiment.run_experiment(cfg, data, 2, run=0, name="r2", seed=11)
+    assert a["sample_likelihood"] != b["sample_likelihood"]
+    assert a["sample_likelihood"] == c["sample_likelihood"]

@@ -254,3 +254,78 @@ def test_chain_tickets_rearm_across_launches(gpu_available):
     for sl in (slice(0, 24), slice(3, 8), slice(0, 1), slice(5, 22), slice(0, 24)):
         got = eng.loglik(zos[sl], w[sl], pg[sl], pz[sl], pf[sl])
         np.testing.assert_array_equal(got, ref[sl])
+
+
+def test_partials_handoff_stress(gpu_available):
+    """The cross-workgroup hand-off of the task partials (finish_chain, sbz_lik.hip) under uneven
+    load: 512 chains x W > 1 tasks spread over every XCD, launched back to back with varying batch
+    sizes while another stream keeps the HBM busy.  A stale partial would change a chain's sum;
+    every launch must reproduce a quiet launch of the same batch size bit for bit (the task split,
+    W, depends on the batch size, so different sizes may differ in the last ulp), and the quiet
+    launches must match the oracle."""
+    import torch
+    from contact_zones_amd.likelihood import LikelihoodEngine
+    from oracle import oracle_c
+    rng = np.random.default_rng(31)
+    B = 512
+    obs, fam, zos, w, pg, pz, pf, _ = _random_batch(rng, 300, 240, 6, 4, 3, B, True, 12)
+    eng = LikelihoodEngine(obs, fam, 6, 4, 3, True)
+    dev = torch.device("cuda:0")
+    t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev)
+         for k, v in dict(zos=zos, w=w, pg=pg, pz=pz, pf=pf).items()}
+    main = torch.cuda.Stream()
+    noise = torch.cuda.Stream()
+    big = torch.empty(64 << 20, dtype=torch.float32, device=dev)
+    eng.set_stream(main.cuda_stream)
+    sizes = (B, 384, 100, 26, 7)
+    quiet = {nb: eng.loglik(zos[:nb], w[:nb], pg[:nb], pz[:nb], pf[:nb]) for nb in sizes}
+    outs = []
+    for it in range(40):
+        nb = sizes[it % len(sizes)] if it % 2 == 0 else sizes[int(rng.integers(0, len(sizes)))]
+        out = torch.full((B,), np.nan, dtype=torch.float64, device=dev)
+        with torch.cuda.stream(noise):
+            big.mul_(1.0000001)  # keep HBM / other CUs busy while the chains finish
+        with torch.cuda.stream(main):
+            eng.loglik_device(nb, t["zos"].data_ptr(), t["w"].data_ptr(), t["pg"].data_ptr(),
+                              t["pz"].data_ptr(), t["pf"].data_ptr(), 0, out.data_ptr(), validate=False)
+        outs.append((nb, out))
+    torch.cuda.synchronize()
+    for nb, out in outs:
+        np.testing.assert_array_equal(out.cpu().numpy()[:nb], quiet[nb])
+    oracle = oracle_c.loglik_batch(obs, fam, zos[:8], w[:8], pg[:8], pz[:8], pf[:8], inheritance=True)
+    for nb in sizes:
+        _assert_close(quiet[nb][:7], oracle[:7], 1e-12)
+
+
+def test_device_index_validation(gpu_available):
+    """The device entry points trust their index bytes; sbz_check_indices_device (and
+    LikelihoodEngine.loglik_device's default validate=True) refuse out-of-range zones / sources
+    with SBZ_EINVAL instead of letting the kernels read out of bounds."""
+    import torch
+    from contact_zones_amd._lib import SbzError
+    from contact_zones_amd.likelihood import LikelihoodEngine
+    rng = np.random.default_rng(5)
+    obs, fam, zos, w, pg, pz, pf, src = _random_batch(rng, 120, 30, 4, 2, 2, 6, True, 10)
+    eng = LikelihoodEngine(obs, fam, 4, 2, 2, True)
+    dev = torch.device("cuda:0")
+    t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev)
+         for k, v in dict(zos=zos, w=w, pg=pg, pz=pz, pf=pf, src=src).items()}
+    eng.set_stream(torch.cuda.current_stream().cuda_stream)
+    eng.check_indices_device(6, t["zos"].data_ptr(), t["src"].data_ptr())  # valid: no error
+    out = torch.empty(6, dtype=torch.float64, device=dev)
+    bad_z = t["zos"].clone()
+    bad_z[4, 77] = 2  # n_zones = 2: zone index 2 is out of range
+    with pytest.raises(SbzError, match="zone_of_site"):
+        eng.check_indices_device(6, bad_z.data_ptr(), 0)
+    with pytest.raises(SbzError, match="zone_of_site"):
+        eng.loglik_device(6, bad_z.data_ptr(), t["w"].data_ptr(), t["pg"].data_ptr(),
+                          t["pz"].data_ptr(), t["pf"].data_ptr(), 0, out.data_ptr())
+    bad_s = t["src"].clone()
+    bad_s[5, 119, 29] = 3  # C = 3
+    with pytest.raises(SbzError, match="source"):
+        eng.check_indices_device(6, t["zos"].data_ptr(), bad_s.data_ptr())
+    # after the refusals the engine still evaluates correctly
+    eng.loglik_device(6, t["zos"].data_ptr(), t["w"].data_ptr(), t["pg"].data_ptr(),
+                      t["pz"].data_ptr(), t["pf"].data_ptr(), 0, out.data_ptr())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy(), eng.loglik(zos, w, pg, pz, pf))
