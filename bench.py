@@ -253,9 +253,9 @@ def sampler_leg(args, eng, obs, fam, dev, rank, world, stream):
                      dtype=torch.float64, device=dev)
     if world > 1:
         red = t.clone()
-        dist.all_reduce(red, op=dist.ReduceOp.MAX)
+        _all_reduce(red, dist.ReduceOp.MAX)
         sm = t.clone()
-        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        _all_reduce(sm, dist.ReduceOp.SUM)
         t = torch.stack([red[0], red[1], sm[2], red[3], sm[4] / world])
     wall_max, dev_s, ess_tot, drift_max, acc_mean = (float(v) for v in t)
     return {
@@ -359,8 +359,8 @@ def source_sampler_leg(shape, B, K, burnin, seed, rank=0, world=1, device=0):
     t = torch.tensor([wall, float(e.sum()), acc], dtype=torch.float64, device=torch.device("cuda", device))
     if world > 1:
         mx, sm = t.clone(), t.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        _all_reduce(mx, dist.ReduceOp.MAX)
+        _all_reduce(sm, dist.ReduceOp.SUM)
         t = torch.stack([mx[0], sm[1], sm[2] / world])
     wall_max, ess_tot, acc_mean = (float(v) for v in t)
     eng.close()
@@ -443,8 +443,8 @@ def real_data_leg(name, n_zones_list, B, K, burnin, seed, rank=0, world=1, devic
                           dtype=torch.float64, device=torch.device("cuda", device))
         if world > 1:
             mx, sm = tt.clone(), tt.clone()
-            dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-            dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+            _all_reduce(mx, dist.ReduceOp.MAX)
+            _all_reduce(sm, dist.ReduceOp.SUM)
             tt = torch.stack([mx[0], sm[1], sm[2] / world])
         wall_max, ess_tot, acc = (float(v) for v in tt)
         out["runs"][f"Z={Z}"] = {"chains": B * world, "steps": K, "burnin": burnin,
@@ -453,6 +453,18 @@ def real_data_leg(name, n_zones_list, B, K, burnin, seed, rank=0, world=1, devic
                                  "acceptance": acc}
         eng.close()
     return out
+
+
+def _all_reduce(t, op):
+    """all_reduce of a (device) tensor in place; over gloo (the CPU rehearsal backend) through a
+    host copy."""
+    import torch.distributed as dist
+    if dist.get_backend() == "nccl":
+        dist.all_reduce(t, op=op)
+        return
+    h = t.cpu()
+    dist.all_reduce(h, op=op)
+    t.copy_(h)
 
 
 def main():
@@ -468,10 +480,17 @@ def main():
     import torch
     import torch.distributed as dist
 
+    # one rank per GPU; a rehearsal with more ranks than GPUs (SBZ_DIST_BACKEND=gloo: RCCL
+    # refuses two ranks on one device) shares the GPUs round-robin
+    local_rank = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("SBZ_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from contact_zones_amd.likelihood import LikelihoodEngine
 
@@ -521,7 +540,7 @@ def main():
 
     t = torch.tensor([wall, ev_ms / 1e3], dtype=torch.float64, device=dev)
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        _all_reduce(t, dist.ReduceOp.MAX)
     wall_max, ev_max = float(t[0]), float(t[1])
 
     total_evals = B * args.steps * world
