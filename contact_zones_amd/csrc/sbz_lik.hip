@@ -143,7 +143,8 @@ __device__ __forceinline__ void store_nw(double *nw, int lane, double w0r, doubl
 // ---------------------------------------------------------------------------------------
 #ifndef SBZ_ABLATE
 #define SBZ_ABLATE 0  // diagnostic builds only: 1 = skip gathers, 2 = skip table build,
-                      // 4 = skip tame checks, 8 = skip NA selects (wrong results)
+                      // 4 = skip tame checks, 8 = skip NA selects, 16 = every gather reads
+                      // the first table row (no bank conflicts) (wrong results)
 #endif
 #ifndef SBZ_MIX_WAVES
 #define SBZ_MIX_WAVES 3  // launch bound: minimum waves per SIMD of the dense mixture kernel
@@ -166,7 +167,41 @@ __device__ __forceinline__ void store_nw(double *nw, int lane, double w0r, doubl
 #ifndef SBZ_DB_GBAR
 #define SBZ_DB_GBAR 1  // double-buffered kernel: scheduling barrier every 8 gathers (VGPR bound)
 #endif
+#ifndef SBZ_TAME
+// 1: a feature's inputs are "tame" when every parameter lies in [0, 1 + 2^-20) (one unsigned max
+//    over the high words); products that still leave the normal range (tiny or zero cells) are
+//    caught after the fact and the task is re-run with per-factor renormalisation.
+// 0: every input checked against [2^-60, 2^60] or 0 before the feature (round-1 form).
+#define SBZ_TAME 1
+#endif
+#ifndef SBZ_RN
+// SBZ_TAME = 1: the dense kernel's product chains are checked and renormalised once per SBZ_RN
+// features (8 * SBZ_RN factors per chain; every factor <= ~1, so nothing overflows, and an
+// underflow is caught by the check and re-run exactly)
+#define SBZ_RN 4
+#endif
+#ifndef SBZ_ASM_ADDR
+#define SBZ_ASM_ADDR 0  // cell addresses by inline v_add_u32_sdwa (row offsets stay packed)
+#endif
 constexpr int NS = SBZ_PIPE;
+
+// Banked table layout (dense kernel, S + 1 <= 16).  The table lives in 256-B LDS lines, one
+// line per LDS bank sweep (64 banks x 4 B).  The no-zone rows T0[fc] (read by ~80 % of the
+// sites, mostly one family per 32-lane group after the family sort) own slots [0, S1) of lines
+// 0 .. FamC-1; every zone row (zc, fc) has a line of its own and sits in slots [S1, 2 S1) or
+// [32 - S1, 32) by zone parity, so a zoned lane never lands on a bank the group's hot row
+// uses, and zoned lanes of different zones spread over both halves.  Simulated on the bench
+// data: 3.3 LDS cycles per ds_read_b64 against 4.1 for the packed [class][x] layout.
+// Line FamC slots [0, S1) hold the neutral row (padding sites), lines FamC+1.. slots [0, S1)
+// the junk slots of lanes without an entry.
+__host__ __device__ constexpr int bk_lines(int Z, int FamC, int S1) {
+    return Z * FamC > FamC + 1 + (WAVE + S1 - 1) / S1 ? Z * FamC : FamC + 1 + (WAVE + S1 - 1) / S1;
+}
+// first double of row (zc, fc), zc = zone + 1 (0 = no zone)
+__host__ __device__ __forceinline__ uint32_t bk_row(int zc, int fc, int FamC, int S1) {
+    return zc == 0 ? (uint32_t)fc * 32u
+                   : (uint32_t)(((zc - 1) * FamC + fc) * 32 + S1 + ((zc - 1) & 1) * (32 - 2 * S1));
+}
 
 __device__ __forceinline__ void lds_phase() {
 #if SBZ_LDS_FENCE
@@ -182,6 +217,27 @@ __device__ __forceinline__ void lds_phase() {
 // factors times a mantissa in [0.5, 1) stay in the normal range.  Otherwise (tiny / huge /
 // negative / NaN inputs) the wave renormalises after every factor for that feature.
 __device__ __forceinline__ bool tame(double v) { return v == 0.0 || (v >= 0x1p-60 && v <= 0x1p60); }
+// Byte address of cell j (0..3) of a 4-site group: its 16-bit row offset (WORD_(j&1) of the
+// packed pair) plus its observation byte x*8 (BYTE_j of the observation word), one
+// v_add_u32_sdwa.  Written out so the row offsets stay packed two per register: the compiler
+// otherwise hoists the loop-invariant unpack out of the feature loop into 32 registers.
+__device__ __forceinline__ uint32_t cell_addr(uint32_t bw, uint32_t ow, int j) {
+    uint32_t r;
+    switch (j) {
+        case 0: asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:BYTE_0"
+                    : "=v"(r) : "v"(bw), "v"(ow)); break;
+        case 1: asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:BYTE_1"
+                    : "=v"(r) : "v"(bw), "v"(ow)); break;
+        case 2: asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:BYTE_2"
+                    : "=v"(r) : "v"(bw), "v"(ow)); break;
+        default: asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:BYTE_3"
+                     : "=v"(r) : "v"(bw), "v"(ow)); break;
+    }
+    return r;
+}
+__device__ __forceinline__ uint32_t hiword(double v) {
+    return (uint32_t)((unsigned long long)__double_as_longlong(v) >> 32);
+}
 
 // One feature's parameters as one lane needs them (the weights come from MixTable::prep).
 template <int C, int FR>
@@ -192,7 +248,10 @@ struct MixParams {
 };
 
 // Normalised weights are computed for NWC features at a time (MixTable::prep) and kept in LDS.
-constexpr int NWC = 32;
+#ifndef SBZ_NWC
+#define SBZ_NWC 32
+#endif
+constexpr int NWC = SBZ_NWC;
 // Per feature, h = hz | hf << 1: (c0, c1) of h at [2h, 2h + 1]; c2 of h at 8 + 2 * hz + hf, so
 // c2 of (h, h + 2) is one 16-B pair.  Every read of build() is a ds_read_b128.
 constexpr int NW_PER_F = 12;
@@ -202,8 +261,13 @@ constexpr int NW_PER_F = 12;
 // rows (rows >= Fam unused) so the build has no branches.
 constexpr int DB_TAB_BYTES = 4096;
 
-template <int C, int FR, bool DB = false, int SLOT = -1>
+// BK: banked table layout (bk_row).  PH: the SBZ_TAME = 1 input check, for kernels that catch
+// under-flowing products after the fact (the dense kernel); the others check every input.
+template <int C, int FR, bool DB = false, int SLOT = -1, bool BK = false, bool PH = false>
 struct MixTable {
+    // features per normalised-weight batch: 16 in the banked layout, so that 12 tasks per CU
+    // (3 waves per SIMD) fit the 160 KiB of LDS at the bench shape
+    static constexpr int NWCT = BK ? 16 : NWC;
     // SLOT >= 0: this wave loads and builds only zone-class slot SLOT (i = SLOT of the ZR
     // slots); the wave-specialised kernel splits the table between two builder waves this way.
     static constexpr bool has(int i) { return SLOT < 0 || i == SLOT; }
@@ -220,6 +284,15 @@ struct MixTable {
     int hz0;           // has-zone flag of the lane's slot-0 class (lg > 0)
     const double *pgb, *zbase, *fbase, *wb;
     uint32_t pzo[ZR];  // lane offset of its p_zones rows (elements)
+    // PH (dense kernel): the parameter loads are buffer loads whose per-feature and per-family
+    // advance is a scalar offset, so a feature's loads need no address arithmetic at all.  The
+    // NA column's lanes, and the zone loads of the no-zone class, use an out-of-range offset:
+    // the load returns 0, and adding `naone` (1 on the NA column, else 0) gives the reference's
+    // lh of 1 for NA cells (model.py:247) and 0 for the zone lh outside every zone, with no
+    // selects (p + 0 == p for every p but -0).
+    __amdgpu_buffer_rsrc_t rg, rz, rf;
+    uint32_t vg_off, vz_off[ZR];
+    double naone;
 
     __device__ __forceinline__ MixTable(const LikArgs &a, unsigned char *lds_, int b,
                                         double *tab0 = nullptr, double *tab1 = nullptr)
@@ -244,6 +317,10 @@ struct MixTable {
         junk = dyn + lane;
         // nwt 16-B aligned (one 8-B pad slot in the LDS budget)
         nwt = dyn + WAVE + (DB ? 0 : (((ncls + 1) * S1) & 1));
+        if (BK) {
+            junk = tab + (FamC + 1 + lane / S1) * 32 + lane % S1;
+            nwt = tab + bk_lines(Z, FamC, S1) * 32;
+        }
         nwf0 = -(1 << 30);
         nwbad = 0;
         hz0 = lg > 0 ? 1 : 0;
@@ -256,14 +333,40 @@ struct MixTable {
 #pragma unroll
         for (int i = 0; i < ZR; i++)
             pzo[i] = (uint32_t)(max(min(lg + i * G, Z), 1) - 1) * zfs + lxc;
+        if constexpr (PH) {
+            constexpr uint32_t OOB = 0x80000000u;  // beyond every buffer: the load returns 0
+            vg_off = na ? OOB : lxc * 8u;
+#pragma unroll
+            for (int i = 0; i < ZR; i++) vz_off[i] = (na || lg + i * G == 0) ? OOB : pzo[i] * 8u;
+            naone = na ? 1.0 : 0.0;
+            rg = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(pgb), (short)0, (int)(zfs * 8u), 0x00020000);
+            rz = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(zbase), (short)0,
+                                                   (int)((uint32_t)max(Z, 1) * zfs * 8u), 0x00020000);
+            rf = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(fbase), (short)0,
+                                                   (int)((uint32_t)max(Fam, 1) * zfs * 8u), 0x00020000);
+        }
         for (int x = lane; x < S1; x += WAVE) {  // neutral row (both buffers)
-            tab[ncls * S1 + x] = 1.0;
+            tab[(BK ? FamC * 32 : ncls * S1) + x] = 1.0;
             if (DB) tab1[ncls * S1 + x] = 1.0;
         }
     }
 
     __device__ __forceinline__ void load(int f, MixParams<C, FR> &r) const {
         const uint32_t fo = (uint32_t)f * (uint32_t)S;
+        if constexpr (PH) {
+            const int so = (int)(fo * 8u);
+            r.g = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rg, (int)vg_off, so, 0));
+#pragma unroll
+            for (int i = 0; i < ZR; i++)
+                if (has(i))
+                    r.z[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rz, (int)vz_off[i], so, 0));
+#pragma unroll
+            for (int fm = 0; fm < FR; fm++)
+                r.fm[fm] = __builtin_bit_cast(
+                    double, __builtin_amdgcn_raw_buffer_load_b64(
+                                rf, (int)vg_off, so + (int)((uint32_t)min(fm, max(Fam - 1, 0)) * zfs * 8u), 0));
+            return;
+        }
         r.g = pgb[fo + lxc];
 #pragma unroll
         for (int i = 0; i < ZR; i++)
@@ -299,11 +402,13 @@ struct MixTable {
         }
         lds_phase();  // earlier features' reads of nwt are done
         double *o = nwt + k * NW_PER_F;  // h = 2hp + hz
+        if (NWCT == 32 || k < NWCT) {
 #pragma unroll
-        for (int hz = 0; hz < 2; hz++) {
-            o[2 * (2 * hp + hz)] = n[hz][0];
-            o[2 * (2 * hp + hz) + 1] = n[hz][1];
-            o[8 + 2 * hz + hp] = n[hz][2];
+            for (int hz = 0; hz < 2; hz++) {
+                o[2 * (2 * hp + hz)] = n[hz][0];
+                o[2 * (2 * hp + hz) + 1] = n[hz][1];
+                o[8 + 2 * hz + hp] = n[hz][2];
+            }
         }
         nwbad = __ballot(!ok);
         nwf0 = f0;
@@ -314,12 +419,26 @@ struct MixTable {
     // some input is not tame, so products over this feature must renormalise after every factor.
     __device__ __forceinline__ bool build(const MixParams<C, FR> &r, int f, double *dbtab = nullptr) const {
         const int k = f - nwf0;
-        int ok = (int)tame(r.g);
+        int ok;
+        if constexpr (PH) {
+            // every parameter in [0, 1 + 2^-20): unsigned high words <= hi(1.0) (a sign bit, NaN or
+            // inf fails).  Table entries are then <= ~1, so a product never overflows, and one that
+            // underflows stays below 2^-1022 until the feature's check (see lik_mixture_kernel).
+            uint32_t hmx = hiword(r.g);
 #pragma unroll
-        for (int i = 0; i < ZR; i++)
-            if (has(i)) ok &= (int)tame(r.z[i]);
+            for (int i = 0; i < ZR; i++)
+                if (has(i)) hmx = max(hmx, hiword(r.z[i]));
 #pragma unroll
-        for (int fm = 0; fm < FR; fm++) ok &= (int)tame(r.fm[fm]);
+            for (int fm = 0; fm < FR; fm++) hmx = max(hmx, hiword(r.fm[fm]));
+            ok = hmx <= 0x3FF00000u;
+        } else {
+            ok = (int)tame(r.g);
+#pragma unroll
+            for (int i = 0; i < ZR; i++)
+                if (has(i)) ok &= (int)tame(r.z[i]);
+#pragma unroll
+            for (int fm = 0; fm < FR; fm++) ok &= (int)tame(r.fm[fm]);
+        }
 #if SBZ_ABLATE & 4
         ok = 1;  // diagnostic build: no tame checks
 #endif
@@ -355,7 +474,8 @@ struct MixTable {
         // written was last read by the gathers of feature f - 1, issued earlier.
         if (!DB) lds_phase();
         double *const tb = DB ? dbtab : tab;
-        const double l0 = na ? 1.0 : r.g;
+        const double l0 = PH ? r.g + naone : na ? 1.0 : r.g;
+        const double nad = PH ? naone : na ? 1.0 : 0.0;  // l2 of a class without family
 #pragma unroll
         for (int i = 0; i < ZR; i++) {
 #if SBZ_ABLATE & 2
@@ -366,15 +486,15 @@ struct MixTable {
             const bool valid = (lane < G * S1) && (zc <= Z);
             const double n00 = i == 0 ? p[0][0] : u[0][0], n01 = i == 0 ? p[0][1] : u[0][1];
             // zone lh: 0 for a site outside every zone (model.py:241-247), 1 for NA
-            const double l1 = na ? 1.0 : ((i > 0 || zc > 0) ? r.z[i] : 0.0);
-            double *row = valid ? tb + (zc * RPZ) * S1 + lx : junk;
-            const int rs = valid ? S1 : 0;
+            const double l1 = PH ? r.z[i] + naone : na ? 1.0 : ((i > 0 || zc > 0) ? r.z[i] : 0.0);
+            double *row = valid ? tb + (BK ? bk_row(zc, 0, FamC, S1) : (uint32_t)(zc * RPZ * S1)) + lx : junk;
+            const int rs = valid ? (BK ? 32 : S1) : 0;
             double v = n00 * l0 + n01 * l1;
             if (C == 3 && DB) {
                 // the reference's third term, l2 = 0 (no family) or 1 (NA): +0 for tame inputs
-                v = v + (i == 0 ? p[0][2] : u[0][2]) * (na ? 1.0 : 0.0);
+                v = v + (i == 0 ? p[0][2] : u[0][2]) * nad;
             } else if (C == 3 && wide) {
-                v = v + (i == 0 ? p[0][2] : u[0][2]) * (na ? 1.0 : 0.0);
+                v = v + (i == 0 ? p[0][2] : u[0][2]) * nad;
             }
             row[0] = v;
             if (C == 3) {
@@ -382,8 +502,15 @@ struct MixTable {
                 const double n12 = i == 0 ? p[1][2] : u[1][2];
                 const double a1 = n10 * l0 + n11 * l1;
 #pragma unroll
-                for (int fm = 0; fm < FR; fm++)
-                    if (DB || fm < Fam) row[(fm + 1) * rs] = a1 + n12 * (na ? 1.0 : r.fm[fm]);
+                for (int fm = 0; fm < FR; fm++) {
+                    const double lf = PH ? r.fm[fm] + naone : na ? 1.0 : r.fm[fm];
+                    if (PH) {  // families past Fam write to the junk slot: no branch
+                        double *dst = fm < Fam ? row + (fm + 1) * rs : junk;
+                        *dst = a1 + n12 * lf;
+                    } else if (DB || fm < Fam) {
+                        row[(fm + 1) * rs] = a1 + n12 * lf;
+                    }
+                }
             }
         }
         if (!DB) lds_phase();
@@ -399,35 +526,54 @@ struct MixTable {
 // Dense mixture kernel: every site of the task is gathered from the table.
 // The lane owns SPL sites (4*lane + 256*k + j); their class row offsets live in registers.
 // ---------------------------------------------------------------------------------------
-template <int C, int SPL, int FR, bool XS8>
+template <int C, int SPL, int FR, bool XS8, bool BK>
 __global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     constexpr int NO = SPL / 4;  // observation words (4 sites each) per lane per feature
+    constexpr bool PH = SBZ_TAME != 0;
     const int lane = threadIdx.x;
     const int b = blockIdx.y;
     const int fa = blockIdx.x * a.fpw;
     const int fb = min(a.F, fa + a.fpw);
-    MixTable<C, FR> t(a, lds, b);
+    MixTable<C, FR, false, -1, BK, PH> t(a, lds, b);
 
+    const __amdgpu_buffer_rsrc_t robs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t *>(a.obs_fm), (short)0, a.F * a.Np, 0x00020000);
     auto load_obs = [&](int f, int c0, uint32_t (&o)[NO]) {
-        const uint32_t *op = reinterpret_cast<const uint32_t *>(a.obs_fm + (size_t)f * a.Np + c0);
 #pragma unroll
-        for (int k = 0; k < NO; k++) o[k] = op[(uint32_t)(lane + 64 * k)];
+        for (int k = 0; k < NO; k++)  // one lane offset; the word index goes to the scalar offset
+            o[k] = __builtin_amdgcn_raw_buffer_load_b32(robs, lane * 4, f * a.Np + c0 + 256 * k, 0);
     };
 
-    double m[4] = {1.0, 1.0, 1.0, 1.0};  // four independent product chains
-    int e = 0;
+    double m[4];  // four independent product chains
+    int e;
+    // PH: a lane's product fell below 2^-1022 (a zero or tiny cell): the wave re-runs the task
+    // with per-factor renormalisation (`force`), which is exact for any normal double.
+    uint64_t under;
+    bool force = false;
     uint32_t base2[SPL / 2];  // per-site class row offsets (bytes, < 64 KiB), two per register
     MixParams<C, FR> P[NS];   // parameter sets: feature f uses P[(f - fa) % NS]
     uint32_t O[NS][NO];       // observation sets, same rotation
+
+    // PH: the product chains since the last check; every factor is <= ~1, so a product that left
+    // the normal range is still below it here.  Then renormalise.
+    auto flush = [&]() {
+        if (PH) {
+            const double mn = fmin(fmin(m[0], m[1]), fmin(m[2], m[3]));
+            under |= __ballot(!(mn >= 0x1p-1022));
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            if (q < NO) renorm(m[q], e);
+    };
 
     // One feature: build its table from `cur`, issue the loads of feature f + NS - 1 into
     // `fill` (the sets feature f - 1 used), gather.  `live` = false for padding features.
     auto feature = [&](int f, int c0, bool live, const MixParams<C, FR> &cur, const uint32_t (&ob)[NO],
                        MixParams<C, FR> &fill, uint32_t (&ofill)[NO]) {
         const int fk = min(f, fb - 1);
-        if (fk < t.nwf0 || fk >= t.nwf0 + NWC) t.prep(fk, fb);  // uniform, once per NWC features
-        const bool wide = t.build(cur, fk);
+        if (fk < t.nwf0 || fk >= t.nwf0 + t.NWCT) t.prep(fk, fb);  // uniform, once per NWCT features
+        const bool wide = t.build(cur, fk) || (PH && force);
         __builtin_amdgcn_sched_barrier(0);
         t.load(min(f + NS - 1, fb - 1), fill);
         load_obs(min(f + NS - 1, fb - 1), c0, ofill);
@@ -439,16 +585,16 @@ __global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArg
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     const uint32_t bw = base2[2 * k + (j >> 1)];
-                    const uint32_t bs = (j & 1) ? (bw >> 16) : (bw & 0xffffu);
+                    const uint32_t bs = (SBZ_ABLATE & 16) ? 0u : (j & 1) ? (bw >> 16) : (bw & 0xffffu);
                     const uint32_t xb = (ob[k] >> (8 * j)) & 0xffu;
-                    m[k & 3] *= t.at(bs + (XS8 ? xb : (xb << 3)));
+                    m[k & 3] *= t.at((XS8 && PH && SBZ_ASM_ADDR && !(SBZ_ABLATE & 16))
+                                         ? cell_addr(bw, ob[k], j) : bs + (XS8 ? xb : (xb << 3)));
                     if (j == 3 && (k & 1)) __builtin_amdgcn_sched_barrier(0);  // <= 8 reads in flight
                 }
-#pragma unroll
-            for (int q = 0; q < 4; q++)
-                if (q < NO) renorm(m[q], e);
+            if (!PH || SBZ_RN == 1 || (f - fa) % SBZ_RN == SBZ_RN - 1) flush();
         } else {
             // untamed inputs: renormalise after every factor (exact for any normal double)
+            if (PH) flush();  // the products since the last check first
 #pragma unroll
             for (int k = 0; k < NO; k++)
 #pragma unroll
@@ -456,12 +602,16 @@ __global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArg
                     const uint32_t bw = base2[2 * k + (j >> 1)];
                     const uint32_t bs = (j & 1) ? (bw >> 16) : (bw & 0xffffu);
                     const uint32_t xb = (ob[k] >> (8 * j)) & 0xffu;
-                    m[0] *= t.at(bs + (XS8 ? xb : (xb << 3)));
+                    m[0] *= t.at((XS8 && PH && SBZ_ASM_ADDR) ? cell_addr(bw, ob[k], j) : bs + (XS8 ? xb : (xb << 3)));
                     renorm(m[0], e);
                 }
         }
     };
 
+  for (;;) {
+    m[0] = m[1] = m[2] = m[3] = 1.0;
+    e = 0;
+    under = 0;
     for (int c0 = 0; c0 < a.Np; c0 += SPL * WAVE) {
         // classes of this chunk's sites (cls = zc*FamC + fc, padding -> the neutral row); the
         // first NS - 1 features' parameters and observations
@@ -493,8 +643,10 @@ __global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArg
                 const int pos = c0 + 4 * lane + 256 * (i / 4) + (i % 4);
                 const int z = (int)zs[i];
                 const int fc = (int)((fw[i / 4] >> (8 * (i % 4))) & 0xffu);
-                const int cls = pos < a.N ? ((z < t.Z ? z + 1 : 0) * t.FamC + fc) : t.ncls;
-                const uint32_t off = (uint32_t)(cls * t.row_bytes);
+                const int zc = z < t.Z ? z + 1 : 0;
+                uint32_t off;
+                if (BK) off = 8u * (pos < a.N ? bk_row(zc, fc, t.FamC, t.S1) : (uint32_t)(t.FamC * 32));
+                else off = (uint32_t)((pos < a.N ? zc * t.FamC + fc : t.ncls) * t.row_bytes);
                 if (i & 1) base2[i >> 1] |= off << 16;
                 else base2[i >> 1] = off;
             }
@@ -505,6 +657,10 @@ __global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArg
                 feature(f + j, c0, f + j < fb, P[j], O[j], P[(j + NS - 1) % NS], O[(j + NS - 1) % NS]);
         }
     }
+    if (PH) flush();
+    if (!PH || force || under == 0) break;
+    force = true;  // uniform: `under` is a ballot
+  }
     double v = (log(m[0]) + log(m[1])) + (log(m[2]) + log(m[3]));
     v = v + (double)e * LN2;
     const double tot = wave_sum(v);
@@ -1635,7 +1791,7 @@ const void *mix_ws_kernel(int C, int fr, int spl, int ng, int nb) {
     return mix_ws_kernel_c<2, 4>(spl, ng, nb);
 }
 
-template <int C, int FR, bool XS8>
+template <int C, int FR, bool XS8, bool BK = false>
 const void *mix_kernel_x(bool zoned, int spl, int zspl) {
     if (zoned) {
         switch (zspl) {
@@ -1645,14 +1801,19 @@ const void *mix_kernel_x(bool zoned, int spl, int zspl) {
         }
     }
     switch (spl) {
-        case 4: return reinterpret_cast<const void *>(&lik_mixture_kernel<C, 4, FR, XS8>);
-        case 8: return reinterpret_cast<const void *>(&lik_mixture_kernel<C, 8, FR, XS8>);
-        case 16: return reinterpret_cast<const void *>(&lik_mixture_kernel<C, 16, FR, XS8>);
-        default: return reinterpret_cast<const void *>(&lik_mixture_kernel<C, 32, FR, XS8>);
+        case 4: return reinterpret_cast<const void *>(&lik_mixture_kernel<C, 4, FR, XS8, BK>);
+        case 8: return reinterpret_cast<const void *>(&lik_mixture_kernel<C, 8, FR, XS8, BK>);
+        case 16: return reinterpret_cast<const void *>(&lik_mixture_kernel<C, 16, FR, XS8, BK>);
+        default: return reinterpret_cast<const void *>(&lik_mixture_kernel<C, 32, FR, XS8, BK>);
     }
 }
 
-const void *mix_kernel(int C, int fr, bool xs8, bool zoned, int spl, int zspl) {
+const void *mix_kernel(int C, int fr, bool xs8, bool zoned, int spl, int zspl, bool bk = false) {
+    if (bk && !zoned) {  // banked layout: S + 1 <= 16, so observations are always x*8
+        if (C == 3) return fr == 4 ? mix_kernel_x<3, 4, true, true>(false, spl, zspl)
+                                   : mix_kernel_x<3, 8, true, true>(false, spl, zspl);
+        return mix_kernel_x<2, 4, true, true>(false, spl, zspl);
+    }
     if (C == 3) {
         if (fr == 4) return xs8 ? mix_kernel_x<3, 4, true>(zoned, spl, zspl) : mix_kernel_x<3, 4, false>(zoned, spl, zspl);
         return xs8 ? mix_kernel_x<3, 8, true>(zoned, spl, zspl) : mix_kernel_x<3, 8, false>(zoned, spl, zspl);
@@ -1697,11 +1858,15 @@ void configure_mix_x(std::vector<const void *> &v) {
     v.push_back(reinterpret_cast<const void *>(&lik_zoned_kernel<C, 4, FR, XS8>));
     v.push_back(reinterpret_cast<const void *>(&lik_zoned_kernel<C, 8, FR, XS8>));
     v.push_back(reinterpret_cast<const void *>(&lik_zoned_kernel<C, 16, FR, XS8>));
-    v.push_back(reinterpret_cast<const void *>(&lik_mixture_kernel<C, 4, FR, XS8>));
-    v.push_back(reinterpret_cast<const void *>(&lik_mixture_kernel<C, 8, FR, XS8>));
-    v.push_back(reinterpret_cast<const void *>(&lik_mixture_kernel<C, 16, FR, XS8>));
-    v.push_back(reinterpret_cast<const void *>(&lik_mixture_kernel<C, 32, FR, XS8>));
+    v.push_back(reinterpret_cast<const void *>(&lik_mixture_kernel<C, 4, FR, XS8, false>));
+    v.push_back(reinterpret_cast<const void *>(&lik_mixture_kernel<C, 8, FR, XS8, false>));
+    v.push_back(reinterpret_cast<const void *>(&lik_mixture_kernel<C, 16, FR, XS8, false>));
+    v.push_back(reinterpret_cast<const void *>(&lik_mixture_kernel<C, 32, FR, XS8, false>));
     if (XS8) {
+        v.push_back(reinterpret_cast<const void *>(&lik_mixture_kernel<C, 4, FR, true, true>));
+        v.push_back(reinterpret_cast<const void *>(&lik_mixture_kernel<C, 8, FR, true, true>));
+        v.push_back(reinterpret_cast<const void *>(&lik_mixture_kernel<C, 16, FR, true, true>));
+        v.push_back(reinterpret_cast<const void *>(&lik_mixture_kernel<C, 32, FR, true, true>));
         for (int nb = 1; nb <= 2; nb++)
             for (int ng = 1; ng <= 2; ng++)
                 for (int spl = 4; spl <= 32; spl *= 2) v.push_back(mix_ws_kernel(C, FR, spl, ng, nb));
@@ -1742,11 +1907,14 @@ void configure_source(std::vector<const void *> &v) {
 struct MixPlan {
     int fr = 0;
     bool db = false;  // the double-buffered kernel applies (obs as x*8, table <= DB_TAB_BYTES)
+    bool bk = false;  // the banked table layout applies (S + 1 <= 16, fits 64 KiB)
 };
 
-size_t mix_lds_bytes(const sbz_dims &d, int C) {
+size_t mix_lds_bytes(const sbz_dims &d, int C, bool bk = false) {
     const size_t S1 = (size_t)d.n_states + 1;
     const size_t Fam = C == 3 ? (size_t)d.n_families : 0;
+    if (bk)  // the lines hold the table, the neutral row and the junk slots
+        return ((size_t)bk_lines(d.n_zones, (int)Fam + 1, (int)S1) * 32 + (size_t)16 * NW_PER_F) * 8;
     const size_t ncls = (size_t)(d.n_zones + 1) * (Fam + 1);
     return ((ncls + 1) * S1 + WAVE + 1 + (size_t)NWC * NW_PER_F) * 8;
 }
@@ -1771,6 +1939,7 @@ MixPlan plan_mixture(const sbz_dims &d, int C, bool xs8 = false) {
         const int rpz = C == 3 ? p.fr + 1 : 1;
         const size_t tab = ((size_t)(d.n_zones + 1) * rpz + 1) * S1 * 8;
         p.db = xs8 && tab <= (size_t)DB_TAB_BYTES;
+        p.bk = 2 * S1 <= 32 && mix_lds_bytes(d, C, true) <= 64 * 1024;
     }
     return p;
 }
@@ -1795,7 +1964,10 @@ size_t lik_lds_bytes(const sbz_dims &d, bool source_mode) {
     const bool inh = (d.flags & SBZ_INHERITANCE) != 0;
     const int C = inh ? 3 : 2;
     const size_t S1 = (size_t)d.n_states + 1;
-    if (!source_mode) return plan_mixture(d, C).fr ? mix_lds_bytes(d, C) : 0;
+    if (!source_mode) {
+        const MixPlan p = plan_mixture(d, C);
+        return p.fr ? mix_lds_bytes(d, C, p.bk) : 0;
+    }
     const size_t rows = 4 + 2 * (size_t)d.n_zones + (inh ? 2 * (size_t)d.n_families : 0) + 2;
     return NW_BYTES + rows * S1 * sizeof(double);
 }
@@ -1860,6 +2032,7 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
                      ctx->FamC * (d.n_states + 1) <= WAVE;
             }
             // (the <C=3, SPL=32, FR=8> instantiation of the double-buffered kernel spills)
+            const bool bk = plan.bk && ctx->lik_kernel == 1 && ctx->lik_banked;
             const bool db = plan.db && !zoned && ctx->lik_kernel == 3 &&
                             !(ctx->C == 3 && plan.fr == 8 && ctx->spl == 32);
             // wave-specialised: a builder wave and ng gatherer waves of spl / ng sites per lane
@@ -1879,7 +2052,7 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
                 a.cnt = ctx->d_cnt;
             }
             lds = zd ? zd_lds_bytes(d, ctx->C) : ws ? mix_ws_lds_bytes() : db ? mix_db_lds_bytes()
-                                                                             : mix_lds_bytes(d, ctx->C);
+                                                                             : mix_lds_bytes(d, ctx->C, bk);
             if (zd) {
                 a.obs8 = ctx->d_obs8;
                 a.F4 = ctx->F4;
@@ -1890,7 +2063,7 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
                 mix_fn = mix_ws_kernel(ctx->C, plan.fr, ctx->spl / ng, ng, ctx->ws_nb);
             } else {
                 mix_fn = db ? mix_db_kernel(ctx->C, plan.fr, ctx->spl)
-                            : mix_kernel(ctx->C, plan.fr, ctx->xs8 != 0, zoned, ctx->spl, ctx->zspl);
+                            : mix_kernel(ctx->C, plan.fr, ctx->xs8 != 0, zoned, ctx->spl, ctx->zspl, bk);
             }
             // Long tasks: one resident round of single-wave tasks (occupancy x CUs) over the
             // launch, so every wave streams its features with no tail of late tasks.

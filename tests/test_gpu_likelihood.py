@@ -221,6 +221,40 @@ def test_zone_sparse_paths(gpu_available, monkeypatch, kernel, zspl):
     _assert_close(got, ref, tol=1e-12)
 
 
+@pytest.mark.parametrize("banked", ["1", "0"])
+@pytest.mark.parametrize("shape", [(1500, 40, 6, 4, 3, 9), (2000, 64, 10, 8, 4, 9), (300, 21, 15, 3, 2, 9)])
+def test_dense_edge_paths(gpu_available, monkeypatch, banked, shape):
+    """Dense kernel (banked and packed table layouts) on inputs that leave the fast path: zero
+    cells (finite when another component covers them, -inf otherwise), tiny parameters whose
+    products underflow (the task re-runs with per-factor renormalisation), parameters above 1
+    and denormal parameters (per-feature renormalisation)."""
+    from contact_zones_amd.likelihood import LikelihoodEngine
+    from oracle import oracle_c
+    monkeypatch.setenv("SBZ_LIK_KERNEL", "dense")
+    monkeypatch.setenv("SBZ_LIK_BANKED", banked)
+    N, F, S, Z, Fam, B = shape
+    rng = np.random.default_rng(N + F)
+    obs, fam, zos, w, pg, pz, pf, _ = _random_batch(rng, N, F, S, Z, Fam, B, True, N // (3 * Z))
+    zoned34 = (zos[3] != 255) & (zos[4] != 255)
+    obs[~zoned34 & (obs[:, 0] == 0), 0] = 1
+    for b in (3, 4):
+        pg[b, 0, 0] = 0.0
+        pf[b, :, 0, 0] = 0.0
+    s_out = int(np.flatnonzero(zos[4] == 255)[0])
+    obs[s_out, 0] = 0
+    zos[3, s_out] = 0
+    pg[5, :, 1] = 1e-200                 # tiny: products underflow -> task re-run
+    pz[6, :, :, 2] = 0.0                 # zero zoned cells
+    pg[7, 3:9] *= 7.5                    # above 1 -> per-feature renormalisation
+    pf[8, :, 5, :] = 4e-320              # denormal family parameters
+    eng = LikelihoodEngine(obs, fam, S, Z, Fam, True)
+    got = eng.loglik(zos, w, pg, pz, pf)
+    ref = oracle_c.loglik_batch(obs, fam, zos, w, pg, pz, pf, inheritance=True)
+    assert np.isfinite(ref[3]) and ref[4] == -np.inf
+    _assert_close(got, ref, tol=1e-12)
+    assert eng.lds_bytes(False) > 0
+
+
 @pytest.mark.parametrize("nofam,Fam,inh", [(0.0, 4, True), (1.0, 4, True), (0.3, 4, True),
                                            (0.0, 0, False), (0.0, 0, True)])
 @pytest.mark.parametrize("zspl", ["4", "8"])
