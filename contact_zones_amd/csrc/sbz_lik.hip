@@ -180,9 +180,30 @@ __device__ __forceinline__ void store_nw(double *nw, int lane, double w0r, doubl
 // underflow is caught by the check and re-run exactly)
 #define SBZ_RN 4
 #endif
+#ifndef SBZ_GIF
+#define SBZ_GIF 16  // dense kernel: table reads in flight per wave (scheduling barrier every SBZ_GIF)
+#endif
+#ifndef SBZ_OBS_X4
+#define SBZ_OBS_X4 0  // dense kernel: observations as 16-B loads (4 words of 4 sites per lane)
+#endif
 #ifndef SBZ_ASM_ADDR
 #define SBZ_ASM_ADDR 0  // cell addresses by inline v_add_u32_sdwa (row offsets stay packed)
 #endif
+#ifndef SBZ_LIK_STAMP
+// diagnostic builds only: the dense kernel returns, instead of each chain's log-likelihood, the
+// s_memtime cycles its waves spent in phase a.F4 (0 weights, 1 table build, 2 load issue,
+// 3 gathers + renorm, 4 task set-up, 5 whole task), summed over the chain's tasks
+#define SBZ_LIK_STAMP 0
+#endif
+__device__ __forceinline__ uint64_t lik_stamp() {
+    uint64_t t = 0;
+    if (SBZ_LIK_STAMP) {
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    return t;
+}
 constexpr int NS = SBZ_PIPE;
 
 // Banked table layout (dense kernel, S + 1 <= 16).  The table lives in 256-B LDS lines, one
@@ -380,10 +401,32 @@ struct MixTable {
     // h = hz | hf << 1 of features f0 .. f0 + NWC (clamped to fb - 1), into nwt.  Lane 2k + hp
     // computes feature k's h = 2hp and 2hp + 1 (one division per weight, as the reference).
     // Runs once per NWC features instead of once per feature.
+    // PH: the weights of the next batch are loaded one batch ahead (prep_issue), so prep does
+    // not wait a memory round trip; a batch other than the one in flight loads on the spot.
+    double pw0 = 0.0, pw1 = 0.0, pw2 = 0.0;
+    int pwf0 = -(1 << 30);
+    __device__ __forceinline__ void prep_issue(int f0, int fb) {
+        const uint32_t f = (uint32_t)min(f0 + (lane >> 1), fb - 1);
+        pw0 = wb[f * C];
+        pw1 = wb[f * C + 1];
+        pw2 = C == 3 ? wb[f * C + 2] : 0.0;
+        pwf0 = f0;
+    }
     __device__ __forceinline__ void prep(int f0, int fb) {
         const int k = lane >> 1, hp = lane & 1;
-        const uint32_t f = (uint32_t)min(f0 + k, fb - 1);
-        const double w0r = wb[f * C], w1r = wb[f * C + 1], w2r = C == 3 ? wb[f * C + 2] : 0.0;
+        double w0r, w1r, w2r;
+        if (PH) {
+            if (pwf0 != f0) prep_issue(f0, fb);
+            w0r = pw0;
+            w1r = pw1;
+            w2r = pw2;
+            prep_issue(f0 + NWCT, fb);
+        } else {
+            const uint32_t f = (uint32_t)min(f0 + k, fb - 1);
+            w0r = wb[f * C];
+            w1r = wb[f * C + 1];
+            w2r = C == 3 ? wb[f * C + 2] : 0.0;
+        }
         int ok = 1;
         double n[2][3];
 #pragma unroll
@@ -537,12 +580,29 @@ __global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArg
     const int fb = min(a.F, fa + a.fpw);
     MixTable<C, FR, false, -1, BK, PH> t(a, lds, b);
 
+    // SBZ_OBS_X4 (NO a multiple of 4): word k of a lane holds positions
+    // c0 + 1024 (k / 4) + 16 lane + 4 (k % 4) + 0..3, one 16-B load per 4 words; otherwise
+    // positions c0 + 256 k + 4 lane + 0..3, one dword load per word.
+    constexpr bool X4 = SBZ_OBS_X4 && PH && NO % 4 == 0;
+    auto wpos = [&](int c0, int k) {
+        return X4 ? c0 + 1024 * (k / 4) + 16 * lane + 4 * (k % 4) : c0 + 4 * lane + 256 * k;
+    };
     const __amdgpu_buffer_rsrc_t robs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t *>(a.obs_fm), (short)0, a.F * a.Np, 0x00020000);
     auto load_obs = [&](int f, int c0, uint32_t (&o)[NO]) {
 #pragma unroll
         for (int k = 0; k < NO; k++)  // one lane offset; the word index goes to the scalar offset
-            o[k] = __builtin_amdgcn_raw_buffer_load_b32(robs, lane * 4, f * a.Np + c0 + 256 * k, 0);
+            if (!X4) o[k] = __builtin_amdgcn_raw_buffer_load_b32(robs, lane * 4, f * a.Np + c0 + 256 * k, 0);
+        if (X4) {
+#pragma unroll
+            for (int q = 0; q < NO / 4; q++) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(robs, lane * 16, f * a.Np + c0 + 1024 * q, 0);
+                o[4 * q] = v[0];
+                o[4 * q + 1] = v[1];
+                o[4 * q + 2] = v[2];
+                o[4 * q + 3] = v[3];
+            }
+        }
     };
 
     double m[4];  // four independent product chains
@@ -555,6 +615,8 @@ __global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArg
     MixParams<C, FR> P[NS];   // parameter sets: feature f uses P[(f - fa) % NS]
     uint32_t O[NS][NO];       // observation sets, same rotation
 
+    uint64_t cyc[6] = {0, 0, 0, 0, 0, 0};  // SBZ_LIK_STAMP: cycles per phase
+    const uint64_t tstart = lik_stamp();
     // PH: the product chains since the last check; every factor is <= ~1, so a product that left
     // the normal range is still below it here.  Then renormalise.
     auto flush = [&]() {
@@ -572,11 +634,20 @@ __global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArg
     auto feature = [&](int f, int c0, bool live, const MixParams<C, FR> &cur, const uint32_t (&ob)[NO],
                        MixParams<C, FR> &fill, uint32_t (&ofill)[NO]) {
         const int fk = min(f, fb - 1);
+        uint64_t t0 = lik_stamp();
         if (fk < t.nwf0 || fk >= t.nwf0 + t.NWCT) t.prep(fk, fb);  // uniform, once per NWCT features
+        uint64_t t1 = lik_stamp();
         const bool wide = t.build(cur, fk) || (PH && force);
+        uint64_t t2 = lik_stamp();
         __builtin_amdgcn_sched_barrier(0);
         t.load(min(f + NS - 1, fb - 1), fill);
         load_obs(min(f + NS - 1, fb - 1), c0, ofill);
+        uint64_t t3 = lik_stamp();
+        if (SBZ_LIK_STAMP) {
+            cyc[0] += t1 - t0;
+            cyc[1] += t2 - t1;
+            cyc[2] += t3 - t2;
+        }
         if (SBZ_ABLATE & 1 || !live) {
             // padding feature (or diagnostic build): no gathers
         } else if (!wide) {
@@ -589,7 +660,8 @@ __global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArg
                     const uint32_t xb = (ob[k] >> (8 * j)) & 0xffu;
                     m[k & 3] *= t.at((XS8 && PH && SBZ_ASM_ADDR && !(SBZ_ABLATE & 16))
                                          ? cell_addr(bw, ob[k], j) : bs + (XS8 ? xb : (xb << 3)));
-                    if (j == 3 && (k & 1)) __builtin_amdgcn_sched_barrier(0);  // <= 8 reads in flight
+                    // <= SBZ_GIF reads in flight
+                    if (j == 3 && (k & (SBZ_GIF / 4 - 1)) == SBZ_GIF / 4 - 1) __builtin_amdgcn_sched_barrier(0);
                 }
             if (!PH || SBZ_RN == 1 || (f - fa) % SBZ_RN == SBZ_RN - 1) flush();
         } else {
@@ -606,6 +678,7 @@ __global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArg
                     renorm(m[0], e);
                 }
         }
+        if (SBZ_LIK_STAMP) cyc[3] += lik_stamp() - t3;
     };
 
   for (;;) {
@@ -613,6 +686,7 @@ __global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArg
     e = 0;
     under = 0;
     for (int c0 = 0; c0 < a.Np; c0 += SPL * WAVE) {
+        const uint64_t ts = lik_stamp();
         // classes of this chunk's sites (cls = zc*FamC + fc, padding -> the neutral row); the
         // first NS - 1 features' parameters and observations
         {
@@ -622,7 +696,7 @@ __global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArg
             uint32_t fw[NO];
 #pragma unroll
             for (int k = 0; k < NO; k++) {
-                const uint32_t p0 = (uint32_t)(c0 + 4 * lane + 256 * k);  // < Np (arrays padded)
+                const uint32_t p0 = (uint32_t)wpos(c0, k);  // < Np (arrays padded)
                 pv[k] = *reinterpret_cast<const int4 *>(a.perm + p0);
                 fw[k] = *reinterpret_cast<const uint32_t *>(a.famc + p0);
             }
@@ -638,9 +712,10 @@ __global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArg
                 t.load(min(fa + j, fb - 1), P[j]);
                 load_obs(min(fa + j, fb - 1), c0, O[j]);
             }
+            if (PH && t.pwf0 != fa) t.prep_issue(fa, fb);  // the first weights, with the zone bytes
 #pragma unroll
             for (int i = 0; i < SPL; i++) {
-                const int pos = c0 + 4 * lane + 256 * (i / 4) + (i % 4);
+                const int pos = wpos(c0, i / 4) + (i % 4);
                 const int z = (int)zs[i];
                 const int fc = (int)((fw[i / 4] >> (8 * (i % 4))) & 0xffu);
                 const int zc = z < t.Z ? z + 1 : 0;
@@ -651,6 +726,7 @@ __global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArg
                 else base2[i >> 1] = off;
             }
         }
+        if (SBZ_LIK_STAMP) cyc[4] += lik_stamp() - ts;
         for (int f = fa; f < fb; f += NS) {
 #pragma unroll
             for (int j = 0; j < NS; j++)
@@ -663,7 +739,14 @@ __global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArg
   }
     double v = (log(m[0]) + log(m[1])) + (log(m[2]) + log(m[3]));
     v = v + (double)e * LN2;
-    const double tot = wave_sum(v);
+    double tot = wave_sum(v);
+    if (SBZ_LIK_STAMP) {
+        cyc[5] = lik_stamp() - tstart;
+        uint64_t c = cyc[0];
+#pragma unroll
+        for (int q = 1; q < 6; q++) c = a.F4 == q ? cyc[q] : c;
+        tot = (double)c;
+    }
     finish_chain(a, b, tot);
 }
 
@@ -2014,6 +2097,10 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
     a.pg = pg;
     a.pz = pz;
     a.pf = pf;
+    if (SBZ_LIK_STAMP) {  // diagnostic build: the phase the dense kernel reports
+        const char *v = getenv("SBZ_STAMP_PHASE");
+        a.F4 = v ? atoi(v) : 5;
+    }
 
     MixPlan plan;
     bool zoned = false, ws = false, zd = false;
