@@ -144,7 +144,8 @@ __device__ __forceinline__ void store_nw(double *nw, int lane, double w0r, doubl
 #ifndef SBZ_ABLATE
 #define SBZ_ABLATE 0  // diagnostic builds only: 1 = skip gathers, 2 = skip table build,
                       // 4 = skip tame checks, 8 = skip NA selects, 16 = every gather reads
-                      // the first table row (no bank conflicts) (wrong results)
+                      // the first table row (no bank conflicts), 32 = constant normalised
+                      // weights (no LDS weight reads) (wrong results)
 #endif
 #ifndef SBZ_MIX_WAVES
 #define SBZ_MIX_WAVES 3  // launch bound: minimum waves per SIMD of the dense mixture kernel
@@ -366,6 +367,8 @@ struct MixTable {
             rf = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(fbase), (short)0,
                                                    (int)((uint32_t)max(Fam, 1) * zfs * 8u), 0x00020000);
         }
+        if (SBZ_ABLATE & 2)  // diagnostic build without table builds: a constant table
+            for (int q = lane; q < (BK ? bk_lines(Z, FamC, S1) * 32 : (ncls + 1) * S1); q += WAVE) tab[q] = 0.5;
         for (int x = lane; x < S1; x += WAVE) {  // neutral row (both buffers)
             tab[(BK ? FamC * 32 : ncls * S1) + x] = 1.0;
             if (DB) tab1[ncls * S1 + x] = 1.0;
@@ -491,7 +494,10 @@ struct MixTable {
         //    (lanes lg == 0, h = 0 / 2) and zone classes (h = 1 / 3).
         //    Six 16-B reads: (c0, c1) of each h, and c2 of (h, h + 2) as one pair.
         const double *nk = static_cast<const double *>(__builtin_assume_aligned(nwt + k * NW_PER_F, 16));
-        auto pair = [&](int at) { return *reinterpret_cast<const double2 *>(nk + at); };
+        auto pair = [&](int at) {
+            if (SBZ_ABLATE & 32) return double2{0.25 + at, 0.5};  // diagnostic: no LDS weight reads
+            return *reinterpret_cast<const double2 *>(nk + at);
+        };
         double u[2][3], p[2][3];
         const double2 cu = pair(10), cp = pair(8 + 2 * hz0);  // c2 of (h, h + 2), hz = 1 / hz0
 #pragma unroll
