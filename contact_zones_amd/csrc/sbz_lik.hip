@@ -184,6 +184,9 @@ __device__ __forceinline__ void store_nw(double *nw, int lane, double w0r, doubl
 #ifndef SBZ_GIF
 #define SBZ_GIF 16  // dense kernel: table reads in flight per wave (scheduling barrier every SBZ_GIF)
 #endif
+#ifndef SBZ_GPIPE
+#define SBZ_GPIPE 0  // dense kernel: software-pipelined gather groups of SBZ_GIF reads
+#endif
 #ifndef SBZ_OBS_X4
 #define SBZ_OBS_X4 0  // dense kernel: observations as 16-B loads (4 words of 4 sites per lane)
 #endif
@@ -657,18 +660,44 @@ __global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArg
         if (SBZ_ABLATE & 1 || !live) {
             // padding feature (or diagnostic build): no gathers
         } else if (!wide) {
+            auto cell_at = [&](int i) {  // cell i = 4k + j of the lane
+                const int k = i >> 2, j = i & 3;
+                const uint32_t bw = base2[2 * k + (j >> 1)];
+                const uint32_t bs = (SBZ_ABLATE & 16) ? 0u : (j & 1) ? (bw >> 16) : (bw & 0xffffu);
+                const uint32_t xb = (ob[k] >> (8 * j)) & 0xffu;
+                return (XS8 && PH && SBZ_ASM_ADDR && !(SBZ_ABLATE & 16)) ? cell_addr(bw, ob[k], j)
+                                                                         : bs + (XS8 ? xb : (xb << 3));
+            };
+            if (SBZ_GPIPE) {
+                // software-pipelined gathers: the reads of group g + 1 are issued before the
+                // products of group g, so 2 * SBZ_GIF reads are in flight
+                constexpr int GQ = SBZ_GIF < SPL ? SBZ_GIF : SPL, NG = SPL / GQ;
+                double va[GQ], vb[GQ];
 #pragma unroll
-            for (int k = 0; k < NO; k++)
+                for (int q = 0; q < GQ; q++) va[q] = t.at(cell_at(q));
 #pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const uint32_t bw = base2[2 * k + (j >> 1)];
-                    const uint32_t bs = (SBZ_ABLATE & 16) ? 0u : (j & 1) ? (bw >> 16) : (bw & 0xffffu);
-                    const uint32_t xb = (ob[k] >> (8 * j)) & 0xffu;
-                    m[k & 3] *= t.at((XS8 && PH && SBZ_ASM_ADDR && !(SBZ_ABLATE & 16))
-                                         ? cell_addr(bw, ob[k], j) : bs + (XS8 ? xb : (xb << 3)));
-                    // <= SBZ_GIF reads in flight
-                    if (j == 3 && (k & (SBZ_GIF / 4 - 1)) == SBZ_GIF / 4 - 1) __builtin_amdgcn_sched_barrier(0);
+                for (int g = 0; g < NG; g++) {
+                    if (g + 1 < NG) {
+#pragma unroll
+                        for (int q = 0; q < GQ; q++) vb[q] = t.at(cell_at((g + 1) * GQ + q));
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int q = 0; q < GQ; q++) m[((g * GQ + q) >> 2) & 3] *= va[q];
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int q = 0; q < GQ; q++) va[q] = vb[q];
                 }
+            } else {
+#pragma unroll
+                for (int k = 0; k < NO; k++)
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        m[k & 3] *= t.at(cell_at(4 * k + j));
+                        // <= SBZ_GIF reads in flight
+                        if (j == 3 && (k & (SBZ_GIF / 4 - 1)) == SBZ_GIF / 4 - 1) __builtin_amdgcn_sched_barrier(0);
+                    }
+            }
             if (!PH || SBZ_RN == 1 || (f - fa) % SBZ_RN == SBZ_RN - 1) flush();
         } else {
             // untamed inputs: renormalise after every factor (exact for any normal double)
