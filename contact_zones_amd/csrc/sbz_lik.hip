@@ -184,6 +184,15 @@ __device__ __forceinline__ void store_nw(double *nw, int lane, double w0r, doubl
 #ifndef SBZ_GIF
 #define SBZ_GIF 16  // dense kernel: table reads in flight per wave (scheduling barrier every SBZ_GIF)
 #endif
+#ifndef SBZ_PAIR
+// dense kernel, packed layout (experiment): tables of two features built back to back into two
+// 4-KiB LDS tables, then both features gathered together (one build phase and twice the
+// independent reads per pair)
+#define SBZ_PAIR 0
+#endif
+#ifndef SBZ_PAIR_ASM
+#define SBZ_PAIR_ASM 1
+#endif
 #ifndef SBZ_GPIPE
 #define SBZ_GPIPE 0  // dense kernel: software-pipelined gather groups of SBZ_GIF reads
 #endif
@@ -293,6 +302,8 @@ struct MixTable {
     // features per normalised-weight batch: 16 in the banked layout, so that 12 tasks per CU
     // (3 waves per SIMD) fit the 160 KiB of LDS at the bench shape
     static constexpr int NWCT = BK ? 16 : NWC;
+    static constexpr bool PRT = SBZ_PAIR && PH && !BK && !DB;  // two 512-double tables
+    int tbo = 0;  // PRT: doubles from `tab` to the table being built
     // SLOT >= 0: this wave loads and builds only zone-class slot SLOT (i = SLOT of the ZR
     // slots); the wave-specialised kernel splits the table between two builder waves this way.
     static constexpr bool has(int i) { return SLOT < 0 || i == SLOT; }
@@ -338,7 +349,7 @@ struct MixTable {
         // LDS: non-DB  [table | junk | nwt] from the dynamic base;
         //      DB      two static tables (tab0, tab1), [junk | nwt] from the dynamic base
         tab = DB ? tab0 : reinterpret_cast<double *>(lds);
-        double *dyn = DB ? reinterpret_cast<double *>(lds) : tab + (ncls + 1) * S1;
+        double *dyn = DB ? reinterpret_cast<double *>(lds) : tab + (PRT ? 1024 : (ncls + 1) * S1);
         junk = dyn + lane;
         // nwt 16-B aligned (one 8-B pad slot in the LDS budget)
         nwt = dyn + WAVE + (DB ? 0 : (((ncls + 1) * S1) & 1));
@@ -374,6 +385,7 @@ struct MixTable {
             for (int q = lane; q < (BK ? bk_lines(Z, FamC, S1) * 32 : (ncls + 1) * S1); q += WAVE) tab[q] = 0.5;
         for (int x = lane; x < S1; x += WAVE) {  // neutral row (both buffers)
             tab[(BK ? FamC * 32 : ncls * S1) + x] = 1.0;
+            if (PRT) tab[512 + ncls * S1 + x] = 1.0;
             if (DB) tab1[ncls * S1 + x] = 1.0;
         }
     }
@@ -525,7 +537,7 @@ struct MixTable {
         // DB: no fences — a wave's LDS operations complete in issue order, and the buffer being
         // written was last read by the gathers of feature f - 1, issued earlier.
         if (!DB) lds_phase();
-        double *const tb = DB ? dbtab : tab;
+        double *const tb = DB ? dbtab : tab + (PRT ? tbo : 0);
         const double l0 = PH ? r.g + naone : na ? 1.0 : r.g;
         const double nad = PH ? naone : na ? 1.0 : 0.0;  // l2 of a class without family
 #pragma unroll
@@ -716,6 +728,54 @@ __global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArg
         if (SBZ_LIK_STAMP) cyc[3] += lik_stamp() - t3;
     };
 
+    constexpr bool PR = SBZ_PAIR && PH && !BK && NS == 2;
+    // PR: features f (table at 0) and f + 1 (table at 4096 B) with P[0] / O[0] and P[1] / O[1]
+    auto feature_pair = [&](int f, int c0) {
+        const int fk0 = min(f, fb - 1), fk1 = min(f + 1, fb - 1);
+        if (fk0 < t.nwf0 || fk0 >= t.nwf0 + t.NWCT) t.prep(fk0, fb);
+        t.tbo = 0;
+        const bool wa = t.build(P[0], fk0) || force;
+        if (fk1 < t.nwf0 || fk1 >= t.nwf0 + t.NWCT) t.prep(fk1, fb);
+        t.tbo = 512;
+        const bool wb = t.build(P[1], fk1) || force;
+        __builtin_amdgcn_sched_barrier(0);
+        t.load(min(f + 2, fb - 1), P[0]);
+        t.load(min(f + 3, fb - 1), P[1]);
+        const bool live1 = f + 1 < fb;
+        auto addr = [&](const uint32_t (&ob)[NO], int i) {
+            const int k = i >> 2, j = i & 3;
+            const uint32_t bw = base2[2 * k + (j >> 1)];
+            if (SBZ_PAIR_ASM) return cell_addr(bw, ob[k], j);
+            return ((j & 1) ? (bw >> 16) : (bw & 0xffffu)) + ((ob[k] >> (8 * j)) & 0xffu);
+        };
+        if (!wa && !wb) {
+#pragma unroll
+            for (int i = 0; i < SPL; i++) {
+                m[(i >> 2) & 3] *= t.at(addr(O[0], i));
+                if (live1) m[(i >> 2) & 3] *= t.at(addr(O[1], i) + 4096u);
+                if ((i & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+            }
+            if (SBZ_RN <= 2 || ((f - fa) >> 1) % (SBZ_RN / 2) == SBZ_RN / 2 - 1) flush();
+        } else {
+            flush();
+#pragma unroll
+            for (int i = 0; i < SPL; i++) {
+                m[0] *= t.at(addr(O[0], i));
+                if (wa) renorm(m[0], e);
+            }
+            if (live1) {
+#pragma unroll
+                for (int i = 0; i < SPL; i++) {
+                    m[1] *= t.at(addr(O[1], i) + 4096u);
+                    if (wb) renorm(m[1], e);
+                }
+            }
+            flush();
+        }
+        load_obs(min(f + 2, fb - 1), c0, O[0]);
+        load_obs(min(f + 3, fb - 1), c0, O[1]);
+    };
+
   for (;;) {
     m[0] = m[1] = m[2] = m[3] = 1.0;
     e = 0;
@@ -743,7 +803,7 @@ __global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArg
                 zs[4 * k + 3] = zb[(uint32_t)pv[k].w];
             }
 #pragma unroll
-            for (int j = 0; j < NS - 1; j++) {
+            for (int j = 0; j < (PR ? NS : NS - 1); j++) {
                 t.load(min(fa + j, fb - 1), P[j]);
                 load_obs(min(fa + j, fb - 1), c0, O[j]);
             }
@@ -762,10 +822,14 @@ __global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArg
             }
         }
         if (SBZ_LIK_STAMP) cyc[4] += lik_stamp() - ts;
-        for (int f = fa; f < fb; f += NS) {
+        if (PR) {
+            for (int f = fa; f < fb; f += 2) feature_pair(f, c0);
+        } else {
+            for (int f = fa; f < fb; f += NS) {
 #pragma unroll
-            for (int j = 0; j < NS; j++)
-                feature(f + j, c0, f + j < fb, P[j], O[j], P[(j + NS - 1) % NS], O[(j + NS - 1) % NS]);
+                for (int j = 0; j < NS; j++)
+                    feature(f + j, c0, f + j < fb, P[j], O[j], P[(j + NS - 1) % NS], O[(j + NS - 1) % NS]);
+            }
         }
     }
     if (PH) flush();
@@ -2034,6 +2098,7 @@ size_t mix_lds_bytes(const sbz_dims &d, int C, bool bk = false) {
     if (bk)  // the lines hold the table, the neutral row and the junk slots
         return ((size_t)bk_lines(d.n_zones, (int)Fam + 1, (int)S1) * 32 + (size_t)16 * NW_PER_F) * 8;
     const size_t ncls = (size_t)(d.n_zones + 1) * (Fam + 1);
+    if (SBZ_PAIR) return (1024 + WAVE + 1 + (size_t)NWC * NW_PER_F) * 8;  // (experiment: tables <= 4 KiB)
     return ((ncls + 1) * S1 + WAVE + 1 + (size_t)NWC * NW_PER_F) * 8;
 }
 
