@@ -156,6 +156,7 @@ int sbz_open(int device, const sbz_dims *dims, const int8_t *obs, const uint8_t 
         ctx->lik_kernel = strcmp(v, "zoned") == 0 ? 2 : strcmp(v, "db") == 0 ? 3 : strcmp(v, "ws") == 0 ? 4
                         : strcmp(v, "zd") == 0 ? 5 : 1;
     if (const char *v = getenv("SBZ_LIK_BANKED")) ctx->lik_banked = atoi(v) != 0;
+    if (const char *v = getenv("SBZ_SRC_RC")) ctx->src_rc = atoi(v) != 0;
     if (const char *v = getenv("SBZ_WS_NG")) ctx->ws_ng = std::min(2, std::max(1, atoi(v)));
     if (const char *v = getenv("SBZ_WS_NB")) ctx->ws_nb = std::min(2, std::max(1, atoi(v)));
     if (const char *v = getenv("SBZ_SRC_HBM")) ctx->src_hbm = atoi(v) != 0;

@@ -54,6 +54,14 @@ __device__ __forceinline__ void renorm(double &m, int &e) {
     e += ex;
 }
 
+// m * 2^e *= v exactly for any v (denormal v too): v is split into its mantissa and exponent
+// first, then the product renormalised (the per-factor paths of untamed inputs)
+__device__ __forceinline__ void mul_exact(double &m, int &e, double v) {
+    e += __builtin_amdgcn_frexp_exp(v);
+    m *= __builtin_amdgcn_frexp_mant(v);
+    renorm(m, e);
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
@@ -721,8 +729,7 @@ __global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArg
                     const uint32_t bw = base2[2 * k + (j >> 1)];
                     const uint32_t bs = (j & 1) ? (bw >> 16) : (bw & 0xffffu);
                     const uint32_t xb = (ob[k] >> (8 * j)) & 0xffu;
-                    m[0] *= t.at((XS8 && PH && SBZ_ASM_ADDR) ? cell_addr(bw, ob[k], j) : bs + (XS8 ? xb : (xb << 3)));
-                    renorm(m[0], e);
+                    mul_exact(m[0], e, t.at((XS8 && PH && SBZ_ASM_ADDR) ? cell_addr(bw, ob[k], j) : bs + (XS8 ? xb : (xb << 3))));
                 }
         }
         if (SBZ_LIK_STAMP) cyc[3] += lik_stamp() - t3;
@@ -1864,8 +1871,8 @@ __global__ __launch_bounds__(WAVE) void lik_source_kernel(LikArgs a) {
                     const uint32_t rr = (c < (uint32_t)C) ? r : (uint32_t)rz;
                     const int addr = NW_BYTES + (int)rr * row_bytes +
                                      (int)(((o[k] >> (8 * j)) & 0xff) << shift);
-                    m *= *reinterpret_cast<const double *>(lds + addr);
-                    if (wide) renorm(m, e);
+                    if (wide) mul_exact(m, e, *reinterpret_cast<const double *>(lds + addr));
+                    else m *= *reinterpret_cast<const double *>(lds + addr);
                 }
                 if (k & 1) renorm(m, e);
             }
@@ -1878,13 +1885,240 @@ __global__ __launch_bounds__(WAVE) void lik_source_kernel(LikArgs a) {
     finish_chain(a, b, tot);
 }
 
+// ---------------------------------------------------------------------------------------
+// Source kernel, table form (lik_source_rc_kernel; the default where it applies).  Same rows as
+// lik_source_kernel (T0[h] 0..3, T1[z][hf] from 4, T2[fam][hz] from 4 + 2Z, the zero row rz, the
+// neutral row rn), but the repack writes each cell's ROW INDEX (its source byte mapped through
+// the chain's zone and the site's family, repack_source_kernel with `rows`), so a cell costs one
+// multiply-add for its address, one ds_read_b64 and one v_mul_f64.  Per feature each lane loads
+// (buffer loads, scalar per-feature offsets, one feature ahead) p_global[x], the p_zones rows
+// lg, lg + G and the p_families rows lg, lg + G of its state x = lane % S1 (NA lanes read
+// out of range: 0, plus `naone` = 1), and writes T0[lg] (lg < 4), the two T1 rows of each zone
+// and the two T2 rows of each family.  Normalised weights come from per-batch LDS (prep).  Inputs
+// are checked as in the dense kernel (one unsigned max; products checked when renormalised, the
+// task re-run per factor when one left the normal range, e.g. a zero weight's -inf cell).
+// ---------------------------------------------------------------------------------------
+constexpr int SRC_NWC = 32;  // features per normalised-weight batch
+template <int C, int SPL, bool XS8>
+__global__ __launch_bounds__(WAVE, 3) void lik_source_rc_kernel(LikArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    constexpr int NO = SPL / 4;
+    const int lane = threadIdx.x;
+    const int b = blockIdx.y;
+    const int fa = blockIdx.x * a.fpw;
+    const int fb = min(a.F, fa + a.fpw);
+    if (fa >= fb) {
+        finish_chain(a, b, 0.0);
+        return;
+    }
+    const int S = a.S, S1 = a.S + 1, Z = a.Z;
+    const int Fam = (C == 3) ? a.Fam : 0;
+    const int off1 = 4, off2 = 4 + 2 * Z, rz = off2 + 2 * Fam, rn = rz + 1;
+    const int row_bytes = S1 * 8;
+    double *tab = reinterpret_cast<double *>(lds);
+    double *nwt = tab + ((((rn + 1) * S1) + 1) & ~1);  // [SRC_NWC][8], 16-B aligned
+    double *junk = nwt + SRC_NWC * 8 + lane;
+
+    const int G = WAVE / S1, lx = lane % S1, lg = lane / S1;
+    const bool na = lx == S, act = lane < G * S1;
+    const uint32_t lxc = (uint32_t)min(lx, S - 1);
+    const uint32_t zfs = (uint32_t)(a.F * S);
+    const double naone = na ? 1.0 : 0.0;
+    constexpr uint32_t OOB = 0x80000000u;
+    const double *pgb = a.pg + (size_t)b * zfs;
+    const double *zbase = Z > 0 ? a.pz + (size_t)b * Z * zfs : pgb;
+    const double *fbase = Fam > 0 ? a.pf + (size_t)b * Fam * zfs : pgb;
+    const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(pgb), (short)0, (int)(zfs * 8u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rzr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(zbase), (short)0,
+                                                                         (int)((uint32_t)max(Z, 1) * zfs * 8u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rf = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(fbase), (short)0,
+                                                                        (int)((uint32_t)max(Fam, 1) * zfs * 8u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t robs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(a.obs_fm), (short)0,
+                                                                          a.F * a.Np, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t *>(a.src_fm + (size_t)b * a.F * a.Np), (short)0, a.F * a.Np, 0x00020000);
+    // lane offsets (bytes) of its parameter rows; rows past Z / Fam read a valid row (unused)
+    const uint32_t vg = na ? OOB : lxc * 8u;
+    uint32_t vz[2], vf[2];
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+        vz[i] = na ? OOB : ((uint32_t)min(lg + G * i, max(Z - 1, 0)) * zfs + lxc) * 8u;
+        vf[i] = na ? OOB : ((uint32_t)min(lg + G * i, max(Fam - 1, 0)) * zfs + lxc) * 8u;
+    }
+    struct SrcParams {
+        double g, z[2], fm[2];
+    };
+    auto load = [&](int f, SrcParams &r) {
+        const int so = f * S * 8;
+        r.g = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rg, (int)vg, so, 0));
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            r.z[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rzr, (int)vz[i], so, 0));
+            r.fm[i] = C == 3 ? __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rf, (int)vf[i], so, 0)) : 0.0;
+        }
+    };
+    auto load_words = [&](const __amdgpu_buffer_rsrc_t &rs, int f, int c0, uint32_t (&o)[NO]) {
+#pragma unroll
+        for (int k = 0; k < NO; k++) o[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, lane * 4, f * a.Np + c0 + 256 * k, 0);
+    };
+
+    for (int x = lane; x < S1; x += WAVE) {
+        tab[rz * S1 + x] = 0.0;  // a component the site lacks: weight 0
+        tab[rn * S1 + x] = 1.0;  // padding positions
+    }
+    // normalised weights of features f0 .. f0 + SRC_NWC: [k][q], q = h (w_norm[h][0]), 4 / 5 =
+    // w_norm[1 / 3][1], 6 / 7 = w_norm[2 / 3][2]; lane 2k + hp computes feature k's h = 2hp + hz
+    int nwf0 = -(1 << 30);
+    uint64_t nwbad = 0;
+    const double *wb = a.w + (size_t)b * a.F * C;
+    auto prep = [&](int f0) {
+        const int k = lane >> 1, hp = lane & 1;
+        const uint32_t f = (uint32_t)min(f0 + k, fb - 1);
+        const double w0r = wb[f * C], w1r = wb[f * C + 1], w2r = C == 3 ? wb[f * C + 2] : 0.0;
+        int ok = 1;
+        double n[2][3];
+#pragma unroll
+        for (int hz = 0; hz < 2; hz++) {
+            const double w0 = w0r * 1.0, w1 = w1r * (hz ? 1.0 : 0.0);
+            double sum = w0 + w1, w2 = 0.0;
+            if (C == 3) {
+                w2 = w2r * (hp ? 1.0 : 0.0);
+                sum = sum + w2;
+            }
+            n[hz][0] = w0 / sum;
+            n[hz][1] = w1 / sum;
+            n[hz][2] = C == 3 ? w2 / sum : 0.0;
+            ok &= (int)tame(n[hz][0]) & (int)tame(n[hz][1]) & (int)tame(n[hz][2]);
+        }
+        wave_lds_sync();  // earlier features' reads of nwt are done
+        double *o = nwt + k * 8;
+        o[2 * hp] = n[0][0];      // h = 2hp
+        o[2 * hp + 1] = n[1][0];  // h = 2hp + 1
+        o[4 + hp] = n[1][1];      // h = 1 / 3
+        if (hp) {
+            o[6] = n[0][2];       // h = 2
+            o[7] = n[1][2];       // h = 3
+        }
+        nwbad = __ballot(!ok);
+        nwf0 = f0;
+        wave_lds_sync();
+    };
+    // the table of feature f; returns `wide`
+    auto build = [&](const SrcParams &r, int f) -> bool {
+        const int k = f - nwf0;
+        uint32_t hmx = max(hiword(r.g), max(hiword(r.z[0]), hiword(r.z[1])));
+        if (C == 3) hmx = max(hmx, max(hiword(r.fm[0]), hiword(r.fm[1])));
+        const bool wide = ((nwbad >> (2 * k)) & 3ull) != 0 || __ballot(hmx > 0x3FF00000u) != 0;
+        const double *q = nwt + k * 8;
+        const double wh = q[min(lg, 3)], wz0 = q[4], wz1 = q[5], wf0 = q[6], wf1 = q[7];
+        wave_lds_sync();  // the previous feature's gathers are done with the table
+        const double l0 = r.g + naone;
+        double *t0 = (act && lg < 4) ? tab + lg * S1 + lx : junk;
+        *t0 = wh * l0;
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            const int zr = lg + G * i;
+            const double l1 = r.z[i] + naone;
+            double *tz = (act && zr < Z) ? tab + (off1 + 2 * zr) * S1 + lx : junk;
+            const int sz = (act && zr < Z) ? S1 : 0;
+            tz[0] = wz0 * l1;
+            tz[sz] = wz1 * l1;
+            if (C == 3) {
+                const double l2 = r.fm[i] + naone;
+                double *tf = (act && zr < Fam) ? tab + (off2 + 2 * zr) * S1 + lx : junk;
+                const int sf = (act && zr < Fam) ? S1 : 0;
+                tf[0] = wf0 * l2;
+                tf[sf] = wf1 * l2;
+            }
+        }
+        wave_lds_sync();
+        return wide;
+    };
+
+    double m[4];
+    int e;
+    uint64_t under;
+    bool force = false;
+    SrcParams P[2];
+    uint32_t O[2][NO], R[2][NO];
+    auto flush = [&]() {
+        const double mn = fmin(fmin(m[0], m[1]), fmin(m[2], m[3]));
+        under |= __ballot(!(mn >= 0x1p-1022));
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            if (q < NO) renorm(m[q], e);
+    };
+    auto feature = [&](int f, int c0, bool live, const SrcParams &cur, const uint32_t (&ob)[NO],
+                       const uint32_t (&rb)[NO], SrcParams &fill, uint32_t (&ofill)[NO], uint32_t (&rfill)[NO]) {
+        const int fk = min(f, fb - 1);
+        if (fk < nwf0 || fk >= nwf0 + SRC_NWC) prep(fk);
+        const bool wide = build(cur, fk) || force;
+        __builtin_amdgcn_sched_barrier(0);
+        const int fn = min(f + 1, fb - 1);
+        load(fn, fill);
+        load_words(robs, fn, c0, ofill);
+        load_words(rsrc, fn, c0, rfill);
+        if (!live) return;
+        auto addr = [&](int k, int j) {
+            const uint32_t xb = (ob[k] >> (8 * j)) & 0xffu;
+            const uint32_t rr = (rb[k] >> (8 * j)) & 0xffu;
+            return rr * (uint32_t)row_bytes + (XS8 ? xb : (xb << 3));
+        };
+        if (!wide) {
+#pragma unroll
+            for (int k = 0; k < NO; k++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    m[k & 3] *= *reinterpret_cast<const double *>(lds + addr(k, j));
+                    if (j == 3 && (k & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+                }
+            if ((f - fa) % SBZ_RN == SBZ_RN - 1) flush();
+        } else {
+            flush();
+#pragma unroll
+            for (int k = 0; k < NO; k++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    mul_exact(m[0], e, *reinterpret_cast<const double *>(lds + addr(k, j)));
+                }
+        }
+    };
+
+    for (;;) {
+        m[0] = m[1] = m[2] = m[3] = 1.0;
+        e = 0;
+        under = 0;
+        for (int c0 = 0; c0 < a.Np; c0 += SPL * WAVE) {
+            load(fa, P[0]);
+            load_words(robs, fa, c0, O[0]);
+            load_words(rsrc, fa, c0, R[0]);
+            for (int f = fa; f < fb; f += 2) {
+                feature(f, c0, true, P[0], O[0], R[0], P[1], O[1], R[1]);
+                feature(f + 1, c0, f + 1 < fb, P[1], O[1], R[1], P[0], O[0], R[0]);
+            }
+        }
+        flush();
+        if (force || under == 0) break;
+        force = true;  // uniform: `under` is a ballot
+    }
+    const double v = (log(m[0]) + log(m[1])) + (log(m[2]) + log(m[3])) + (double)e * LN2;
+    finish_chain(a, b, wave_sum(v));
+}
+
 // Row-major source [B][N][F] -> feature-major [B][F][Np] in the family-sorted site order
 // (padded sites -> component 0).  One workgroup transposes a tile of 64 positions x 64 features
 // through LDS: each site's 64 feature bytes are read as one contiguous run (4-byte words when F
 // is a multiple of 4), each feature's 64 position bytes written as 16-byte stores.
 constexpr int RP_T = 64;
+// With `zone` (lik_source_rc_kernel) each byte is the cell's table row instead: the source
+// component c mapped through the chain's zone of the site and its family class (rows as in
+// lik_source_rc_kernel; a component the site lacks, or c >= C -> the zero row; padding -> the
+// neutral row).
 __global__ __launch_bounds__(256) void repack_source_kernel(int N, int F, int Np, const int *perm,
-                                                            const uint8_t *src, uint8_t *dst) {
+                                                            const uint8_t *src, uint8_t *dst,
+                                                            const uint8_t *zone = nullptr,
+                                                            const uint8_t *famc = nullptr, int Z = 0,
+                                                            int Fam = 0, int C = 3) {
     __shared__ uint8_t tile[RP_T][RP_T + 4];  // [position][feature]
     const int tid = threadIdx.x;
     const int p0 = blockIdx.x * RP_T, f0 = blockIdx.y * RP_T;
@@ -1894,6 +2128,23 @@ __global__ __launch_bounds__(256) void repack_source_kernel(int N, int F, int Np
         const int p = p0 + r;
         const int fq = f0 + 16 * q;
         uint8_t v[16];
+        // row map of this position: byte c = table row of component c (c = 3: c >= C)
+        const int off2 = 4 + 2 * Z, rz = off2 + 2 * Fam, rn = rz + 1;
+        uint32_t map = 0;
+        if (zone) {
+            if (p < N) {
+                const int z = zone[b * N + perm[p]];
+                const bool hz = z < Z;
+                const int fc = (C == 3) ? famc[p] : 0;
+                const bool hf = fc > 0;
+                const uint32_t r0 = (hz ? 1u : 0u) | (hf ? 2u : 0u);
+                const uint32_t r1 = hz ? (uint32_t)(4 + 2 * z + (hf ? 1 : 0)) : (uint32_t)rz;
+                const uint32_t r2 = (C == 3 && hf) ? (uint32_t)(off2 + 2 * (fc - 1) + (hz ? 1 : 0)) : (uint32_t)rz;
+                map = r0 | (r1 << 8) | (r2 << 16) | ((uint32_t)rz << 24);
+            } else {
+                map = (uint32_t)rn * 0x01010101u;
+            }
+        }
         if (p < N) {
             const uint8_t *row = src + (b * N + perm[p]) * F;
             if ((F & 3) == 0 && fq + 16 <= F) {
@@ -1911,6 +2162,10 @@ __global__ __launch_bounds__(256) void repack_source_kernel(int N, int F, int Np
         } else {
 #pragma unroll
             for (int j = 0; j < 16; j++) v[j] = 0;
+        }
+        if (zone) {
+#pragma unroll
+            for (int j = 0; j < 16; j++) v[j] = (uint8_t)(map >> (8 * min((int)v[j], 3)));
         }
 #pragma unroll
         for (int j = 0; j < 16; j++) tile[r][16 * q + j] = v[j];
@@ -2076,8 +2331,45 @@ void configure_zd(std::vector<const void *> &v) {
     }
 }
 
+// lik_source_rc_kernel applies: G = 64 / S1 lanes groups cover 2G zone and family rows, row
+// indices are bytes
+bool source_rc_applies(const sbz_dims &d, int C) {
+    const int S1 = d.n_states + 1;
+    if (S1 > WAVE) return false;
+    const int G = WAVE / S1;
+    const int Fam = C == 3 ? d.n_families : 0;
+    return d.n_zones <= 2 * G && Fam <= 2 * G && 4 + 2 * d.n_zones + 2 * Fam + 1 < 256;
+}
+size_t source_rc_lds_bytes(const sbz_dims &d, int C) {
+    const size_t S1 = (size_t)d.n_states + 1;
+    const size_t Fam = C == 3 ? (size_t)d.n_families : 0;
+    const size_t rows = 4 + 2 * (size_t)d.n_zones + 2 * Fam + 2;
+    return ((((rows * S1) + 1) & ~(size_t)1) + (size_t)SRC_NWC * 8 + WAVE) * 8;
+}
+template <int C>
+const void *source_rc_kernel(int spl, bool xs8) {
+    if (xs8) {
+        switch (spl) {
+            case 4: return reinterpret_cast<const void *>(&lik_source_rc_kernel<C, 4, true>);
+            case 8: return reinterpret_cast<const void *>(&lik_source_rc_kernel<C, 8, true>);
+            case 16: return reinterpret_cast<const void *>(&lik_source_rc_kernel<C, 16, true>);
+            default: return reinterpret_cast<const void *>(&lik_source_rc_kernel<C, 32, true>);
+        }
+    }
+    switch (spl) {
+        case 4: return reinterpret_cast<const void *>(&lik_source_rc_kernel<C, 4, false>);
+        case 8: return reinterpret_cast<const void *>(&lik_source_rc_kernel<C, 8, false>);
+        case 16: return reinterpret_cast<const void *>(&lik_source_rc_kernel<C, 16, false>);
+        default: return reinterpret_cast<const void *>(&lik_source_rc_kernel<C, 32, false>);
+    }
+}
+
 template <int C>
 void configure_source(std::vector<const void *> &v) {
+    for (int spl = 4; spl <= 32; spl *= 2) {
+        v.push_back(source_rc_kernel<C>(spl, true));
+        v.push_back(source_rc_kernel<C>(spl, false));
+    }
     v.push_back(reinterpret_cast<const void *>(&lik_source_kernel<C, 4>));
     v.push_back(reinterpret_cast<const void *>(&lik_source_kernel<C, 8>));
     v.push_back(reinterpret_cast<const void *>(&lik_source_kernel<C, 16>));
@@ -2203,7 +2495,7 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
     }
 
     MixPlan plan;
-    bool zoned = false, ws = false, zd = false;
+    bool zoned = false, ws = false, zd = false, src_rc = false;
     int block = WAVE;
     const void *mix_fn = nullptr;
     size_t lds = 0;
@@ -2269,12 +2561,28 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
             }
         }
     } else {
-        lds = lik_lds_bytes(d, true);
+        src_rc = ctx->src_rc && source_rc_applies(d, ctx->C) &&
+                 source_rc_lds_bytes(d, ctx->C) <= 64 * 1024;
+        lds = src_rc ? source_rc_lds_bytes(d, ctx->C) : lik_lds_bytes(d, true);
         if (lds > 64 * 1024)
             return fail(ctx, SBZ_EINVAL, "source-mode table needs " + std::to_string(lds) +
                                              " B of LDS per wave (> 64 KiB)");
+        if (src_rc) {
+            // one resident round of single-wave tasks, as the dense mixture kernel
+            mix_fn = ctx->C == 3 ? source_rc_kernel<3>(ctx->spl, ctx->xs8 != 0)
+                                 : source_rc_kernel<2>(ctx->spl, ctx->xs8 != 0);
+            if (ctx->mix_occ == 0 || ctx->mix_occ_fn != mix_fn) {
+                int occ = 0;
+                hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, mix_fn, WAVE, lds);
+                ctx->mix_occ = (e == hipSuccess && occ > 0) ? occ : 8;
+                ctx->mix_occ_fn = mix_fn;
+            }
+            const int per_cu = ctx->tasks_per_cu > 0 ? ctx->tasks_per_cu : ctx->mix_occ;
+            const int W = std::max(1, std::min((F + 1) / 2, (ctx->n_cu * per_cu + B - 1) / B));
+            a.fpw = (F + W - 1) / W;
+        }
     }
-    if (src_mode || !plan.fr) {
+    if ((src_mode && !src_rc) || (!src_mode && !plan.fr)) {
         // one wave per (chain, feature range): enough tasks to fill 256 CUs x 32 waves
         int W = std::max(1, std::min(F, (256 * 32 + B - 1) / B));
         a.fpw = (F + W - 1) / W;
@@ -2298,8 +2606,13 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
         rc = ensure(ctx, ctx->src_t, bytes);
         if (rc) return rc;
         const dim3 rgrid(ctx->Np / RP_T, (F + RP_T - 1) / RP_T, B);
-        repack_source_kernel<<<rgrid, 256, 0, ctx->stream>>>(d.n_sites, F, ctx->Np, ctx->d_perm, source,
-                                                            static_cast<uint8_t *>(ctx->src_t.ptr));
+        if (src_rc)  // row codes for lik_source_rc_kernel
+            repack_source_kernel<<<rgrid, 256, 0, ctx->stream>>>(
+                d.n_sites, F, ctx->Np, ctx->d_perm, source, static_cast<uint8_t *>(ctx->src_t.ptr), zone,
+                ctx->d_famc, d.n_zones, ctx->C == 3 ? d.n_families : 0, ctx->C);
+        else
+            repack_source_kernel<<<rgrid, 256, 0, ctx->stream>>>(d.n_sites, F, ctx->Np, ctx->d_perm, source,
+                                                                static_cast<uint8_t *>(ctx->src_t.ptr));
         a.src_fm = static_cast<const uint8_t *>(ctx->src_t.ptr);
     }
 
@@ -2311,7 +2624,11 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
         (void)hipMemsetAsync(ctx->ticket.ptr, 0, ctx->ticket.bytes, st);
         return hip_fail(ctx, e, what);
     };
-    if (src_mode) {
+    if (src_rc) {
+        void *args[] = {&a};
+        hipError_t e = hipLaunchKernel(mix_fn, grid, dim3(WAVE), args, lds, st);
+        if (e != hipSuccess) return launch_failed(e, "source kernel launch");
+    } else if (src_mode) {
         if (ctx->C == 3) launch_source<3>(ctx->spl, grid, lds, st, a);
         else launch_source<2>(ctx->spl, grid, lds, st, a);
     } else if (!plan.fr) {

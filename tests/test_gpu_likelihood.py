@@ -40,12 +40,17 @@ def _assert_close(got, ref, tol=REL_TOL):
 # kernel, "zd" = zone-sparse direct kernel (no class table) (SBZ_LIK_KERNEL and SBZ_WS_NG are
 # read when a context opens).
 MODES = [("mixture", "dense"), ("mixture", "db"), ("mixture", "ws"), ("mixture", "ws1"),
-         ("mixture", "zoned"), ("mixture", "zd"), ("source", "dense")]
+         ("mixture", "zoned"), ("mixture", "zd"), ("source", "dense"), ("source", "src_select")]
 
 
 @pytest.fixture
 def lik_kernel(request, monkeypatch):
     kernel = request.param
+    # "src_select": the source branch with the per-cell component select (lik_source_kernel)
+    # instead of the row-code table kernel (lik_source_rc_kernel, the default)
+    monkeypatch.setenv("SBZ_SRC_RC", "0" if kernel == "src_select" else "1")
+    if kernel == "src_select":
+        kernel = "dense"
     if kernel.startswith("ws"):
         monkeypatch.setenv("SBZ_WS_NG", "1" if kernel == "ws1" else "2")
         kernel = "ws"
@@ -253,6 +258,41 @@ def test_dense_edge_paths(gpu_available, monkeypatch, banked, shape):
     assert np.isfinite(ref[3]) and ref[4] == -np.inf
     _assert_close(got, ref, tol=1e-12)
     assert eng.lds_bytes(False) > 0
+
+
+@pytest.mark.parametrize("rc", ["1", "0"])
+@pytest.mark.parametrize("shape", [(2000, 64, 10, 8, 4, 8), (300, 21, 15, 3, 2, 8), (120, 30, 4, 0, 3, 8)])
+def test_source_edge_paths(gpu_available, monkeypatch, rc, shape):
+    """Source branch (row-code table kernel and the per-cell select kernel): a selected component
+    of weight 0 (-inf, model.py:181-182), tiny parameters (products underflow -> task re-run),
+    parameters above 1, denormal family parameters, sources past the site's components."""
+    from contact_zones_amd.likelihood import LikelihoodEngine
+    from oracle import oracle_c
+    monkeypatch.setenv("SBZ_SRC_RC", rc)
+    N, F, S, Z, Fam, B = shape
+    rng = np.random.default_rng(N * 3 + F)
+    obs, fam, zos, w, pg, pz, pf, src = _random_batch(rng, N, F, S, Z, Fam, B, True, max(1, N // (3 * max(Z, 1))))
+    w[3, 5, 1] = 0.0                    # zone weight 0 where a zoned site selects the zone
+    if Z:
+        s3 = int(np.flatnonzero(zos[3] != 255)[0])
+        src[3, s3, 5] = 1
+    else:
+        # family weight 0 where a site with a family selects its family (a zero global weight
+        # would make the no-family sites' weights 0 / 0 = NaN: the reference then still returns
+        # -inf from its any(weight == 0) test, the kernels NaN; DESIGN.md §3.3)
+        w[3, 5, 2] = 0.0
+        src[3, int(np.flatnonzero(fam != 255)[0]), 5] = 2
+    pg[4, :, 1] = 1e-200                # tiny
+    pg[5, 3:9] *= 7.5                   # above 1
+    pf[6, :, 2, :] = 4e-320             # denormal family parameters
+    src[7, :, 0] = 0                    # every site from the global component at feature 0
+    s2 = int(np.flatnonzero(fam == 255)[0])
+    src[2, s2, 1] = 2                   # a site without family selects the family component
+    eng = LikelihoodEngine(obs, fam, S, Z, Fam, True)
+    got = eng.loglik(zos, w, pg, pz, pf, src)
+    ref = oracle_c.loglik_batch(obs, fam, zos, w, pg, pz, pf, source=src, inheritance=True)
+    assert ref[3] == -np.inf and ref[2] == -np.inf
+    _assert_close(got, ref, tol=1e-12)
 
 
 @pytest.mark.parametrize("nofam,Fam,inh", [(0.0, 4, True), (1.0, 4, True), (0.3, 4, True),
