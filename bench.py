@@ -49,6 +49,8 @@ def parse():
     p.add_argument("--mh-steps", type=int, default=50000,
                    help="sampler leg: timed MH steps per chain (0 disables the leg)")
     p.add_argument("--mh-burnin", type=int, default=200000, help="sampler leg: untimed MH steps")
+    p.add_argument("--source-lik-steps", type=int, default=20,
+                   help="source-branch likelihood leg: timed launches (0: off)")
     p.add_argument("--src-steps", type=int, default=2000,
                    help="real-data sampler legs (the reference's Balkan / South America configs, "
                         "SAMPLE_SOURCE = true): timed MH steps (0 = skip)")
@@ -467,6 +469,50 @@ def _all_reduce(t, op):
     t.copy_(h)
 
 
+def source_lik_leg(args, eng, gen, dev, stream, rank, world):
+    """The source branch of the likelihood (model.py:177-184) on the same
+    workload: every cell's component drawn among those the site has, B chains, full evaluation
+    (repack + lik_source_rc_kernel), timed with HIP events on the engine's stream."""
+    import copy
+    import torch
+    import torch.distributed as dist
+    a = copy.copy(args)
+    a.mode = "source"
+    B, K = args.chains, args.source_lik_steps
+    pool = [make_chains_torch(a, B, gen, dev) for _ in range(2)]
+    out = torch.empty(2, B, dtype=torch.float64, device=dev)
+
+    def step(i):
+        c = pool[i % 2]
+        eng.loglik_device(B, c["zos"].data_ptr(), c["w"].data_ptr(), c["pg"].data_ptr(),
+                          c["pz"].data_ptr(), c["pf"].data_ptr() if c["pf"] is not None else 0,
+                          c["src"].data_ptr(), out[i % 2].data_ptr(), validate=False)
+    for i in range(3):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    for i in range(K):
+        step(i)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    t = torch.tensor([ev0.elapsed_time(ev1) / 1e3], dtype=torch.float64, device=dev)
+    if world > 1:
+        _all_reduce(t, dist.ReduceOp.MAX)
+    secs = float(t[0])
+    P, D, per_launch = algorithmic_bytes(a, B, True)
+    launch_s = secs / K
+    del pool
+    return {"evals_per_sec": B * K * world / secs, "launch_us": launch_s * 1e6,
+            "bytes_per_eval": P + D / B, "bytes_per_launch": per_launch,
+            "achieved_GBs": per_launch / launch_s / 1e9,
+            "frac": per_launch / launch_s / 1e9 / HBM_PEAK_GBS, "steps": K,
+            "kernels": "repack_source_kernel (row codes) + lik_source_rc_kernel"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -550,6 +596,11 @@ def main():
     achieved = per_launch / launch_s / 1e9
 
     traffic, traffic_src = pmc_traffic(args, B)
+    src_leg = None
+    if args.source_lik_steps > 0 and not src_mode:
+        del pool
+        torch.cuda.empty_cache()
+        src_leg = source_lik_leg(args, eng, gen, dev, stream, rank, world)
     sampler = None
     if args.mh_steps > 0 and args.mode == "mixture" and args.families > 0:
         sampler = sampler_leg(args, eng, obs, fam, dev, rank, world, stream)
@@ -602,6 +653,8 @@ def main():
             },
             "device_time_s": ev_max,
         }
+        if src_leg is not None:
+            line["likelihood_source_branch"] = src_leg
         if sampler is not None:
             line["sampler"] = sampler
         if real is not None:
