@@ -13,7 +13,7 @@ run timeout -k 10 500 python bench.py --steps 200 --warmup 20 > gpurun_out/bench
 tail -c 400 gpurun_out/bench.json
 run timeout -k 10 500 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 200 --warmup 20 --cpu-seconds 0 > gpurun_out/prof.log 2>&1
 find gpurun_out/prof -name "*kernel_stats.csv" -exec head -5 {} \;
-run timeout -k 10 900 bash tools/pmc.sh --mh-steps 0 --src-steps 0 > gpurun_out/pmc.log 2>&1
+run timeout -k 10 900 bash tools/pmc.sh --mh-steps 0 --src-steps 0 --source-lik-steps 0 > gpurun_out/pmc.log 2>&1
 tail -3 gpurun_out/pmc.log
 SBZ_DIST_BACKEND=gloo run timeout -k 10 400 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29631 bench.py --gpus 2 --steps 50 --warmup 5 --cpu-seconds 0 --mh-steps 2000 --mh-burnin 2000 --src-steps 200 --src-burnin 200 > gpurun_out/bench_2rank.json 2> gpurun_out/bench_2rank.err
 tail -c 300 gpurun_out/bench_2rank.json
