@@ -204,6 +204,9 @@ __device__ __forceinline__ void store_nw(double *nw, int lane, double w0r, doubl
 #ifndef SBZ_GPIPE
 #define SBZ_GPIPE 0  // dense kernel: software-pipelined gather groups of SBZ_GIF reads
 #endif
+#ifndef SBZ_NCH
+#define SBZ_NCH 4  // dense kernel: independent product chains per lane (4 or 8)
+#endif
 #ifndef SBZ_OBS_X4
 #define SBZ_OBS_X4 0  // dense kernel: observations as 16-B loads (4 words of 4 sites per lane)
 #endif
@@ -603,6 +606,7 @@ __global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArg
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     constexpr int NO = SPL / 4;  // observation words (4 sites each) per lane per feature
     constexpr bool PH = SBZ_TAME != 0;
+    constexpr int NCH = (SBZ_NCH == 8 && NO >= 8) ? 8 : 4;
     const int lane = threadIdx.x;
     const int b = blockIdx.y;
     const int fa = blockIdx.x * a.fpw;
@@ -634,7 +638,7 @@ __global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArg
         }
     };
 
-    double m[4];  // four independent product chains
+    double m[NCH];  // independent product chains (SBZ_NCH)
     int e;
     // PH: a lane's product fell below 2^-1022 (a zero or tiny cell): the wave re-runs the task
     // with per-factor renormalisation (`force`), which is exact for any normal double.
@@ -650,11 +654,13 @@ __global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArg
     // the normal range is still below it here.  Then renormalise.
     auto flush = [&]() {
         if (PH) {
-            const double mn = fmin(fmin(m[0], m[1]), fmin(m[2], m[3]));
+            double mn = fmin(fmin(m[0], m[1]), fmin(m[2], m[3]));
+#pragma unroll
+            for (int q = 4; q < NCH; q++) mn = fmin(mn, m[q]);
             under |= __ballot(!(mn >= 0x1p-1022));
         }
 #pragma unroll
-        for (int q = 0; q < 4; q++)
+        for (int q = 0; q < NCH; q++)
             if (q < NO) renorm(m[q], e);
     };
 
@@ -703,7 +709,7 @@ __global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArg
                     }
                     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                    for (int q = 0; q < GQ; q++) m[((g * GQ + q) >> 2) & 3] *= va[q];
+                    for (int q = 0; q < GQ; q++) m[((g * GQ + q) >> 2) & (NCH - 1)] *= va[q];
                     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                     for (int q = 0; q < GQ; q++) va[q] = vb[q];
@@ -713,7 +719,7 @@ __global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArg
                 for (int k = 0; k < NO; k++)
 #pragma unroll
                     for (int j = 0; j < 4; j++) {
-                        m[k & 3] *= t.at(cell_at(4 * k + j));
+                        m[k & (NCH - 1)] *= t.at(cell_at(4 * k + j));
                         // <= SBZ_GIF reads in flight
                         if (j == 3 && (k & (SBZ_GIF / 4 - 1)) == SBZ_GIF / 4 - 1) __builtin_amdgcn_sched_barrier(0);
                     }
@@ -784,7 +790,7 @@ __global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArg
     };
 
   for (;;) {
-    m[0] = m[1] = m[2] = m[3] = 1.0;
+    for (int q = 0; q < NCH; q++) m[q] = 1.0;
     e = 0;
     under = 0;
     for (int c0 = 0; c0 < a.Np; c0 += SPL * WAVE) {
@@ -844,6 +850,8 @@ __global__ __launch_bounds__(WAVE, SBZ_MIX_WAVES) void lik_mixture_kernel(LikArg
     force = true;  // uniform: `under` is a ballot
   }
     double v = (log(m[0]) + log(m[1])) + (log(m[2]) + log(m[3]));
+#pragma unroll
+    for (int q = 4; q < NCH; q++) v = v + log(m[q]);
     v = v + (double)e * LN2;
     double tot = wave_sum(v);
     if (SBZ_LIK_STAMP) {
