@@ -85,7 +85,9 @@ size_t mh_src_lds_bytes(const sbz_dims &d, int C, bool hbm_sources, bool geo) {
     return MH_SRC_MAX_WAVES * 2 * (8 + 4) + cnt * 4 + ((Z + 1) & ~(size_t)1) * 4 + MH_STAT_INTS * 4 +
            ((N + 1) & ~(size_t)1) * 2 +
            (hbm_sources ? 0 : ((N * F + 15) & ~(size_t)15) * 2) + ((N + 15) & ~(size_t)15) +
-           ((F + 15) & ~(size_t)15) + (geo ? 16 + geo_scratch_bytes((int)N) : 0);
+           ((F + 15) & ~(size_t)15) + (geo ? 16 + geo_scratch_bytes((int)N) : 0) +
+           // redraw_rows: draws [F][S] doubles, per-feature tape offsets and counter ranks [F] ints
+           16 + F * S * 8 + 2 * F * 4 + 8;
 }
 
 namespace {
@@ -130,6 +132,12 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     int *geo_cnt = reinterpret_cast<int *>(geo_mem + ((N + 7) & ~7));
     double *geo_rd = reinterpret_cast<double *>(geo_cnt + 4);
     int *geo_ri = reinterpret_cast<int *>(geo_rd + 16);
+    // redraw_rows scratch, 16-B aligned after the geo scratch
+    const size_t par_off = (geo_off + (a.geo_cost ? geo_scratch_bytes(N) : 0) + 15) & ~(size_t)15;
+    double *gbuf = reinterpret_cast<double *>(lds + par_off);  // [F][S] draws
+    int *fpre = reinterpret_cast<int *>(gbuf + (size_t)F * S);  // [F] tape offset of feature f
+    int *frank = fpre + F;                                      // [F] counter rank of feature f
+    int *misc_i = frank + F;                                    // [2] totals of those scans
 
     uint8_t *gzos = ch.zone_of_site + (size_t)b * N;
     uint8_t *gsrc = ch.source + (size_t)b * NF;
@@ -371,41 +379,81 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     auto redraw_rows = [&](double *base, const double *gc, double gc_default, const double *al,
                            const double *tape, int64_t len, uint32_t key0, uint32_t key1,
                            uint64_t chain, int64_t &pos, uint64_t &ctr, int &bad) -> double {
-        double dp = 0.0;
-        for (int f = 0; f < F; f++) {
-            if (!sub[f]) continue;
-            const int n = a.app_cnt[f];
-            if (f % NW == wv) {
-                double *row = base + (size_t)f * S;
-                const int x = lane < n ? a.app_list[(size_t)f * S + lane] : 0;
-                double g = 0.0;
-                if (tape) {
-                    const bool have = pos + n <= len;
-                    g = (lane < n && have) ? tape[pos + lane] : 0.0;
-                    bad |= have ? 0 : 1;
-                } else {
-                    LaneRng lr;
-                    lr.initk(key0, key1, chain, ctr, lane);
-                    const double alpha = (gc ? ldp(gc + (size_t)f * S + x) : gc_default) + (double)cnt[f * S + x];
-                    g = lane < n ? lr.gamma(alpha) : 0.0;
-                    const double tot = uni(wave_sum(g));
-                    g = g / tot;
+        // every (feature, state) draw at once: thread t <-> (f, j) = (t / S, t % S).  Feature f's
+        // draws are its tape values pos + fpre[f] + j, or the gammas of lane stream j at counter
+        // ctr + frank[f] (LaneRng, as one wave per feature drew them), fpre / frank the exclusive
+        // scans over the subset features (wave 0, 64 features at a time).
+        if (wv == 0) {
+            int cn = 0, cr = 0;
+            for (int f0 = 0; f0 < F; f0 += WAVE) {
+                const int f = f0 + lane;
+                const int in = f < F && sub[f];
+                int v = in ? a.app_cnt[f] : 0;
+#pragma unroll
+                for (int o = 1; o < WAVE; o <<= 1) {
+                    const int t = __shfl_up(v, o, WAVE);
+                    if (lane >= o) v += t;
                 }
-                if (lane < n) {
-                    const double old = ldp(row + x);
-                    stp(row + x, g);
-                    if (al) {
-                        const double am1 = ldp(al + (size_t)f * S + x) - 1.0;
-                        dp += xlogy(am1, g) - xlogy(am1, old);
-                    }
+                const uint64_t m = __ballot(in);
+                if (f < F) {
+                    fpre[f] = cn + v - (in ? a.app_cnt[f] : 0);
+                    frank[f] = cr + lane_prefix(m);
+                }
+                cn += uni(__shfl(v, WAVE - 1, WAVE));
+                cr += __popcll(m);
+            }
+            if (lane == 0) {
+                misc_i[0] = cn;
+                misc_i[1] = cr;
+            }
+        }
+        sync();
+        const int tot_n = uni(misc_i[0]), tot_r = uni(misc_i[1]);
+        const int64_t pos0 = pos;
+        const uint64_t ctr0 = ctr;
+        const bool have = !tape || pos0 + tot_n <= len;
+        const int FS = F * S;
+        for (int t = tid; t < FS; t += NT) {
+            const int f = t / S, j = t - f * S;
+            const bool act = sub[f] && j < a.app_cnt[f];
+            double g = 0.0;
+            if (act) {
+                if (tape) {
+                    g = have ? tape[pos0 + fpre[f] + j] : 0.0;
+                } else {
+                    const int x = a.app_list[(size_t)f * S + j];
+                    LaneRng lr;
+                    lr.initk(key0, key1, chain, ctr0 + (uint64_t)frank[f], j);
+                    const double alpha = (gc ? ldp(gc + (size_t)f * S + x) : gc_default) + (double)cnt[f * S + x];
+                    g = lr.gamma(alpha);
                 }
             }
-            if (tape) pos = pos + n;
-            else ctr++;
+            gbuf[t] = g;
         }
-        bad = bor(bad);
-        pos = uni64(pos);
-        ctr = (uint64_t)uni64((int64_t)ctr);
+        sync();
+        double dp = 0.0;
+        for (int t = tid; t < FS; t += NT) {
+            const int f = t / S, j = t - f * S;
+            const int n = a.app_cnt[f];
+            if (!(sub[f] && j < n)) continue;
+            double g = gbuf[t];
+            if (!tape) {
+                double tot = 0.0;
+                for (int i = 0; i < n; i++) tot += gbuf[f * S + i];
+                g = g / tot;
+            }
+            const int x = a.app_list[(size_t)f * S + j];
+            double *row = base + (size_t)f * S;
+            const double old = ldp(row + x);
+            stp(row + x, g);
+            if (al) {
+                const double am1 = ldp(al + (size_t)f * S + x) - 1.0;
+                dp += xlogy(am1, g) - xlogy(am1, old);
+            }
+        }
+        bad = have ? 0 : 1;
+        pos = uni64(pos0 + (tape ? tot_n : 0));
+        ctr = (uint64_t)uni64((int64_t)(ctr0 + (tape ? 0 : (uint64_t)tot_r)));
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         return bsum(dp);
     };
