@@ -283,22 +283,39 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     };
 
     // ---- passes over the N*F observations (cell c = s*F + f, C order)
+    // Sums of logs as one log per thread: each factor's mantissa multiplies a product and its
+    // exponent adds to an integer (exact for any factor, denormals included), the product is
+    // renormalised every 8 cells, and log(m) + e ln 2 is taken once (~1e-16 relative).
+    struct LogAcc {
+        double m = 1.0;
+        int e = 0, k = 0;
+        __device__ __forceinline__ void add(double v) {
+            e += __builtin_amdgcn_frexp_exp(v);
+            m *= __builtin_amdgcn_frexp_mant(v);
+            if (++k == 8) {
+                k = 0;
+                e += __builtin_amdgcn_frexp_exp(m);
+                m = __builtin_amdgcn_frexp_mant(m);
+            }
+        }
+        __device__ __forceinline__ double value() const { return log(m) + (double)e * LN2; }
+    };
     // sum over observations of log posterior[src] for the current sample (zone_sampling.py:718-722)
     auto pass_logq = [&]() -> double {
-        double acc = 0.0;
+        LogAcc acc;
         for (int c = tid; c < NF; c += NT) {
             const int s = c / F, f = c - s * F;
             double l[3], wn[3], p[3];
             obs_terms<C>(a, w, pg, pz, pf, s, f, zos[s], C == 3 ? a.fam_site[s] : 0, l, wn);
             posterior_draw<C>(l, wn, 2.0, p);
-            acc += log(p[rsrc(src, c)]);
+            acc.add(p[rsrc(src, c)]);
         }
-        return bsum(acc);
+        return bsum(acc.value());
     };
     // log-likelihood of the current sample with sources `sv` (combine_lh source branch,
     // model.py:177-184): sum log(w_src * lh_src), -inf if a selected weight is 0
     auto pass_ll = [&](const uint8_t *sv) -> double {
-        double acc = 0.0;
+        LogAcc acc;
         int zero_w = 0;
         for (int c = tid; c < NF; c += NT) {
             const int s = c / F, f = c - s * F;
@@ -306,9 +323,9 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             obs_terms<C>(a, w, pg, pz, pf, s, f, zos[s], C == 3 ? a.fam_site[s] : 0, l, wn);
             const int k = rsrc(sv, c);
             zero_w |= wn[k] == 0.0;
-            acc += log(wn[k] * l[k]);
+            acc.add(wn[k] * l[k]);
         }
-        const double v = bsum(acc);
+        const double v = bsum(acc.value());
         return bor(zero_w) ? -INFINITY : v;
     };
     // redraw every source from the current sample's posterior into srcb; returns log q (sum log
@@ -316,7 +333,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     auto pass_resample = [&](double &log_q_s, double &ll_new) {
         LaneRng lr;
         lr.initw(rng, tid);
-        double acc_q = 0.0, acc_l = 0.0;
+        LogAcc acc_q, acc_l;
         int zero_w = 0;
         const int64_t pos0 = rng.pos;
         const bool have = !rng.tape || pos0 + NF <= rng.len;
@@ -327,9 +344,9 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             const double u = rng.tape ? (have ? rng.tape[pos0 + c] : 0.0) : lr.u();
             const int k = posterior_draw<C>(l, wn, u, p);
             wsrc(srcb, c, k);
-            acc_q += log(p[k]);
+            acc_q.add(p[k]);
             zero_w |= wn[k] == 0.0;
-            acc_l += log(wn[k] * l[k]);
+            acc_l.add(wn[k] * l[k]);
         }
         if (rng.tape) {
             if (!have) rng.bad = 1;
@@ -337,8 +354,8 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         } else {
             rng.ctr++;
         }
-        log_q_s = bsum(acc_q);
-        const double v = bsum(acc_l);
+        log_q_s = bsum(acc_q.value());
+        const double v = bsum(acc_l.value());
         ll_new = bor(zero_w) ? -INFINITY : v;
     };
     auto commit_sources = [&]() {
