@@ -157,6 +157,7 @@ int sbz_open(int device, const sbz_dims *dims, const int8_t *obs, const uint8_t 
                         : strcmp(v, "zd") == 0 ? 5 : 1;
     if (const char *v = getenv("SBZ_LIK_BANKED")) ctx->lik_banked = atoi(v) != 0;
     if (const char *v = getenv("SBZ_SRC_RC")) ctx->src_rc = atoi(v) != 0;
+    if (const char *v = getenv("SBZ_SRC_STAGE")) ctx->src_stage = atoi(v) != 0;
     if (const char *v = getenv("SBZ_WS_NG")) ctx->ws_ng = std::min(2, std::max(1, atoi(v)));
     if (const char *v = getenv("SBZ_WS_NB")) ctx->ws_nb = std::min(2, std::max(1, atoi(v)));
     if (const char *v = getenv("SBZ_SRC_HBM")) ctx->src_hbm = atoi(v) != 0;

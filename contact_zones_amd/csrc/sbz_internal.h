@@ -80,7 +80,8 @@ struct sbz_ctx {
                            // 4 wave-specialised builder + gatherers ("ws", same condition),
                            // 5 zone-sparse direct ("zd")
     int lik_banked = 1;
-    int src_rc = 1;        // SBZ_SRC_RC=0: source-mode likelihood with the per-cell component select    // SBZ_LIK_BANKED=0: dense kernel with the packed [class][x] table
+    int src_rc = 1;
+    int src_stage = 1;     // SBZ_SRC_STAGE=0: source-mode sampler passes read parameters from L2        // SBZ_SRC_RC=0: source-mode likelihood with the per-cell component select    // SBZ_LIK_BANKED=0: dense kernel with the packed [class][x] table
     int ws_ng = 2;         // SBZ_WS_NG: gatherer waves of the wave-specialised kernel (1 or 2)
     int ws_nb = 2;         // SBZ_WS_NB: its builder waves (1 or 2; 2 split the zone-class slots)
     const void *mix_occ_fn = nullptr;  // the kernel mix_occ was queried for

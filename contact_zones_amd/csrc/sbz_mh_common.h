@@ -382,6 +382,7 @@ struct Chain {
 struct MhArgs {
     int N, F, S, Z, Fam, C, FamC, Np, xs8;
     int n_steps, nops, min_size, warmup;
+    int stage;  // mh_src_kernel: parameters and normalised weights staged in LDS for the N*F passes
     double op_cdf[SBZ_N_OPS];
     double prec[4];
     const uint8_t *obs_fm;      // [F][Np] by position
@@ -503,7 +504,7 @@ constexpr int MH_SRC_MAX_WAVES = 16;         // waves per chain of the source-mo
 
 // SAMPLE_SOURCE = true sampler (sbz_mh_src.hip): LDS bytes per chain (sources in LDS, or in
 // HBM: hbm_sources) and the launch.
-size_t mh_src_lds_bytes(const sbz_dims &d, int C, bool hbm_sources = false, bool geo = false);
+size_t mh_src_lds_bytes(const sbz_dims &d, int C, bool hbm_sources = false, bool geo = false, bool stage = false);
 int launch_mh_source(sbz_ctx *ctx, int B, const MhArgs &a);
 
 }  // namespace sbz

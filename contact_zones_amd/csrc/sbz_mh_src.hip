@@ -79,7 +79,7 @@ __device__ __forceinline__ int posterior_draw(const double (&l)[3], const double
 
 }  // namespace
 
-size_t mh_src_lds_bytes(const sbz_dims &d, int C, bool hbm_sources, bool geo) {
+size_t mh_src_lds_bytes(const sbz_dims &d, int C, bool hbm_sources, bool geo, bool stage) {
     const size_t N = d.n_sites, F = d.n_features, S = d.n_states, Z = d.n_zones;
     const size_t cnt = F * (S > (size_t)C ? S : (size_t)C);
     return MH_SRC_MAX_WAVES * 2 * (8 + 4) + cnt * 4 + ((Z + 1) & ~(size_t)1) * 4 + MH_STAT_INTS * 4 +
@@ -87,7 +87,9 @@ size_t mh_src_lds_bytes(const sbz_dims &d, int C, bool hbm_sources, bool geo) {
            (hbm_sources ? 0 : ((N * F + 15) & ~(size_t)15) * 2) + ((N + 15) & ~(size_t)15) +
            ((F + 15) & ~(size_t)15) + (geo ? 16 + geo_scratch_bytes((int)N) : 0) +
            // redraw_rows: draws [F][S] doubles, per-feature tape offsets and counter ranks [F] ints
-           16 + F * S * 8 + 2 * F * 4 + 8;
+           16 + F * S * 8 + 2 * F * 4 + 8 +
+           // staged parameters: normalised weights [F][4][3], p_global, p_zones, p_families
+           (stage ? 16 + (12 * F + (1 + Z + (C == 3 ? (size_t)d.n_families : 0)) * F * S) * 8 : 0);
 }
 
 namespace {
@@ -138,6 +140,15 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     int *fpre = reinterpret_cast<int *>(gbuf + (size_t)F * S);  // [F] tape offset of feature f
     int *frank = fpre + F;                                      // [F] counter rank of feature f
     int *misc_i = frank + F;                                    // [2] totals of those scans
+    // a.stage: the N*F passes read the chain's parameters and normalised weights from LDS copies
+    // (staged when a pass starts after the parameters changed) instead of L2
+    const size_t stg_off = ((size_t)(reinterpret_cast<unsigned char *>(misc_i + 2) - lds) + 15) & ~(size_t)15;
+    double *lnw = reinterpret_cast<double *>(lds + stg_off);  // [F][4][3] by h = hz | hf << 1
+    double *lpg = lnw + (size_t)F * 12;                        // [F][S]
+    double *lpz = lpg + (size_t)F * S;                         // [Z][F][S]
+    double *lpf = lpz + (size_t)Z * F * S;                     // [Fam][F][S]
+    const bool stg = a.stage != 0;
+    bool stg_ok = false;
 
     uint8_t *gzos = ch.zone_of_site + (size_t)b * N;
     uint8_t *gsrc = ch.source + (size_t)b * NF;
@@ -282,6 +293,52 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         return uni(found);
     };
 
+    // normalize_weights (model.py:436-452) of feature f's weights for the 4 classes h = hz | hf << 1
+    auto stage_nw = [&](int f, double w0r, double w1r, double w2r) {
+#pragma unroll
+        for (int h = 0; h < 4; h++) {
+            const double w0 = w0r * 1.0, w1 = w1r * ((h & 1) ? 1.0 : 0.0);
+            double sum = w0 + w1, w2 = 0.0;
+            if (C == 3) {
+                w2 = w2r * ((h & 2) ? 1.0 : 0.0);
+                sum = sum + w2;
+            }
+            lnw[(f * 4 + h) * 3] = w0 / sum;
+            lnw[(f * 4 + h) * 3 + 1] = w1 / sum;
+            lnw[(f * 4 + h) * 3 + 2] = C == 3 ? w2 / sum : 0.0;
+        }
+    };
+    auto ensure_staged = [&]() {
+        if (!stg || stg_ok) return;
+        const int fs = F * S;
+        for (int i = tid; i < fs; i += NT) lpg[i] = ldp(pg + i);
+        for (int i = tid; i < Z * fs; i += NT) lpz[i] = ldp(pz + i);
+        if (C == 3)
+            for (int i = tid; i < Fam * fs; i += NT) lpf[i] = ldp(pf + i);
+        for (int f = tid; f < F; f += NT)
+            stage_nw(f, ldp(w + (size_t)f * C), ldp(w + (size_t)f * C + 1), C == 3 ? ldp(w + (size_t)f * C + 2) : 0.0);
+        sync();
+        stg_ok = true;
+    };
+    // obs_terms from the staged copies (the same values, the same operations)
+    auto terms = [&](int s, int f, double (&l)[3], double (&wn)[3]) {
+        const int zc = zos[s], fc = C == 3 ? a.fam_site[s] : 0;
+        if (!stg) {
+            obs_terms<C>(a, w, pg, pz, pf, s, f, zc, fc, l, wn);
+            return;
+        }
+        const int x = a.obs_sm[(size_t)s * F + f];
+        const bool na = x >= S;
+        const int xc = na ? 0 : x;
+        const bool hz = zc < Z, hf = (C == 3) && fc > 0;
+        const double *q = lnw + ((size_t)f * 4 + (hz ? 1 : 0) + (hf ? 2 : 0)) * 3;
+        wn[0] = q[0];
+        wn[1] = q[1];
+        wn[2] = q[2];
+        l[0] = na ? 1.0 : lpg[f * S + xc];
+        l[1] = na ? 1.0 : (hz ? lpz[(zc * F + f) * S + xc] : 0.0);
+        l[2] = (C == 3) ? (na ? 1.0 : (hf ? lpf[((fc - 1) * F + f) * S + xc] : 0.0)) : 0.0;
+    };
     // ---- passes over the N*F observations (cell c = s*F + f, C order)
     // Sums of logs as one log per thread: each factor's mantissa multiplies a product and its
     // exponent adds to an integer (exact for any factor, denormals included), the product is
@@ -302,11 +359,12 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     };
     // sum over observations of log posterior[src] for the current sample (zone_sampling.py:718-722)
     auto pass_logq = [&]() -> double {
+        ensure_staged();
         LogAcc acc;
         for (int c = tid; c < NF; c += NT) {
             const int s = c / F, f = c - s * F;
             double l[3], wn[3], p[3];
-            obs_terms<C>(a, w, pg, pz, pf, s, f, zos[s], C == 3 ? a.fam_site[s] : 0, l, wn);
+            terms(s, f, l, wn);
             posterior_draw<C>(l, wn, 2.0, p);
             acc.add(p[rsrc(src, c)]);
         }
@@ -315,12 +373,13 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     // log-likelihood of the current sample with sources `sv` (combine_lh source branch,
     // model.py:177-184): sum log(w_src * lh_src), -inf if a selected weight is 0
     auto pass_ll = [&](const uint8_t *sv) -> double {
+        ensure_staged();
         LogAcc acc;
         int zero_w = 0;
         for (int c = tid; c < NF; c += NT) {
             const int s = c / F, f = c - s * F;
             double l[3], wn[3];
-            obs_terms<C>(a, w, pg, pz, pf, s, f, zos[s], C == 3 ? a.fam_site[s] : 0, l, wn);
+            terms(s, f, l, wn);
             const int k = rsrc(sv, c);
             zero_w |= wn[k] == 0.0;
             acc.add(wn[k] * l[k]);
@@ -331,6 +390,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     // redraw every source from the current sample's posterior into srcb; returns log q (sum log
     // posterior[new source]) and the new log-likelihood
     auto pass_resample = [&](double &log_q_s, double &ll_new) {
+        ensure_staged();
         LaneRng lr;
         lr.initw(rng, tid);
         LogAcc acc_q, acc_l;
@@ -340,7 +400,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         for (int c = tid; c < NF; c += NT) {
             const int s = c / F, f = c - s * F;
             double l[3], wn[3], p[3];
-            obs_terms<C>(a, w, pg, pz, pf, s, f, zos[s], C == 3 ? a.fam_site[s] : 0, l, wn);
+            terms(s, f, l, wn);
             const double u = rng.tape ? (have ? rng.tape[pos0 + c] : 0.0) : lr.u();
             const int k = posterior_draw<C>(l, wn, u, p);
             wsrc(srcb, c, k);
@@ -393,7 +453,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     // if al != null.
     // (the generator's fields come in as values and go out through pos / ctr / bad: the lambda
     // does not touch `rng`, which keeps it in registers)
-    auto redraw_rows = [&](double *base, const double *gc, double gc_default, const double *al,
+    auto redraw_rows = [&](double *base, double *lbase, const double *gc, double gc_default, const double *al,
                            const double *tape, int64_t len, uint32_t key0, uint32_t key1,
                            uint64_t chain, int64_t &pos, uint64_t &ctr, int &bad) -> double {
         // every (feature, state) draw at once: thread t <-> (f, j) = (t / S, t % S).  Feature f's
@@ -463,6 +523,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             double *row = base + (size_t)f * S;
             const double old = ldp(row + x);
             stp(row + x, g);
+            if (lbase) lbase[(size_t)f * S + x] = g;  // the staged copy follows
             if (al) {
                 const double am1 = ldp(al + (size_t)f * S + x) - 1.0;
                 dp += xlogy(am1, g) - xlogy(am1, old);
@@ -611,6 +672,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                     }
                     stp(wf, d0);
                     stp(wf + 1, d1);
+                    if (stg) stage_nw(f, d0, d1, 0.0);
                 } else {
                     const int cu = cnt[f * C], cx = cnt[f * C + (fixed == 0 ? 1 : 2)];
                     double r;
@@ -627,6 +689,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                     stp(wf, w0 / sum);
                     stp(wf + 1, w1 / sum);
                     stp(wf + 2, w2 / sum);
+                    if (stg) stage_nw(f, w0 / sum, w1 / sum, w2 / sum);
                 }
             }
             if (rng.tape) {
@@ -635,7 +698,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             } else {
                 rng.ctr++;
             }
-            gsync();  // the new weights are visible to every thread
+            gsync();  // the new weights are visible to every thread (and their staged forms)
             ll_new = pass_ll(src);
         } else {
             // ---- gibbs_sample_p_global / p_zones / p_families
@@ -669,12 +732,14 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             int64_t rpos = rng.pos;
             uint64_t rctr = rng.ctr;
             int rbad = 0;
-            dprior = redraw_rows(base, gc, 1.0, al, rng.tape, rng.len, rng.key0, rng.key1, rng.chain,
+            double *lbase = !stg ? nullptr : (comp == 0 ? lpg : (comp == 1 ? lpz + (size_t)row * F * S
+                                                                         : lpf + (size_t)row * F * S));
+            dprior = redraw_rows(base, lbase, gc, 1.0, al, rng.tape, rng.len, rng.key0, rng.key1, rng.chain,
                                  rpos, rctr, rbad);
             rng.pos = rpos;
             rng.ctr = rctr;
             if (rbad) rng.bad = 1;
-            gsync();  // the new rows are visible to every thread
+            gsync();  // the new rows are visible to every thread (and their staged copies)
             ll_new = pass_ll(src);
         }
 
@@ -764,8 +829,10 @@ int launch_mh_source(sbz_ctx *ctx, int B, const MhArgs &a0) {
     MhArgs a = a0;
     constexpr size_t LDS_MAX = 160 * 1024;
     const bool geo = a.geo_cost != nullptr;
-    const bool gs = ctx->src_hbm || mh_src_lds_bytes(ctx->d, ctx->C, false, geo) > LDS_MAX;  // do not fit: HBM
-    const size_t lds = mh_src_lds_bytes(ctx->d, ctx->C, gs, geo);
+    const bool gs = ctx->src_hbm || mh_src_lds_bytes(ctx->d, ctx->C, false, geo, false) > LDS_MAX;  // do not fit: HBM
+    // parameters staged in LDS when they fit too (SBZ_SRC_STAGE=0: off)
+    a.stage = ctx->src_stage && mh_src_lds_bytes(ctx->d, ctx->C, gs, geo, true) <= LDS_MAX ? 1 : 0;
+    const size_t lds = mh_src_lds_bytes(ctx->d, ctx->C, gs, geo, a.stage != 0);
     if (lds > LDS_MAX)
         return fail(ctx, SBZ_EINVAL, "SAMPLE_SOURCE sampler needs " + std::to_string(lds) +
                                          " B of LDS per chain even with the sources in HBM (> 160 KiB)");
