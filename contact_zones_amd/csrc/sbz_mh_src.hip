@@ -89,7 +89,7 @@ size_t mh_src_lds_bytes(const sbz_dims &d, int C, bool hbm_sources, bool geo, bo
            // redraw_rows: draws [F][S] doubles, per-feature tape offsets and counter ranks [F] ints
            16 + F * S * 8 + 2 * F * 4 + 8 +
            // staged parameters: normalised weights [F][4][3], p_global, p_zones, p_families
-           (stage ? 16 + (12 * F + (1 + Z + (C == 3 ? (size_t)d.n_families : 0)) * F * S) * 8 : 0);
+           (stage ? 16 + (12 * F + (1 + Z + (C == 3 ? (size_t)d.n_families : 0)) * F * S) * 8 + N * F : 0);
 }
 
 namespace {
@@ -147,6 +147,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     double *lpg = lnw + (size_t)F * 12;                        // [F][S]
     double *lpz = lpg + (size_t)F * S;                         // [Z][F][S]
     double *lpf = lpz + (size_t)Z * F * S;                     // [Fam][F][S]
+    uint8_t *lobs = reinterpret_cast<uint8_t *>(lpf + (size_t)Fam * F * S);  // [N][F] x by site
     const bool stg = a.stage != 0;
     bool stg_ok = false;
 
@@ -205,6 +206,8 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     const double p_grow = ch.p_grow_connected[b];
 
     for (int z = tid; z < Z; z += NT) zsize[z] = 0;
+    if (a.stage)  // the observations never change: staged once
+        for (int c = tid; c < NF; c += NT) lobs[c] = a.obs_sm[c];
     if (tid < MH_STAT_INTS) stat[tid] = 0;
     for (int s = tid; s < N; s += NT) nb[s] = 0;
     if (!GS)
@@ -327,7 +330,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             obs_terms<C>(a, w, pg, pz, pf, s, f, zc, fc, l, wn);
             return;
         }
-        const int x = a.obs_sm[(size_t)s * F + f];
+        const int x = lobs[s * F + f];
         const bool na = x >= S;
         const int xc = na ? 0 : x;
         const bool hz = zc < Z, hf = (C == 3) && fc > 0;
@@ -719,7 +722,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             clear_cnt();
             for (int c = tid; c < NF; c += NT) {
                 const int s = c / F, f = c - s * F;
-                const int x = a.obs_sm[c];
+                const int x = stg ? lobs[c] : a.obs_sm[c];
                 bool in = sub[f] && rsrc(src, c) == comp && x < S;
                 if (comp == 1) in = in && zos[s] == row;
                 if (comp == 2) in = in && a.fam_site[s] == row + 1;
