@@ -197,6 +197,9 @@ struct Rng {
 // 2^32; the host keeps global chain ids below 2^32 (c2).
 struct LaneRng {
     uint32_t k0, k1, base, c2, c3, j;
+    // one Philox block gives two uniforms (words 0-1 and 2-3): the second is kept for the next call
+    double spare;
+    int has_spare;  // set by init / initk
     __device__ __forceinline__ void init(const Rng &r, int lane) {
         k0 = r.key0;
         k1 = r.key1;
@@ -204,6 +207,7 @@ struct LaneRng {
         c2 = (uint32_t)r.chain;
         c3 = (uint32_t)(r.ctr >> 32) ^ ((uint32_t)(lane + 1) << 24);
         j = 0;
+        has_spare = 0;
     }
     // as init, from the key / chain / counter values themselves
     __device__ __forceinline__ void initk(uint32_t key0, uint32_t key1, uint64_t chain, uint64_t ctr,
@@ -214,6 +218,7 @@ struct LaneRng {
         c2 = (uint32_t)chain;
         c3 = (uint32_t)(ctr >> 32) ^ ((uint32_t)(lane + 1) << 24);
         j = 0;
+        has_spare = 0;
     }
     // a stream per thread of a multi-wave workgroup (id < 2048)
     __device__ __forceinline__ void initw(const Rng &r, int id) {
@@ -221,8 +226,14 @@ struct LaneRng {
         c3 = (uint32_t)(r.ctr >> 32) ^ ((uint32_t)(id + 1) << 20);
     }
     __device__ __forceinline__ double u() {
+        if (has_spare) {
+            has_spare = 0;
+            return spare;
+        }
         uint32_t c[4] = {j++, base, c2, c3};
         philox4x32_10(c, k0, k1);
+        spare = u53(c[2], c[3]);
+        has_spare = 1;
         return u53(c[0], c[1]);
     }
     __device__ __forceinline__ double normal() {
