@@ -2114,10 +2114,18 @@ __global__ __launch_bounds__(WAVE, 3) void lik_source_rc_kernel(LikArgs a) {
 }
 
 // Row-major source [B][N][F] -> feature-major [B][F][Np] in the family-sorted site order
-// (padded sites -> component 0).  One workgroup transposes a tile of 64 positions x 64 features
-// through LDS: each site's 64 feature bytes are read as one contiguous run (4-byte words when F
-// is a multiple of 4), each feature's 64 position bytes written as 16-byte stores.
-constexpr int RP_T = 64;
+// (padded sites -> component 0).  One workgroup transposes a tile of RP_T positions x RP_F
+// features through LDS.  Read side: RP_F / 16 lanes per site row, each loading 16 feature bytes
+// as 4-byte words (F a multiple of 4); every pass's loads are issued before the first is used.
+// Write side: 4 lanes per feature, each storing 16 position bytes per 64-position subtile.
+#ifndef SBZ_RP_T
+#define SBZ_RP_T 256
+#endif
+#ifndef SBZ_RP_F
+#define SBZ_RP_F 64
+#endif
+constexpr int RP_T = SBZ_RP_T;  // positions per workgroup (a multiple of 64)
+constexpr int RP_F = SBZ_RP_F;  // features per workgroup (a multiple of 16, RP_F / 16 divides 256)
 // With `zone` (lik_source_rc_kernel) each byte is the cell's table row instead: the source
 // component c mapped through the chain's zone of the site and its family class (rows as in
 // lik_source_rc_kernel; a component the site lacks, or c >= C -> the zero row; padding -> the
@@ -2127,23 +2135,57 @@ __global__ __launch_bounds__(256) void repack_source_kernel(int N, int F, int Np
                                                             const uint8_t *zone = nullptr,
                                                             const uint8_t *famc = nullptr, int Z = 0,
                                                             int Fam = 0, int C = 3) {
-    __shared__ uint8_t tile[RP_T][RP_T + 4];  // [position][feature]
+    constexpr int RW = RP_F / 4 + 1;  // words per LDS row (odd: the write side's 4 position
+                                      // groups fall in distinct banks)
+    constexpr int LR = RP_F / 16;     // lanes per site row
+    constexpr int RPP = 256 / LR;     // rows per pass
+    constexpr int NP = RP_T / RPP;    // passes
+    __shared__ uint32_t tile[RP_T][RW];  // [position][feature word]
     const int tid = threadIdx.x;
-    const int p0 = blockIdx.x * RP_T, f0 = blockIdx.y * RP_T;
+    const int p0 = blockIdx.x * RP_T, f0 = blockIdx.y * RP_F;
     const size_t b = blockIdx.z;
-    {
-        const int r = tid >> 2, q = tid & 3;  // row (position) r, 16 features from f0 + 16 q
-        const int p = p0 + r;
-        const int fq = f0 + 16 * q;
-        uint8_t v[16];
-        // row map of this position: byte c = table row of component c (c = 3: c >= C)
-        const int off2 = 4 + 2 * Z, rz = off2 + 2 * Fam, rn = rz + 1;
-        uint32_t map = 0;
+    const int l = tid % LR, rg = tid / LR;  // lane l of row group rg: features f0 + 16 l ..
+    const int fq = f0 + 16 * l;
+    const bool words = (F & 3) == 0 && fq + 16 <= F;
+    uint32_t w[NP][4];
+    int row[NP];
+#pragma unroll
+    for (int t = 0; t < NP; t++) {
+        const int p = p0 + RPP * t + rg;
+        row[t] = p < N ? perm[p] : -1;
+    }
+#pragma unroll
+    for (int t = 0; t < NP; t++) {
+        if (row[t] >= 0 && fq < F) {
+            const uint8_t *rp = src + (b * N + row[t]) * F;
+            if (words) {
+                const uint32_t *wp = reinterpret_cast<const uint32_t *>(rp + fq);
+#pragma unroll
+                for (int k = 0; k < 4; k++) w[t][k] = wp[k];
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    uint32_t x = 0;
+#pragma unroll
+                    for (int j = 0; j < 4; j++) x |= (fq + 4 * k + j < F ? (uint32_t)rp[fq + 4 * k + j] : 0u) << (8 * j);
+                    w[t][k] = x;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; k++) w[t][k] = 0;
+        }
+    }
+    const int off2 = 4 + 2 * Z, rz = off2 + 2 * Fam, rn = rz + 1;
+#pragma unroll
+    for (int t = 0; t < NP; t++) {
         if (zone) {
-            if (p < N) {
-                const int z = zone[b * N + perm[p]];
+            // row map of this position: byte c = table row of component c (c = 3: c >= C)
+            uint32_t map;
+            if (row[t] >= 0) {
+                const int z = zone[b * N + row[t]];
                 const bool hz = z < Z;
-                const int fc = (C == 3) ? famc[p] : 0;
+                const int fc = (C == 3) ? famc[p0 + RPP * t + rg] : 0;
                 const bool hf = fc > 0;
                 const uint32_t r0 = (hz ? 1u : 0u) | (hf ? 2u : 0u);
                 const uint32_t r1 = hz ? (uint32_t)(4 + 2 * z + (hf ? 1 : 0)) : (uint32_t)rz;
@@ -2152,47 +2194,40 @@ __global__ __launch_bounds__(256) void repack_source_kernel(int N, int F, int Np
             } else {
                 map = (uint32_t)rn * 0x01010101u;
             }
-        }
-        if (p < N) {
-            const uint8_t *row = src + (b * N + perm[p]) * F;
-            if ((F & 3) == 0 && fq + 16 <= F) {
-                const uint32_t *w = reinterpret_cast<const uint32_t *>(row + fq);
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const uint32_t x = w[k];
-#pragma unroll
-                    for (int j = 0; j < 4; j++) v[4 * k + j] = (uint8_t)(x >> (8 * j));
-                }
-            } else {
-#pragma unroll
-                for (int j = 0; j < 16; j++) v[j] = fq + j < F ? row[fq + j] : 0;
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < 16; j++) v[j] = 0;
-        }
-        if (zone) {
-#pragma unroll
-            for (int j = 0; j < 16; j++) v[j] = (uint8_t)(map >> (8 * min((int)v[j], 3)));
-        }
-#pragma unroll
-        for (int j = 0; j < 16; j++) tile[r][16 * q + j] = v[j];
-    }
-    __syncthreads();
-    {
-        const int fr = tid >> 2, q = tid & 3;  // feature f0 + fr, positions p0 + 16 q ..
-        const int f = f0 + fr;
-        if (f < F) {
-            uint32_t w[4];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 uint32_t x = 0;
 #pragma unroll
-                for (int j = 0; j < 4; j++) x |= (uint32_t)tile[16 * q + 4 * k + j][fr] << (8 * j);
-                w[k] = x;
+                for (int j = 0; j < 4; j++) {
+                    const uint32_t c = min((w[t][k] >> (8 * j)) & 0xffu, 3u);
+                    x |= ((map >> (8 * c)) & 0xffu) << (8 * j);
+                }
+                w[t][k] = x;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) tile[RPP * t + rg][4 * l + k] = w[t][k];
+    }
+    __syncthreads();
+    const uint8_t *tb = reinterpret_cast<const uint8_t *>(&tile[0][0]);
+    const int q = tid & 3;  // positions p0 + 64 t + 16 q .. of feature f0 + fr
+    for (int fr = tid >> 2; fr < RP_F; fr += 64) {
+        const int f = f0 + fr;
+        if (f >= F) break;
+        uint8_t *drow = dst + (b * F + f) * Np + p0 + 16 * q;
+#pragma unroll
+        for (int t = 0; t < RP_T / 64; t++) {
+            if (p0 + 64 * t >= Np) break;
+            uint32_t o[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                uint32_t x = 0;
+#pragma unroll
+                for (int j = 0; j < 4; j++) x |= (uint32_t)tb[(64 * t + 16 * q + 4 * k + j) * (RW * 4) + fr] << (8 * j);
+                o[k] = x;
             }
             // Np is a multiple of 64, so the 16 bytes are 16-byte aligned and inside the row
-            *reinterpret_cast<uint4 *>(dst + (b * F + f) * Np + p0 + 16 * q) = make_uint4(w[0], w[1], w[2], w[3]);
+            *reinterpret_cast<uint4 *>(drow + 64 * t) = make_uint4(o[0], o[1], o[2], o[3]);
         }
     }
 }
@@ -2613,7 +2648,7 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
         const size_t bytes = (size_t)B * F * ctx->Np;
         rc = ensure(ctx, ctx->src_t, bytes);
         if (rc) return rc;
-        const dim3 rgrid(ctx->Np / RP_T, (F + RP_T - 1) / RP_T, B);
+        const dim3 rgrid((ctx->Np + RP_T - 1) / RP_T, (F + RP_F - 1) / RP_F, B);
         if (src_rc)  // row codes for lik_source_rc_kernel
             repack_source_kernel<<<rgrid, 256, 0, ctx->stream>>>(
                 d.n_sites, F, ctx->Np, ctx->d_perm, source, static_cast<uint8_t *>(ctx->src_t.ptr), zone,
