@@ -89,10 +89,23 @@ size_t mh_src_lds_bytes(const sbz_dims &d, int C, bool hbm_sources, bool geo, bo
            // redraw_rows: draws [F][S] doubles, per-feature tape offsets and counter ranks [F] ints
            16 + F * S * 8 + 2 * F * 4 + 8 +
            // staged parameters: normalised weights [F][4][3], p_global, p_zones, p_families
-           (stage ? 16 + (12 * F + (1 + Z + (C == 3 ? (size_t)d.n_families : 0)) * F * S) * 8 + N * F : 0);
+           (stage ? 16 + (12 * F + (1 + Z + (C == 3 ? (size_t)d.n_families : 0)) * F * S) * 8 + N * F + N : 0);
 }
 
 namespace {
+
+// (s, f) of cell c = s * F + f, advanced by NT cells per step
+struct CellWalk {
+    int s, f, dS, dF, F;
+    __device__ __forceinline__ void next() {
+        f += dF;
+        s += dS;
+        if (f >= F) {
+            f -= F;
+            s++;
+        }
+    }
+};
 
 // One workgroup of NW waves runs one chain.  Every decision is uniform across the workgroup:
 // all waves draw the same values from identical RNG states and take the same branches; the
@@ -148,6 +161,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     double *lpz = lpg + (size_t)F * S;                         // [Z][F][S]
     double *lpf = lpz + (size_t)Z * F * S;                     // [Fam][F][S]
     uint8_t *lobs = reinterpret_cast<uint8_t *>(lpf + (size_t)Fam * F * S);  // [N][F] x by site
+    uint8_t *lfam = lobs + NF;                                                 // [N] family class
     const bool stg = a.stage != 0;
     bool stg_ok = false;
 
@@ -206,8 +220,10 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     const double p_grow = ch.p_grow_connected[b];
 
     for (int z = tid; z < Z; z += NT) zsize[z] = 0;
-    if (a.stage)  // the observations never change: staged once
+    if (a.stage) {  // the observations and family classes never change: staged once
         for (int c = tid; c < NF; c += NT) lobs[c] = a.obs_sm[c];
+        for (int s = tid; s < N; s += NT) lfam[s] = C == 3 ? a.fam_site[s] : 0;
+    }
     if (tid < MH_STAT_INTS) stat[tid] = 0;
     for (int s = tid; s < N; s += NT) nb[s] = 0;
     if (!GS)
@@ -325,12 +341,13 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     };
     // obs_terms from the staged copies (the same values, the same operations)
     auto terms = [&](int s, int f, double (&l)[3], double (&wn)[3]) {
-        const int zc = zos[s], fc = C == 3 ? a.fam_site[s] : 0;
+        const int zc = zos[s];
         if (!stg) {
+            const int fc = C == 3 ? a.fam_site[s] : 0;
             obs_terms<C>(a, w, pg, pz, pf, s, f, zc, fc, l, wn);
             return;
         }
-        const int x = lobs[s * F + f];
+        const int x = lobs[s * F + f], fc = lfam[s];
         const bool na = x >= S;
         const int xc = na ? 0 : x;
         const bool hz = zc < Z, hf = (C == 3) && fc > 0;
@@ -342,7 +359,9 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         l[1] = na ? 1.0 : (hz ? lpz[(zc * F + f) * S + xc] : 0.0);
         l[2] = (C == 3) ? (na ? 1.0 : (hf ? lpf[((fc - 1) * F + f) * S + xc] : 0.0)) : 0.0;
     };
-    // ---- passes over the N*F observations (cell c = s*F + f, C order)
+    // ---- passes over the N*F observations (cell c = s*F + f, C order); (s, f) stepped with the
+    // cell index (CellWalk) instead of a division per cell
+    const int cdS = NT / F, cdF = NT - cdS * F;
     // Sums of logs as one log per thread: each factor's mantissa multiplies a product and its
     // exponent adds to an integer (exact for any factor, denormals included), the product is
     // renormalised every 8 cells, and log(m) + e ln 2 is taken once (~1e-16 relative).
@@ -364,8 +383,9 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     auto pass_logq = [&]() -> double {
         ensure_staged();
         LogAcc acc;
-        for (int c = tid; c < NF; c += NT) {
-            const int s = c / F, f = c - s * F;
+        CellWalk cw{tid / F, tid - (tid / F) * F, cdS, cdF, F};
+        for (int c = tid; c < NF; c += NT, cw.next()) {
+            const int s = cw.s, f = cw.f;
             double l[3], wn[3], p[3];
             terms(s, f, l, wn);
             posterior_draw<C>(l, wn, 2.0, p);
@@ -379,8 +399,9 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         ensure_staged();
         LogAcc acc;
         int zero_w = 0;
-        for (int c = tid; c < NF; c += NT) {
-            const int s = c / F, f = c - s * F;
+        CellWalk cw{tid / F, tid - (tid / F) * F, cdS, cdF, F};
+        for (int c = tid; c < NF; c += NT, cw.next()) {
+            const int s = cw.s, f = cw.f;
             double l[3], wn[3];
             terms(s, f, l, wn);
             const int k = rsrc(sv, c);
@@ -400,8 +421,9 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         int zero_w = 0;
         const int64_t pos0 = rng.pos;
         const bool have = !rng.tape || pos0 + NF <= rng.len;
-        for (int c = tid; c < NF; c += NT) {
-            const int s = c / F, f = c - s * F;
+        CellWalk cw{tid / F, tid - (tid / F) * F, cdS, cdF, F};
+        for (int c = tid; c < NF; c += NT, cw.next()) {
+            const int s = cw.s, f = cw.f;
             double l[3], wn[3], p[3];
             terms(s, f, l, wn);
             const double u = rng.tape ? (have ? rng.tape[pos0 + c] : 0.0) : lr.u();
