@@ -867,9 +867,10 @@ int launch_mh_source(sbz_ctx *ctx, int B, const MhArgs &a0) {
         if (rc) return rc;
         a.src_scratch = static_cast<uint8_t *>(ctx->src_cand.ptr);
     }
-    // waves per chain: 8 when the passes over the N * F observations dominate, else 4
-    // (SBZ_SRC_WAVES overrides: 1, 4 or 8).  8 waves = 2 per SIMD, so up to 256 VGPRs: no spills.
-    int nw = nf >= 16384 ? 8 : 4;
+    // waves per chain: 8 (SBZ_SRC_WAVES overrides: 1, 4 or 8).  8 waves = 2 per SIMD, so up to
+    // 256 VGPRs: no spills.  Measured against 4 on the real-data shapes (tools/src_optime.py):
+    // Balkan 12.4 -> 11.2 us per step, South America 18.0 -> 14.2.
+    int nw = 8;
     if (ctx->src_waves == 1 || ctx->src_waves == 4 || ctx->src_waves == 8) nw = ctx->src_waves;
     static bool configured = false;
     if (!configured) {

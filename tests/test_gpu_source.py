@@ -14,11 +14,11 @@ SRC_CASES = mh_cases(source=True)
 REL_TOL = 1e-9
 
 
-@pytest.fixture(params=["lds", "hbm", "lds-w1", "hbm-w8"])
+@pytest.fixture(params=["lds", "hbm", "lds-w1", "hbm-w4"])
 def src_home(request, monkeypatch):
     """Where the sampler keeps the sources — LDS (when they fit) or HBM (SBZ_SRC_HBM=1, the path
-    every N x F too large for LDS takes) — and the waves per chain (default by N x F, or
-    SBZ_SRC_WAVES = 1 / 8); read when the context opens."""
+    every N x F too large for LDS takes) — and the waves per chain (default 8, or
+    SBZ_SRC_WAVES = 1 / 4); read when the context opens."""
     home, _, waves = request.param.partition("-w")
     monkeypatch.setenv("SBZ_SRC_HBM", "1" if home == "hbm" else "0")
     monkeypatch.setenv("SBZ_SRC_WAVES", waves or "0")
