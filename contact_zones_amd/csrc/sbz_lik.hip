@@ -2121,6 +2121,9 @@ __global__ __launch_bounds__(WAVE, 3) void lik_source_rc_kernel(LikArgs a) {
 #ifndef SBZ_RP_T
 #define SBZ_RP_T 256
 #endif
+#ifndef SBZ_RP_NT
+#define SBZ_RP_NT 0  // non-temporal loads (1) / stores (2) in the repack
+#endif
 #ifndef SBZ_RP_F
 #define SBZ_RP_F 64
 #endif
@@ -2161,7 +2164,7 @@ __global__ __launch_bounds__(256) void repack_source_kernel(int N, int F, int Np
             if (words) {
                 const uint32_t *wp = reinterpret_cast<const uint32_t *>(rp + fq);
 #pragma unroll
-                for (int k = 0; k < 4; k++) w[t][k] = wp[k];
+                for (int k = 0; k < 4; k++) w[t][k] = (SBZ_RP_NT & 1) ? __builtin_nontemporal_load(wp + k) : wp[k];
             } else {
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
@@ -2227,7 +2230,13 @@ __global__ __launch_bounds__(256) void repack_source_kernel(int N, int F, int Np
                 o[k] = x;
             }
             // Np is a multiple of 64, so the 16 bytes are 16-byte aligned and inside the row
-            *reinterpret_cast<uint4 *>(drow + 64 * t) = make_uint4(o[0], o[1], o[2], o[3]);
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            u32x4 *dp = reinterpret_cast<u32x4 *>(drow + 64 * t);
+            const u32x4 ov = {o[0], o[1], o[2], o[3]};
+            if (SBZ_RP_NT & 2)
+                __builtin_nontemporal_store(ov, dp);
+            else
+                *dp = ov;
         }
     }
 }
