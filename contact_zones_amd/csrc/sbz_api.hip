@@ -263,6 +263,7 @@ void sbz_close(sbz_ctx *ctx) {
     free_buf(ctx->zl);
     free_buf(ctx->nzs);
     free_buf(ctx->partial);
+    free_buf(ctx->zflag);
     free_buf(ctx->src_t);
     free_buf(ctx->src_cand);
     free_buf(ctx->ticket);

@@ -41,6 +41,8 @@ struct LikArgs {
     int F4;
     double *partial;        // [B][W]     task partial sums
     unsigned *ticket;       // [B]        finished tasks per chain (0 between launches)
+    unsigned *zflag;        // [B]        source branch: a task saw a zero selected weight (0
+                            //            between launches), or nullptr (mixture)
     double *out;            // [B]        log-likelihood per chain
 };
 
@@ -90,7 +92,7 @@ struct sbz_ctx {
     int n_cu = 256;        // compute units of the device
     int src_waves = 0;     // SBZ_SRC_WAVES: waves per chain of the source-mode sampler (0: by N x F)
     int src_hbm = 0;       // SBZ_SRC_HBM=1: source-mode sampler keeps sources in HBM even when they fit LDS
-    sbz::DevBuf partial, ticket, src_t, zl, nzs, stage, out, src_cand, flags;
+    sbz::DevBuf partial, ticket, zflag, src_t, zl, nzs, stage, out, src_cand, flags;
     std::string err;
 };
 

@@ -93,15 +93,20 @@ __device__ __forceinline__ void wave_lds_sync() {
 // writes back the XCD's L2 once per task: ~1.7 us per fence, measured ~2x the kernel here.
 // tests/test_gpu_likelihood.py::test_partials_handoff_stress re-checks the hand-off under uneven
 // load across all XCDs; the host re-zeroes the tickets when a launch fails (launch_loglik).
+//
+// `zw` (source branch): the task saw a selected normalised weight of exactly 0.  The reference
+// then returns -inf whatever the other cells hold (model.py:181-182, NaN cells included), so the
+// flag travels beside the partials (zflag[b], same sc1 hand-off) and overrides the sum.
 __device__ __forceinline__ void finish_chain(const LikArgs &a, int b, double tot,
-                                             bool leader = threadIdx.x == 0) {
+                                             bool leader = threadIdx.x == 0, bool zw = false) {
     if (!leader) return;
     if (a.W == 1) {
-        a.out[b] = tot;
+        a.out[b] = zw ? -INFINITY : tot;
         return;
     }
     double *pb = a.partial + (size_t)b * a.W;
     __hip_atomic_store(&pb[blockIdx.x], tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (zw) __hip_atomic_store(&a.zflag[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned prev =
         __hip_atomic_fetch_add(&a.ticket[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -110,6 +115,10 @@ __device__ __forceinline__ void finish_chain(const LikArgs &a, int b, double tot
     double s = 0.0;
     for (int t = 0; t < a.W; t++)
         s += __hip_atomic_load(&pb[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (a.zflag != nullptr && __hip_atomic_load(&a.zflag[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        s = -INFINITY;
+        __hip_atomic_store(&a.zflag[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     a.out[b] = s;
     __hip_atomic_store(&a.ticket[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -1768,8 +1777,12 @@ __global__ __launch_bounds__(WAVE) void lik_mixture_generic_kernel(LikArgs a) {
 //   T0[h]            h = hz | hf<<1     w_norm[h][0] * l0                      rows 0..3
 //   T1[z][hf]        has_zone           w_norm[1|hf<<1][1] * l1                rows 4..4+2Z-1
 //   T2[fam][hz]      has_family         w_norm[hz|2][2] * l2                   rows 4+2Z..
-//   Z0               selected component the site lacks: weight 0 -> cell 0 -> -inf
+//   Z0[h]            selected component the site lacks: weight w_c * 0 / sum_h (0, or NaN when
+//                    sum_h = 0), lh 0
 //   N1               neutral row (padded sites)
+// A selected weight of exactly 0 makes the chain -inf whatever the other cells hold
+// (model.py:181-182): zrow[r] flags such rows per feature, and a feature with one runs the
+// per-cell path, which checks every cell's row.
 // Each lane packs its site's three row indices (r0 | r1<<8 | r2<<16); the cell's source
 // byte selects one.
 // ---------------------------------------------------------------------------------------
@@ -1789,7 +1802,8 @@ __global__ __launch_bounds__(WAVE) void lik_source_kernel(LikArgs a) {
     }
     const int S = a.S, S1 = a.S + 1, Z = a.Z;
     const int Fam = (C == 3) ? a.Fam : 0;
-    const int off1 = 4, off2 = 4 + 2 * Z, rz = 4 + 2 * Z + 2 * Fam, rn = rz + 1;
+    const int off1 = 4, off2 = 4 + 2 * Z, rz = 4 + 2 * Z + 2 * Fam, rn = rz + 4;
+    uint8_t *zrow = lds + NW_BYTES + (size_t)(rn + 1) * S1 * 8;
     const size_t zfs = (size_t)a.F * S;
     const double *pgb = a.pg + (size_t)b * zfs;
     const double *pzb = a.pz + (size_t)b * Z * zfs;
@@ -1799,13 +1813,11 @@ __global__ __launch_bounds__(WAVE) void lik_source_kernel(LikArgs a) {
     const int row_bytes = S1 * 8;
     const int shift = a.xs8 ? 0 : 3;
 
-    for (int x = lane; x < S1; x += WAVE) {
-        tab[rz * S1 + x] = 0.0;
-        tab[rn * S1 + x] = 1.0;
-    }
+    for (int x = lane; x < S1; x += WAVE) tab[rn * S1 + x] = 1.0;
 
     double m = 1.0;
     int e = 0;
+    uint32_t zw = 0;
     for (int c0 = 0; c0 < a.Np; c0 += SPL * WAVE) {
         uint32_t rows[SPL];
 #pragma unroll
@@ -1813,16 +1825,16 @@ __global__ __launch_bounds__(WAVE) void lik_source_kernel(LikArgs a) {
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const int s = c0 + 4 * lane + 256 * k + j;  // position (family-sorted order)
-                uint32_t r = (uint32_t)rn | ((uint32_t)rn << 8) | ((uint32_t)rn << 16);
+                uint32_t r = (uint32_t)rn * 0x01010101u;
                 if (s < a.N) {
                     const int z = zb[a.perm[s]];
                     const bool hz = z < Z;
                     const int fc = (C == 3) ? a.famc[s] : 0;
                     const bool hf = fc > 0;
                     const int r0 = (hz ? 1 : 0) | (hf ? 2 : 0);
-                    const int r1 = hz ? off1 + 2 * z + (hf ? 1 : 0) : rz;
-                    const int r2 = hf ? off2 + 2 * (fc - 1) + (hz ? 1 : 0) : rz;
-                    r = (uint32_t)r0 | ((uint32_t)r1 << 8) | ((uint32_t)r2 << 16);
+                    const int r1 = hz ? off1 + 2 * z + (hf ? 1 : 0) : rz + r0;
+                    const int r2 = hf ? off2 + 2 * (fc - 1) + (hz ? 1 : 0) : rz + r0;
+                    r = (uint32_t)r0 | ((uint32_t)r1 << 8) | ((uint32_t)r2 << 16) | ((uint32_t)(rz + r0) << 24);
                 }
                 rows[4 * k + j] = r;
             }
@@ -1842,6 +1854,7 @@ __global__ __launch_bounds__(WAVE) void lik_source_kernel(LikArgs a) {
                     const double v = nw[h * 4 + 0] * l0;
                     bad |= !safe_factor(v);
                     tab[h * S1 + x] = v;
+                    tab[(rz + h) * S1 + x] = nw[h * 4 + 0] * 0.0;
                 }
                 for (int z = 0; z < Z; z++) {
                     const double l1 = na ? 1.0 : pzb[z * zfs + off];
@@ -1857,6 +1870,12 @@ __global__ __launch_bounds__(WAVE) void lik_source_kernel(LikArgs a) {
                     tab[(off2 + 2 * i) * S1 + x] = v0;
                     tab[(off2 + 2 * i + 1) * S1 + x] = v1;
                 }
+            }
+            for (int r = lane; r <= rn; r += WAVE) {  // weights of exactly 0, by table row
+                const double wr = r < 4 ? nw[r * 4] : r < off2 ? nw[(1 | (((r - 4) & 1) << 1)) * 4 + 1]
+                                : r < rz ? nw[(2 | ((r - off2) & 1)) * 4 + 2] : r < rn ? nw[(r - rz) * 4] * 0.0 : 1.0;
+                zrow[r] = wr == 0.0 ? 1 : 0;
+                bad |= wr == 0.0;
             }
             const bool wide = __ballot(bad) != 0;
             wave_lds_sync();
@@ -1875,12 +1894,15 @@ __global__ __launch_bounds__(WAVE) void lik_source_kernel(LikArgs a) {
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     const uint32_t c = (sc[k] >> (8 * j)) & 0xff;
-                    const uint32_t r = (rows[4 * k + j] >> (8 * min(c, 2u))) & 0xff;
-                    const uint32_t rr = (c < (uint32_t)C) ? r : (uint32_t)rz;
+                    const uint32_t rr = (rows[4 * k + j] >> (8 * (c < (uint32_t)C ? c : 3u))) & 0xff;
                     const int addr = NW_BYTES + (int)rr * row_bytes +
                                      (int)(((o[k] >> (8 * j)) & 0xff) << shift);
-                    if (wide) mul_exact(m, e, *reinterpret_cast<const double *>(lds + addr));
-                    else m *= *reinterpret_cast<const double *>(lds + addr);
+                    if (wide) {
+                        mul_exact(m, e, *reinterpret_cast<const double *>(lds + addr));
+                        zw |= zrow[rr];
+                    } else {
+                        m *= *reinterpret_cast<const double *>(lds + addr);
+                    }
                 }
                 if (k & 1) renorm(m, e);
             }
@@ -1890,7 +1912,7 @@ __global__ __launch_bounds__(WAVE) void lik_source_kernel(LikArgs a) {
     }
     const double v = log(m) + (double)e * LN2;
     const double tot = wave_sum(v);
-    finish_chain(a, b, tot);
+    finish_chain(a, b, tot, lane == 0, __ballot(zw != 0) != 0);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1921,11 +1943,15 @@ __global__ __launch_bounds__(WAVE, 3) void lik_source_rc_kernel(LikArgs a) {
     }
     const int S = a.S, S1 = a.S + 1, Z = a.Z;
     const int Fam = (C == 3) ? a.Fam : 0;
-    const int off1 = 4, off2 = 4 + 2 * Z, rz = off2 + 2 * Fam, rn = rz + 1;
+    const int off1 = 4, off2 = 4 + 2 * Z, rz = off2 + 2 * Fam, rn = rz + 4;
     const int row_bytes = S1 * 8;
     double *tab = reinterpret_cast<double *>(lds);
     double *nwt = tab + ((((rn + 1) * S1) + 1) & ~1);  // [SRC_NWC][8], 16-B aligned
     double *junk = nwt + SRC_NWC * 8 + lane;
+    // zrow[r] = 1: the weight of row r is exactly 0 (written for `wide` features and read by their
+    // per-factor gathers: the reference's any(weight == 0) -> -inf, model.py:181-182).  A zero
+    // weight in a fast-path feature gives a zero product, which re-runs the task per factor.
+    uint8_t *zrow = reinterpret_cast<uint8_t *>(nwt + SRC_NWC * 8 + WAVE);
 
     const int G = WAVE / S1, lx = lane % S1, lg = lane / S1;
     const bool na = lx == S, act = lane < G * S1;
@@ -1970,10 +1996,9 @@ __global__ __launch_bounds__(WAVE, 3) void lik_source_rc_kernel(LikArgs a) {
         for (int k = 0; k < NO; k++) o[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, lane * 4, f * a.Np + c0 + 256 * k, 0);
     };
 
-    for (int x = lane; x < S1; x += WAVE) {
-        tab[rz * S1 + x] = 0.0;  // a component the site lacks: weight 0
-        tab[rn * S1 + x] = 1.0;  // padding positions
-    }
+    for (int x = lane; x < S1; x += WAVE) tab[rn * S1 + x] = 1.0;  // padding positions
+    bool force = false;  // per-factor re-run of the task (uniform)
+    uint32_t zw = 0;     // per-factor features: this lane selected a weight of exactly 0
     // normalised weights of features f0 .. f0 + SRC_NWC: [k][q], q = h (w_norm[h][0]), 4 / 5 =
     // w_norm[1 / 3][1], 6 / 7 = w_norm[2 / 3][2]; lane 2k + hp computes feature k's h = 2hp + hz
     int nwf0 = -(1 << 30);
@@ -2018,11 +2043,25 @@ __global__ __launch_bounds__(WAVE, 3) void lik_source_rc_kernel(LikArgs a) {
         if (C == 3) hmx = max(hmx, max(hiword(r.fm[0]), hiword(r.fm[1])));
         const bool wide = ((nwbad >> (2 * k)) & 3ull) != 0 || __ballot(hmx > 0x3FF00000u) != 0;
         const double *q = nwt + k * 8;
-        const double wh = q[min(lg, 3)], wz0 = q[4], wz1 = q[5], wf0 = q[6], wf1 = q[7];
+        const double wz0 = q[4], wz1 = q[5], wf0 = q[6], wf1 = q[7];
         wave_lds_sync();  // the previous feature's gathers are done with the table
         const double l0 = r.g + naone;
-        double *t0 = (act && lg < 4) ? tab + lg * S1 + lx : junk;
-        *t0 = wh * l0;
+        // T0[h], h = 0..3, from lane group lg (and lg + G, ... when fewer than 4 groups, S1 > 16),
+        // and the zero row of h: a component the site lacks has weight w_c * 0 / sum_h (0, or NaN
+        // when sum_h is 0) and lh 0 (model.py:241-247, 436-452)
+        for (int h = lg; h < 4; h += G) {
+            double *t0 = act ? tab + h * S1 + lx : junk;
+            *t0 = q[h] * l0;
+            double *t0z = act ? tab + (rz + h) * S1 + lx : junk;
+            *t0z = q[h] * 0.0;
+        }
+        if (wide || force) {  // weights of exactly 0, by table row
+            for (int r = lane; r <= rn; r += WAVE) {  // rn: the padding positions' neutral row
+                const double wr = r < 4 ? q[r] : r < off2 ? q[4 + ((r - 4) & 1)]
+                                : r < rz ? q[6 + ((r - off2) & 1)] : r < rn ? q[r - rz] * 0.0 : 1.0;
+                zrow[r] = wr == 0.0 ? 1 : 0;
+            }
+        }
 #pragma unroll
         for (int i = 0; i < 2; i++) {
             const int zr = lg + G * i;
@@ -2046,12 +2085,13 @@ __global__ __launch_bounds__(WAVE, 3) void lik_source_rc_kernel(LikArgs a) {
     double m[4];
     int e;
     uint64_t under;
-    bool force = false;
     SrcParams P[2];
     uint32_t O[2][NO], R[2][NO];
+    // a product that left the normal range (0, tiny, or NaN: fmin would drop a NaN) re-runs the
+    // task per factor, where every cell's row is checked for a zero weight
     auto flush = [&]() {
-        const double mn = fmin(fmin(m[0], m[1]), fmin(m[2], m[3]));
-        under |= __ballot(!(mn >= 0x1p-1022));
+        constexpr double T = 0x1p-1022;
+        under |= __ballot(!(m[0] >= T && m[1] >= T && m[2] >= T && m[3] >= T));
 #pragma unroll
         for (int q = 0; q < 4; q++)
             if (q < NO) renorm(m[q], e);
@@ -2088,6 +2128,7 @@ __global__ __launch_bounds__(WAVE, 3) void lik_source_rc_kernel(LikArgs a) {
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     mul_exact(m[0], e, *reinterpret_cast<const double *>(lds + addr(k, j)));
+                    zw |= zrow[(rb[k] >> (8 * j)) & 0xffu];
                 }
         }
     };
@@ -2110,7 +2151,8 @@ __global__ __launch_bounds__(WAVE, 3) void lik_source_rc_kernel(LikArgs a) {
         force = true;  // uniform: `under` is a ballot
     }
     const double v = (log(m[0]) + log(m[1])) + (log(m[2]) + log(m[3])) + (double)e * LN2;
-    finish_chain(a, b, wave_sum(v));
+    const double tot = wave_sum(v);
+    finish_chain(a, b, tot, lane == 0, __ballot(zw != 0) != 0);
 }
 
 // Row-major source [B][N][F] -> feature-major [B][F][Np] in the family-sorted site order
@@ -2179,7 +2221,7 @@ __global__ __launch_bounds__(256) void repack_source_kernel(int N, int F, int Np
             for (int k = 0; k < 4; k++) w[t][k] = 0;
         }
     }
-    const int off2 = 4 + 2 * Z, rz = off2 + 2 * Fam, rn = rz + 1;
+    const int off2 = 4 + 2 * Z, rz = off2 + 2 * Fam, rn = rz + 4;
 #pragma unroll
     for (int t = 0; t < NP; t++) {
         if (zone) {
@@ -2191,9 +2233,10 @@ __global__ __launch_bounds__(256) void repack_source_kernel(int N, int F, int Np
                 const int fc = (C == 3) ? famc[p0 + RPP * t + rg] : 0;
                 const bool hf = fc > 0;
                 const uint32_t r0 = (hz ? 1u : 0u) | (hf ? 2u : 0u);
-                const uint32_t r1 = hz ? (uint32_t)(4 + 2 * z + (hf ? 1 : 0)) : (uint32_t)rz;
-                const uint32_t r2 = (C == 3 && hf) ? (uint32_t)(off2 + 2 * (fc - 1) + (hz ? 1 : 0)) : (uint32_t)rz;
-                map = r0 | (r1 << 8) | (r2 << 16) | ((uint32_t)rz << 24);
+                const uint32_t rl = (uint32_t)rz + r0;  // a component the site lacks: zero row of h
+                const uint32_t r1 = hz ? (uint32_t)(4 + 2 * z + (hf ? 1 : 0)) : rl;
+                const uint32_t r2 = (C == 3 && hf) ? (uint32_t)(off2 + 2 * (fc - 1) + (hz ? 1 : 0)) : rl;
+                map = r0 | (r1 << 8) | (r2 << 16) | (rl << 24);
             } else {
                 map = (uint32_t)rn * 0x01010101u;
             }
@@ -2383,20 +2426,21 @@ void configure_zd(std::vector<const void *> &v) {
     }
 }
 
-// lik_source_rc_kernel applies: G = 64 / S1 lanes groups cover 2G zone and family rows, row
-// indices are bytes
+// lik_source_rc_kernel applies: G = 64 / S1 lanes groups cover 2G zone and family rows (the 4
+// T0 rows are written by a strided loop over the groups, so any G >= 1), row indices are bytes
 bool source_rc_applies(const sbz_dims &d, int C) {
     const int S1 = d.n_states + 1;
     if (S1 > WAVE) return false;
     const int G = WAVE / S1;
     const int Fam = C == 3 ? d.n_families : 0;
-    return d.n_zones <= 2 * G && Fam <= 2 * G && 4 + 2 * d.n_zones + 2 * Fam + 1 < 256;
+    return d.n_zones <= 2 * G && Fam <= 2 * G && 4 + 2 * d.n_zones + 2 * Fam + 4 < 256;
 }
+// table (T0 4, T1 2Z, T2 2Fam, zero rows 4, neutral 1) | nwt | junk | zrow (row bytes)
 size_t source_rc_lds_bytes(const sbz_dims &d, int C) {
     const size_t S1 = (size_t)d.n_states + 1;
     const size_t Fam = C == 3 ? (size_t)d.n_families : 0;
-    const size_t rows = 4 + 2 * (size_t)d.n_zones + 2 * Fam + 2;
-    return ((((rows * S1) + 1) & ~(size_t)1) + (size_t)SRC_NWC * 8 + WAVE) * 8;
+    const size_t rows = 4 + 2 * (size_t)d.n_zones + 2 * Fam + 5;
+    return ((((rows * S1) + 1) & ~(size_t)1) + (size_t)SRC_NWC * 8 + WAVE) * 8 + ((rows + 7) & ~(size_t)7);
 }
 template <int C>
 const void *source_rc_kernel(int spl, bool xs8) {
@@ -2495,8 +2539,8 @@ size_t lik_lds_bytes(const sbz_dims &d, bool source_mode) {
         const MixPlan p = plan_mixture(d, C);
         return p.fr ? mix_lds_bytes(d, C, p.bk) : 0;
     }
-    const size_t rows = 4 + 2 * (size_t)d.n_zones + (inh ? 2 * (size_t)d.n_families : 0) + 2;
-    return NW_BYTES + rows * S1 * sizeof(double);
+    const size_t rows = 4 + 2 * (size_t)d.n_zones + (inh ? 2 * (size_t)d.n_families : 0) + 5;
+    return NW_BYTES + rows * S1 * sizeof(double) + ((rows + 7) & ~(size_t)7);  // table | zrow
 }
 
 int lik_configure(sbz_ctx *ctx) {
@@ -2652,6 +2696,15 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
     }
     a.ticket = static_cast<unsigned *>(ctx->ticket.ptr);
     a.out = out_ll;
+    if (src_mode) {
+        if (ctx->zflag.bytes < (size_t)B * sizeof(unsigned) || !ctx->zflag.ptr) {
+            rc = ensure(ctx, ctx->zflag, (size_t)B * sizeof(unsigned));
+            if (rc) return rc;
+            hipError_t e = hipMemsetAsync(ctx->zflag.ptr, 0, ctx->zflag.bytes, ctx->stream);
+            if (e != hipSuccess) return hip_fail(ctx, e, "hipMemsetAsync(zflag)");
+        }
+        a.zflag = static_cast<unsigned *>(ctx->zflag.ptr);
+    }
 
     if (src_mode) {
         const size_t bytes = (size_t)B * F * ctx->Np;
@@ -2674,6 +2727,7 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
     // finished would leave the chains' tickets non-zero and corrupt every later sum: re-zero them.
     auto launch_failed = [&](hipError_t e, const char *what) {
         (void)hipMemsetAsync(ctx->ticket.ptr, 0, ctx->ticket.bytes, st);
+        if (ctx->zflag.ptr) (void)hipMemsetAsync(ctx->zflag.ptr, 0, ctx->zflag.bytes, st);
         return hip_fail(ctx, e, what);
     };
     if (src_rc) {

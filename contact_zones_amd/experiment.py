@@ -365,8 +365,12 @@ def main(argv=None):
             for n in sweep:
                 run_experiment(config, data, int(n), run=run, name=name, seed=seed, device=device,
                                logger=logger)
-    finally:
-        _finish_distributed()
+    except BaseException:
+        # no barrier: the other ranks may be waiting in a different collective; leave the group
+        # and exit non-zero so the launcher tears the job down
+        _finish_distributed(ok=False)
+        raise
+    _finish_distributed(ok=True)
     return 0
 
 
@@ -403,9 +407,12 @@ def _broadcast_name(name):
     return box[0]
 
 
-def _finish_distributed():
+def _finish_distributed(ok=True):
+    """Leave the process group: after a barrier on success; without one after a failure (a
+    barrier could pair with a peer's pending all_reduce / broadcast and hang or mismatch)."""
     from .parallel import _dist
     d = _dist()
     if d is not None and int(os.environ.get("WORLD_SIZE", "1")) > 1:
-        d.barrier()
+        if ok:
+            d.barrier()
         d.destroy_process_group()

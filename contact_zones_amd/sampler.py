@@ -87,7 +87,9 @@ class ChainState:
                                  f"got {src.shape}")
             self.source = torch.as_tensor(src, device=dev)
         self.counter = torch.zeros(self.B, dtype=torch.int64, device=dev)
-        # the kernels trust the index bytes (include/sbz.h): range-check them once here
+        # the kernels trust the index bytes (include/sbz.h): range-check them once here, on the
+        # stream that produced the tensors
+        engine.set_stream(torch.cuda.current_stream(dev).cuda_stream)
         engine.check_indices_device(self.B, self.zone_of_site.data_ptr(),
                                     self.source.data_ptr() if self.source is not None else 0)
         self.refresh_ll()

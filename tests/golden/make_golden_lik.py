@@ -15,7 +15,8 @@ Cases follow BASELINE.json's configs:
   cfg5_slice     synthetic 400 x 120 x 10, Z=8, Fam=4 (a reduced slice of the roofline shape)
   cfg5_full      synthetic 2000 x 500 x 10, Z=8, Fam=4 (one chain, full roofline shape)
   edge_*         Z=0, all sites zoned, all-NA feature, S=2, tiny/huge probabilities,
-                 a zero selected source weight (-inf), single site
+                 a zero selected source weight (-inf), single site,
+                 a zero selected weight beside 0/0 normalised weights (-inf, not NaN)
 
 Usage: python tests/golden/make_golden_lik.py   (from the repo root)
 """
@@ -286,9 +287,34 @@ def case_edges():
               Z=2, inheritance=True, B=2, zone_size=10, tweak=zero_w)
 
 
+def case_zero_nan():
+    """model.py:181-182 tests `any(observation_weights == 0)` before taking logs: a selected
+    weight of exactly 0 gives -inf even when other selected weights are NaN (0 / 0 normalised
+    weights at sites with none of the feature's non-zero components).  Chain 0: feature 3 has
+    weights [0, 1, 0], so the no-zone sites' weights are 0 / 0 and a zoned site selecting the
+    global component has weight 0 -> -inf.  Chain 1: the same NaN cells, no zero selected
+    weight (every zoned site selects its zone at feature 3) -> NaN."""
+    def zero_nan(loc):
+        for b in (0, 1):
+            loc["w"][b, 3] = [0.0, 1.0, 0.0]
+            zoned = loc["zos"][b] != 255
+            loc["src"][b, zoned, 3] = 1
+        z0 = np.nonzero(loc["zos"][0] != 255)[0][0]
+        loc["src"][0, z0, 3] = 0
+    rng = np.random.default_rng(76)
+    N, F, S = 64, 20, 3
+    states = random_states_mask(rng, F, S)
+    make_case("edge_zero_nan", rng, random_obs(rng, N, F, states, 0.0), synth_fam(rng, N, 2), states,
+              Z=2, inheritance=True, B=2, zone_size=10, tweak=zero_nan)
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["zero_nan"]:
+        case_zero_nan()
+        sys.exit(0)
     case_kat()
     case_synth()
     case_real()
     case_edges()
+    case_zero_nan()
     case_cfg1_sim()

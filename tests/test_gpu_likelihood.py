@@ -277,9 +277,7 @@ def test_source_edge_paths(gpu_available, monkeypatch, rc, shape):
         s3 = int(np.flatnonzero(zos[3] != 255)[0])
         src[3, s3, 5] = 1
     else:
-        # family weight 0 where a site with a family selects its family (a zero global weight
-        # would make the no-family sites' weights 0 / 0 = NaN: the reference then still returns
-        # -inf from its any(weight == 0) test, the kernels NaN)
+        # family weight 0 where a site with a family selects its family
         w[3, 5, 2] = 0.0
         src[3, int(np.flatnonzero(fam != 255)[0]), 5] = 2
     pg[4, :, 1] = 1e-200                # tiny
@@ -403,3 +401,100 @@ def test_device_index_validation(gpu_available):
                       t["pz"].data_ptr(), t["pf"].data_ptr(), 0, out.data_ptr())
     torch.cuda.synchronize()
     np.testing.assert_array_equal(out.cpu().numpy(), eng.loglik(zos, w, pg, pz, pf))
+
+
+@pytest.mark.parametrize("rc", ["1", "0"])
+@pytest.mark.parametrize("S,Z,Fam,inh", [(15, 3, 3, True), (16, 3, 3, True), (17, 4, 3, True),
+                                         (20, 5, 5, True), (31, 2, 0, False), (32, 2, 0, False),
+                                         (40, 2, 0, False)])
+def test_source_wide_state_tables(gpu_available, monkeypatch, rc, S, Z, Fam, inh):
+    """Source branch with many states: S + 1 > 16 leaves fewer than 4 lane groups of S + 1 lanes
+    in a wave, so the row-code kernel writes its 4 T0 rows (and the 4 zero rows) by a strided
+    loop over the groups; every (class, state) entry must be written (a missed T0 row would read
+    stale LDS).  Both source kernels against the oracle, with the T0 rows of every class h in use
+    (zoned / unzoned sites with and without a family, every component selected)."""
+    from contact_zones_amd.likelihood import LikelihoodEngine
+    from oracle import oracle_c
+    monkeypatch.setenv("SBZ_SRC_RC", rc)
+    N, F, B = 300, 23, 6
+    rng = np.random.default_rng(1000 * S + Z)
+    obs, fam, zos, w, pg, pz, pf, src = _random_batch(rng, N, F, S, Z, Fam, B, inh, 20, nofam=0.3)
+    if not inh:
+        src = np.minimum(src, 1).astype(np.uint8)
+    eng = LikelihoodEngine(obs, fam, S, Z, Fam, inh)
+    got = eng.loglik(zos, w, pg, pz, pf, src)
+    ref = oracle_c.loglik_batch(obs, fam, zos, w, pg, pz, pf, source=src, inheritance=inh)
+    assert np.all(np.isfinite(ref))
+    _assert_close(got, ref, tol=1e-12)
+
+
+@pytest.mark.parametrize("rc", ["1", "0"])
+def test_source_zero_weight_beside_nan(gpu_available, monkeypatch, rc):
+    """model.py:181-182: a selected weight of exactly 0 gives -inf even when other selected
+    weights are NaN (0 / 0); without a zero selected weight the NaN cells give NaN.  The chains
+    are split over several tasks, so the zero and the NaN cells land in different tasks."""
+    from contact_zones_amd.likelihood import LikelihoodEngine
+    from oracle import oracle_c
+    monkeypatch.setenv("SBZ_SRC_RC", rc)
+    N, F, S, Z, Fam, B = 700, 90, 5, 3, 2, 4
+    rng = np.random.default_rng(99)
+    obs, fam, zos, w, pg, pz, pf, src = _random_batch(rng, N, F, S, Z, Fam, B, True, 40)
+    for b in range(B):
+        w[b, 3] = [0.0, 1.0, 0.0]        # no-zone sites: 0 / 0 weights (NaN cells)
+        src[b, zos[b] != 255, 3] = 1
+    z0 = int(np.flatnonzero(zos[0] != 255)[0])
+    src[0, z0, 3] = 0                    # chain 0: a zoned site selects the global weight 0
+    w[2, 80] = [0.0, 0.5, 0.5]           # chain 2: also a zero weight far from the NaN feature
+    s2 = int(np.flatnonzero(zos[2] == 255)[0])
+    src[2, s2, 80] = 0
+    w[3, 3] = [0.2, 0.5, 0.3]            # chain 3: no NaN, no zero weight -> finite
+    eng = LikelihoodEngine(obs, fam, S, Z, Fam, True)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        ref = oracle_c.loglik_batch(obs, fam, zos, w, pg, pz, pf, source=src, inheritance=True)
+    assert ref[0] == -np.inf and np.isnan(ref[1]) and ref[2] == -np.inf and np.isfinite(ref[3])
+    for _ in range(2):  # the per-chain flag is re-armed between launches
+        got = eng.loglik(zos, w, pg, pz, pf, src)
+        _assert_close(got, ref, tol=1e-12)
+    one = eng.loglik(zos[1:2], w[1:2], pg[1:2], pz[1:2], pf[1:2], src[1:2])
+    assert np.isnan(one[0])
+
+
+@pytest.mark.parametrize("B", [256, 2048])
+@pytest.mark.parametrize("mode", ["mixture", "source"])
+def test_bench_launch_parity(gpu_available, B, mode):
+    """The exact launch bench.py times (BASELINE configs[4]: 2000 sites x 500 features x 10
+    states, 8 zones of 50 sites, 4 families, device pointers, validate=False) at the bench's
+    chains per GPU (256) and at 2048 chains on one GPU: the task split W depends on B, so these
+    are the long-task shapes (12 tasks of ~42 features at B = 256, 2 of 250 at B = 2048) no
+    smaller case reaches.  First, last and 8 sampled chains against the C oracle."""
+    import argparse
+    import torch
+    import bench
+    from contact_zones_amd.likelihood import LikelihoodEngine
+    from oracle import oracle_c
+    if mode == "source" and B > 256:
+        pytest.skip("source sweep at the bench's 256 chains (2048 x 1 MB of sources)")
+    args = argparse.Namespace(sites=2000, features=500, states=10, zones=8, families=4,
+                              zone_size=50, mode=mode, seed=5)
+    obs, fam = bench.make_shared(args, np.random.default_rng(args.seed))
+    args._fam = fam
+    dev = torch.device("cuda:0")
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1234 + B)
+    c = bench.make_chains_torch(args, B, gen, dev)
+    eng = LikelihoodEngine(obs, fam, 10, 8, 4, True)
+    eng.set_stream(torch.cuda.current_stream().cuda_stream)
+    out = torch.empty(B, dtype=torch.float64, device=dev)
+    src = c["src"]
+    for _ in range(2):  # twice: the second launch runs on re-armed tickets
+        eng.loglik_device(B, c["zos"].data_ptr(), c["w"].data_ptr(), c["pg"].data_ptr(),
+                          c["pz"].data_ptr(), c["pf"].data_ptr(),
+                          src.data_ptr() if src is not None else 0, out.data_ptr(), validate=False)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    assert np.all(np.isfinite(got))
+    pick = sorted({0, B - 1, *np.random.default_rng(B).choice(B, 8, replace=False).tolist()})
+    h = {k: (v[pick].cpu().numpy() if v is not None else None) for k, v in c.items()}
+    ref = oracle_c.loglik_batch(obs, fam, h["zos"], h["w"], h["pg"], h["pz"], h["pf"],
+                                source=h["src"], inheritance=True)
+    _assert_close(got[pick], ref, tol=1e-12)

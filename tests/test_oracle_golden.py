@@ -21,7 +21,7 @@ def _args(d):
 
 def _rel(a, b):
     a, b = np.asarray(a), np.asarray(b)
-    same_inf = (a == b)
+    same_inf = (a == b) | (np.isnan(a) & np.isnan(b))
     with np.errstate(invalid="ignore", divide="ignore"):
         r = np.abs(a - b) / np.maximum(np.abs(b), 1e-300)
     return float(np.max(np.where(same_inf, 0.0, r)))
