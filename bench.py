@@ -45,7 +45,12 @@ def parse():
     p.add_argument("--mode", choices=["mixture", "source"], default="mixture")
     p.add_argument("--cpu-seconds", type=float, default=12.0,
                    help="bounded CPU-baseline sample (0 disables)")
+    p.add_argument("--cpu-procs", type=int, default=0,
+                   help="CPU baseline: worker processes, one per core (0: the cores this process "
+                        "may run on, at most 16 = a one-GPU box's CPU share)")
     p.add_argument("--seed", type=int, default=5)
+    p.add_argument("--launch-check", action="store_true",
+                   help="only start the ranks (gloo, no GPU) and report the world size")
     p.add_argument("--mh-steps", type=int, default=50000,
                    help="sampler leg: timed MH steps per chain (0 disables the leg)")
     p.add_argument("--mh-burnin", type=int, default=200000, help="sampler leg: untimed MH steps")
@@ -136,11 +141,16 @@ def pmc_traffic(args, B):
     return None, None
 
 
-def cpu_baseline(args, seconds):
-    """Time the numpy restatement of Likelihood.__call__ (oracle, kind 'port') on 1 core."""
+def _cpu_worker(shape, seconds, seed, q):
+    """One CPU-baseline process: Likelihood.__call__(caching=False) restated in numpy
+    (oracle/lik_numpy.py, bit-exact with the reference on the golden vectors) on one chain of
+    the bench workload, repeated for `seconds`.  Started with the spawn method and
+    OMP_NUM_THREADS = OPENBLAS_NUM_THREADS = 1, so it is one core's worth of work."""
+    import argparse
     import numpy as np
     from oracle import lik_numpy
-    rng = np.random.default_rng(args.seed)
+    args = argparse.Namespace(**shape)
+    rng = np.random.default_rng(seed)
     obs, fam = make_shared(args, rng)
     N, F, S, Z, Fam = args.sites, args.features, args.states, args.zones, args.families
     zos = np.full(N, 255, np.uint8)
@@ -161,9 +171,61 @@ def cpu_baseline(args, seconds):
         el = time.perf_counter() - t0
         if el >= seconds:
             break
-    return {"value": n / el, "unit": "likelihood-evals/s", "cores": 1, "kind": "port",
+    q.put((n, el))
+
+
+def cpu_baseline(args, seconds):
+    """SURVEY.md §8d CPU timing: one process per host core (spawned, single-threaded BLAS/OpenMP),
+    each evaluating one chain of the bench workload for `seconds`; per-core and all-core evals/s
+    with os.cpu_count() stated.  Kind 'port': the numpy restatement of the reference's
+    Likelihood.__call__ (the reference itself never travels to the GPU box); its speed relative to
+    the reference, both timed in the build container, is in profiles/r03_cpu_reference_ratio.json."""
+    import multiprocessing as mp
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    procs = args.cpu_procs if args.cpu_procs > 0 else max(1, min(16, avail))
+    shape = {k: getattr(args, k) for k in ("sites", "features", "states", "zones", "families", "zone_size")}
+    keep = {k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS")}
+    for k in keep:
+        os.environ[k] = "1"
+    ctx = mp.get_context("spawn")  # fresh interpreters: nothing of this process's GPU state
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_cpu_worker, args=(shape, seconds, args.seed, q)) for _ in range(procs)]
+    try:
+        for p in ps:
+            p.start()
+        res = [q.get(timeout=seconds * 10 + 300) for _ in ps]
+        for p in ps:
+            p.join()
+    finally:
+        for k, v in keep.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    rates = [n / el for n, el in res]
+    N, F, S, Z, Fam = args.sites, args.features, args.states, args.zones, args.families
+    ratio = None  # restatement / reference speed, both timed in the build container
+    try:
+        with open(os.path.join(ROOT, "profiles", "r03_cpu_reference_ratio.json")) as f:
+            case = json.load(f)["cases"].get(f"{N}x{F}x{S} Z{Z} Fam{Fam}")
+        ratio = case["restatement_over_reference"] if case else None
+    except (OSError, ValueError, KeyError):
+        pass
+    extra = {}
+    if ratio:
+        extra = {"restatement_over_reference": ratio,
+                 "reference_equivalent_value": float(sum(rates)) / ratio,
+                 "ratio_source": "profiles/r03_cpu_reference_ratio.json (tools/time_reference_lik.py)"}
+    return {"value": float(sum(rates)), "unit": "likelihood-evals/s", "cores": procs, "kind": "port",
+            **extra,
+            "per_core": float(sum(rates) / procs), "per_core_min": float(min(rates)),
+            "host_cpu_count": os.cpu_count(), "cores_available": avail,
             "sample": f"numpy restatement of Likelihood.__call__(caching=False) (oracle/lik_numpy.py), "
-                      f"1 chain at {N}x{F}x{S}, Z={Z}, Fam={Fam}: {n} evals in {el:.1f} s, 1 thread"}
+                      f"one chain at {N}x{F}x{S}, Z={Z}, Fam={Fam} per process, {procs} processes x "
+                      f"{seconds:.0f} s, 1 thread each ({sum(n for n, _ in res)} evals)"}
 
 
 # sampler leg: the reference defaults (config/default_config.json:6-20, 29-30)
@@ -202,7 +264,7 @@ def sampler_leg(args, eng, obs, fam, dev, rank, world, stream):
     import torch
     import torch.distributed as dist
     from contact_zones_amd import packing
-    from contact_zones_amd.diagnostics import ess
+    from contact_zones_amd.diagnostics import ess, logged_ess
     from contact_zones_amd.mcmc import InitialSamples
     from contact_zones_amd.sampler import ChainState, Sampler, precisions
     N, F, S, Z, Fam = args.sites, args.features, args.states, args.zones, args.families
@@ -249,22 +311,30 @@ def sampler_leg(args, eng, obs, fam, dev, rank, world, stream):
     ll_full = st.ll.clone()
     st.refresh_ll()  # drift of the incremental log-likelihood over burn-in + K steps
     drift = float(((st.ll - ll_full).abs() / st.ll.abs()).max())
-    e = ess(ll_trace)
+    # ESS as Tracer computes it on the samples the reference logs (every ceil(K / 1000)-th step),
+    # and of the full per-step trace with no lag cap
+    e, sps, capped = logged_ess(ll_trace)
+    e_full = ess(ll_trace, max_lag=None)
     acc = out["accept"].float().mean().item()
-    t = torch.tensor([wall, ev0.elapsed_time(ev1) / 1e3, float(e.sum()), drift, acc],
-                     dtype=torch.float64, device=dev)
+    t = torch.tensor([wall, ev0.elapsed_time(ev1) / 1e3, float(e.sum()), drift, acc,
+                      float(e_full.sum()), float(capped.sum())], dtype=torch.float64, device=dev)
     if world > 1:
         red = t.clone()
         _all_reduce(red, dist.ReduceOp.MAX)
         sm = t.clone()
         _all_reduce(sm, dist.ReduceOp.SUM)
-        t = torch.stack([red[0], red[1], sm[2], red[3], sm[4] / world])
-    wall_max, dev_s, ess_tot, drift_max, acc_mean = (float(v) for v in t)
+        t = torch.stack([red[0], red[1], sm[2], red[3], sm[4] / world, sm[5], sm[6]])
+    wall_max, dev_s, ess_tot, drift_max, acc_mean, ess_full_tot, n_capped = (float(v) for v in t)
     return {
         "mh_steps_per_sec": B * K * world / wall_max,
         "ess_per_sec": ess_tot / wall_max,
         "ess_total": ess_tot,
         "ess_per_chain_mean": ess_tot / (B * world),
+        "ess_trace": f"Tracer ESS (lag cap 2000 samples) of the log-likelihood samples the reference "
+                     f"logs: every {sps}-th step of {K} (N_SAMPLES 1000, mcmc_generative.py:205-218)",
+        "ess_capped_chains": int(n_capped),
+        "ess_full_trace_per_sec": ess_full_tot / wall_max,
+        "ess_full_trace_per_chain_mean": ess_full_tot / (B * world),
         "chains": B * world,
         "steps": K,
         "burnin": args.mh_burnin,
@@ -307,7 +377,7 @@ def source_sampler_leg(shape, B, K, burnin, seed, rank=0, world=1, device=0):
     import torch.distributed as dist
     from scipy.spatial import Delaunay
     from contact_zones_amd import packing
-    from contact_zones_amd.diagnostics import ess
+    from contact_zones_amd.diagnostics import logged_ess
     from contact_zones_amd.likelihood import LikelihoodEngine
     from contact_zones_amd.mcmc import InitialSamples
     from contact_zones_amd.sampler import ChainState, Sampler, precisions
@@ -356,7 +426,7 @@ def source_sampler_leg(shape, B, K, burnin, seed, rank=0, world=1, device=0):
     status = out["status"].cpu().numpy()
     if np.any(status != 0):
         raise SystemExit(f"source-mode leg: chain status {np.unique(status)}")
-    e = ess(out["ll"].cpu().numpy())
+    e = logged_ess(out["ll"].cpu().numpy())[0]
     acc = out["accept"].float().mean().item()
     t = torch.tensor([wall, float(e.sum()), acc], dtype=torch.float64, device=torch.device("cuda", device))
     if world > 1:
@@ -390,7 +460,7 @@ def real_data_leg(name, n_zones_list, B, K, burnin, seed, rank=0, world=1, devic
     import torch
     import torch.distributed as dist
     from contact_zones_amd import experiment, packing
-    from contact_zones_amd.diagnostics import ess
+    from contact_zones_amd.diagnostics import logged_ess
     from contact_zones_amd.likelihood import LikelihoodEngine
     from contact_zones_amd.mcmc import InitialSamples
     from contact_zones_amd.sampler import ChainState, Sampler, precisions
@@ -440,7 +510,7 @@ def real_data_leg(name, n_zones_list, B, K, burnin, seed, rank=0, world=1, devic
         status = res["status"].cpu().numpy()
         if np.any(status != 0):
             raise SystemExit(f"{name} leg: chain status {np.unique(status)}")
-        e = ess(res["ll"].cpu().numpy())
+        e = logged_ess(res["ll"].cpu().numpy())[0]
         tt = torch.tensor([wall, float(e.sum()), res["accept"].float().mean().item()],
                           dtype=torch.float64, device=torch.device("cuda", device))
         if world > 1:
@@ -510,17 +580,49 @@ def source_lik_leg(args, eng, gen, dev, stream, rank, world):
             "bytes_per_eval": P + D / B, "bytes_per_launch": per_launch,
             "achieved_GBs": per_launch / launch_s / 1e9,
             "frac": per_launch / launch_s / 1e9 / HBM_PEAK_GBS, "steps": K,
-            "kernels": "repack_source_kernel (row codes) + lik_source_rc_kernel"}
+            "kernels": eng.last_kernels()}
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def self_launch(n):
+    """`bench.py --gpus N` started directly (no WORLD_SIZE): run the same command as N ranks under
+    torch.distributed.run, one per GPU, as a child process (nothing here has touched the GPU), and
+    exit with its status.  Rank 0 prints the JSON line."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
 
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        raise SystemExit(self_launch(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus > 1 must be launched with torch.distributed.run")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
+    if args.launch_check:  # the launch path alone (CPU, gloo): ranks meet and report
+        import torch
+        import torch.distributed as dist
+        if world > 1:
+            dist.init_process_group("gloo")
+        t = torch.tensor([float(rank), 1.0])
+        if world > 1:
+            dist.all_reduce(t)
+            dist.destroy_process_group()
+        if rank == 0:
+            print(json.dumps({"launch_check": True, "world_size": world, "rank_sum": int(t[0]),
+                              "ranks": int(t[1])}), flush=True)
+        return
 
     import numpy as np
     import torch

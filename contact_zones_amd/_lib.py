@@ -54,6 +54,26 @@ class sbz_chains(ctypes.Structure):
                 ("alias_p_zones", ctypes.c_void_p), ("alias_p_fam", ctypes.c_void_p)]
 
 
+class sbz_state(ctypes.Structure):
+    """Host arrays of a host-form sampler run (sbz_mh_run, include/sbz.h)."""
+    _fields_ = [("zone_of_site", ctypes.c_void_p), ("w", ctypes.c_void_p),
+                ("p_global", ctypes.c_void_p), ("p_zones", ctypes.c_void_p),
+                ("p_fam", ctypes.c_void_p), ("source", ctypes.c_void_p), ("ll", ctypes.c_void_p),
+                ("prior", ctypes.c_void_p), ("max_size", ctypes.c_void_p),
+                ("p_grow_connected", ctypes.c_void_p), ("chain_id0", ctypes.c_uint64),
+                ("counter", ctypes.c_void_p), ("accepted", ctypes.c_void_p),
+                ("proposed", ctypes.c_void_p), ("status", ctypes.c_void_p)]
+
+
+class sbz_tape(ctypes.Structure):
+    _fields_ = [("values", ctypes.c_void_p), ("stride", ctypes.c_int64), ("len", ctypes.c_void_p),
+                ("pos", ctypes.c_void_p)]
+
+
+class sbz_trace(ctypes.Structure):
+    _fields_ = [("op", ctypes.c_void_p), ("accept", ctypes.c_void_p), ("ll", ctypes.c_void_p)]
+
+
 # name -> (restype, argtypes); every symbol declared in include/sbz.h
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -78,7 +98,10 @@ SIGNATURES = {
     "sbz_set_geo_prior": (_I, [_P, _P, ctypes.c_double]),
     "sbz_set_gibbs_counts": (_I, [_P, _P, _P]),
     "sbz_mh_run_device": (_I, [_P, _I, _I, ctypes.POINTER(sbz_mh_config), ctypes.POINTER(sbz_chains)]),
+    "sbz_mh_run": (_I, [_P, _I, _I, ctypes.POINTER(sbz_mh_config), ctypes.c_uint64,
+                        ctypes.POINTER(sbz_tape), ctypes.POINTER(sbz_state), ctypes.POINTER(sbz_trace)]),
     "sbz_mh_lds_bytes": (ctypes.c_uint64, [ctypes.POINTER(sbz_dims)]),
+    "sbz_last_kernels": (ctypes.c_char_p, [_P]),
 }
 
 _lib = None

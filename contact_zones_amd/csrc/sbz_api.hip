@@ -264,6 +264,7 @@ void sbz_close(sbz_ctx *ctx) {
     free_buf(ctx->nzs);
     free_buf(ctx->partial);
     free_buf(ctx->zflag);
+    free_buf(ctx->mh_stage);
     free_buf(ctx->src_t);
     free_buf(ctx->src_cand);
     free_buf(ctx->ticket);
@@ -518,6 +519,115 @@ int sbz_mh_run_device(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg
     if (!cfg || !chains || B < 0 || n_steps < 0) return fail(ctx, SBZ_EINVAL, "bad sampler arguments");
     (void)hipSetDevice(ctx->device);
     return launch_mh(ctx, B, n_steps, cfg, chains);
+}
+
+const char *sbz_last_kernels(const sbz_ctx *ctx) { return ctx ? ctx->last_kernels.c_str() : ""; }
+
+int sbz_mh_run(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg, uint64_t seed,
+               const sbz_tape *tape, sbz_state *st, sbz_trace *tr) {
+    if (!ctx) return SBZ_EINVAL;
+    if (!cfg || !st || B < 0 || n_steps < 0) return fail(ctx, SBZ_EINVAL, "bad sampler arguments");
+    if (B == 0) return SBZ_OK;
+    const sbz_dims &d = ctx->d;
+    const size_t N = d.n_sites, F = d.n_features, S = d.n_states, Z = d.n_zones, Fam = d.n_families;
+    const bool inh = ctx->C == 3, src = cfg->sample_source != 0;
+    if (!st->zone_of_site || !st->w || !st->p_global || (Z > 0 && !st->p_zones) || !st->ll ||
+        !st->max_size || !st->p_grow_connected || (inh && Fam > 0 && !st->p_fam) || (src && !st->source))
+        return fail(ctx, SBZ_EINVAL, "sbz_state: a required array is NULL");
+    if (tape && (!tape->values || !tape->len || tape->stride <= 0))
+        return fail(ctx, SBZ_EINVAL, "sbz_tape: values, len and stride > 0 are required");
+    for (size_t i = 0; i < (size_t)B * N; i++)
+        if (st->zone_of_site[i] != SBZ_NONE && st->zone_of_site[i] >= Z)
+            return fail(ctx, SBZ_EINVAL, "zone_of_site holds an index >= n_zones");
+    if (src)
+        for (size_t i = 0; i < (size_t)B * N * F; i++)
+            if (st->source[i] >= (unsigned)ctx->C) return fail(ctx, SBZ_EINVAL, "source holds a component index >= C");
+    (void)hipSetDevice(ctx->device);
+    // one staging buffer: every array at a 256-B aligned offset
+    const size_t K = SBZ_N_OPS, T = (size_t)n_steps;
+    struct Part { const void *host; size_t bytes; bool in; void *out; size_t off; };
+    std::vector<Part> parts;
+    auto part = [&](const void *h, size_t bytes, bool in, void *out) {
+        parts.push_back({h, bytes, in, out, 0});
+        return parts.size() - 1;
+    };
+    const size_t izos = part(st->zone_of_site, (size_t)B * N, true, st->zone_of_site);
+    const size_t iw = part(st->w, (size_t)B * F * ctx->C * 8, true, st->w);
+    const size_t ig = part(st->p_global, (size_t)B * F * S * 8, true, st->p_global);
+    const size_t iz = part(st->p_zones, (size_t)B * Z * F * S * 8, true, st->p_zones);
+    const size_t ifm = part(st->p_fam, inh ? (size_t)B * Fam * F * S * 8 : 0, true, st->p_fam);
+    const size_t isrc = part(st->source, src ? (size_t)B * N * F : 0, true, st->source);
+    const size_t ill = part(nullptr, (size_t)B * 8, false, st->ll);
+    const size_t ipr = part(st->prior, st->prior ? (size_t)B * 8 : 0, true, st->prior);
+    const size_t ims = part(st->max_size, (size_t)B * 4, true, nullptr);
+    const size_t ipg = part(st->p_grow_connected, (size_t)B * 8, true, nullptr);
+    const size_t ictr = part(st->counter, (size_t)B * 8, st->counter != nullptr, st->counter);
+    const size_t iacc = part(st->accepted, (size_t)B * K * 8, st->accepted != nullptr, st->accepted);
+    const size_t iprp = part(st->proposed, (size_t)B * K * 8, st->proposed != nullptr, st->proposed);
+    const size_t ista = part(nullptr, (size_t)B * 4, false, st->status);
+    const size_t itv = part(tape ? tape->values : nullptr, tape ? (size_t)B * tape->stride * 8 : 0, true, nullptr);
+    const size_t itl = part(tape ? tape->len : nullptr, tape ? (size_t)B * 8 : 0, true, nullptr);
+    const size_t itp = part(tape ? tape->pos : nullptr, tape ? (size_t)B * 8 : 0, tape && tape->pos, tape ? tape->pos : nullptr);
+    const bool trace = tr && tr->op && tr->accept && tr->ll;
+    const size_t iop = part(nullptr, trace ? (size_t)B * T : 0, false, trace ? tr->op : nullptr);
+    const size_t iac = part(nullptr, trace ? (size_t)B * T : 0, false, trace ? tr->accept : nullptr);
+    const size_t itll = part(nullptr, trace ? (size_t)B * T * 8 : 0, false, trace ? tr->ll : nullptr);
+    size_t total = 0;
+    for (Part &p : parts) {
+        p.off = total;
+        total += (p.bytes + 255) & ~(size_t)255;
+    }
+    int rc = ensure(ctx, ctx->mh_stage, total);
+    if (rc) return rc;
+    char *base = static_cast<char *>(ctx->mh_stage.ptr);
+    hipStream_t s = ctx->stream;
+    hipError_t e = hipMemsetAsync(base, 0, total, s);  // counters / cursors / outputs start at 0
+    for (const Part &p : parts)
+        if (e == hipSuccess && p.in && p.host && p.bytes)
+            e = hipMemcpyAsync(base + p.off, p.host, p.bytes, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return hip_fail(ctx, e, "sbz_mh_run: H2D");
+    auto dp = [&](size_t i) -> void * { return parts[i].bytes ? base + parts[i].off : nullptr; };
+    // the chains' log-likelihood from the staged state
+    rc = launch_loglik(ctx, B, static_cast<uint8_t *>(dp(izos)), static_cast<double *>(dp(iw)),
+                       static_cast<double *>(dp(ig)), static_cast<double *>(dp(iz)),
+                       static_cast<double *>(dp(ifm)), src ? static_cast<uint8_t *>(dp(isrc)) : nullptr,
+                       static_cast<double *>(dp(ill)));
+    if (rc) return rc;
+    sbz_chains ch{};
+    ch.zone_of_site = static_cast<uint8_t *>(dp(izos));
+    ch.w = static_cast<double *>(dp(iw));
+    ch.p_global = static_cast<double *>(dp(ig));
+    ch.p_zones = static_cast<double *>(dp(iz));
+    ch.p_fam = static_cast<double *>(dp(ifm));
+    ch.source = src ? static_cast<uint8_t *>(dp(isrc)) : nullptr;
+    ch.ll = static_cast<double *>(dp(ill));
+    ch.prior = static_cast<double *>(dp(ipr));
+    ch.max_size = static_cast<const int32_t *>(dp(ims));
+    ch.p_grow_connected = static_cast<const double *>(dp(ipg));
+    ch.seed = seed;
+    ch.chain_id0 = st->chain_id0;
+    ch.counter = static_cast<uint64_t *>(dp(ictr));
+    ch.accepted = static_cast<int64_t *>(dp(iacc));
+    ch.proposed = static_cast<int64_t *>(dp(iprp));
+    ch.status = static_cast<int32_t *>(dp(ista));
+    if (tape) {
+        ch.tape = static_cast<const double *>(dp(itv));
+        ch.tape_stride = tape->stride;
+        ch.tape_len = static_cast<const int64_t *>(dp(itl));
+        ch.tape_pos = static_cast<int64_t *>(dp(itp));
+    }
+    if (trace) {
+        ch.trace_op = static_cast<int8_t *>(dp(iop));
+        ch.trace_accept = static_cast<uint8_t *>(dp(iac));
+        ch.trace_ll = static_cast<double *>(dp(itll));
+    }
+    rc = launch_mh(ctx, B, n_steps, cfg, &ch);
+    if (rc) return rc;
+    for (const Part &p : parts)
+        if (e == hipSuccess && p.out && p.bytes)
+            e = hipMemcpyAsync(p.out, base + p.off, p.bytes, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    return e == hipSuccess ? SBZ_OK : hip_fail(ctx, e, "sbz_mh_run: D2H");
 }
 
 uint64_t sbz_mh_lds_bytes(const sbz_dims *dims) {

@@ -92,6 +92,8 @@ struct sbz_ctx {
     int n_cu = 256;        // compute units of the device
     int src_waves = 0;     // SBZ_SRC_WAVES: waves per chain of the source-mode sampler (0: by N x F)
     int src_hbm = 0;       // SBZ_SRC_HBM=1: source-mode sampler keeps sources in HBM even when they fit LDS
+    std::string last_kernels;  // sbz_last_kernels
+    sbz::DevBuf mh_stage;      // host-form sampler staging (sbz_mh_run)
     sbz::DevBuf partial, ticket, zflag, src_t, zl, nzs, stage, out, src_cand, flags;
     std::string err;
 };

@@ -2730,6 +2730,11 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
         if (ctx->zflag.ptr) (void)hipMemsetAsync(ctx->zflag.ptr, 0, ctx->zflag.bytes, st);
         return hip_fail(ctx, e, what);
     };
+    ctx->last_kernels = src_rc ? "repack_source_kernel lik_source_rc_kernel"
+                      : src_mode ? "repack_source_kernel lik_source_kernel"
+                      : !plan.fr ? "lik_mixture_generic_kernel"
+                      : zd ? "lik_zdirect_kernel" : zoned ? "zone_list_kernel lik_zoned_kernel"
+                      : ws ? "lik_mixture_ws_kernel" : "lik_mixture_kernel";
     if (src_rc) {
         void *args[] = {&a};
         hipError_t e = hipLaunchKernel(mix_fn, grid, dim3(WAVE), args, lds, st);

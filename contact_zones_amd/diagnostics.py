@@ -20,16 +20,20 @@ def autocovariance(x):
     return acov / (n - np.arange(n))
 
 
-def ess(x, max_lag=2000):
-    """ESS of each trace in x (shape [..., n]); 0 for a constant trace."""
+def ess(x, max_lag=2000, return_capped=False):
+    """ESS of each trace in x (shape [..., n]); 0 for a constant trace.  max_lag=None: no cap
+    beyond the trace length.  return_capped: also a bool array, True where the pair sum was still
+    positive at the cap (the ESS is then an upper bound, not a mixing measurement)."""
     x = np.asarray(x, np.float64)
     flat = x.reshape(-1, x.shape[-1])
     n = flat.shape[1]
     out = np.zeros(flat.shape[0])
+    capped = np.zeros(flat.shape[0], bool)
     if n < 2:
-        return out.reshape(x.shape[:-1])
+        return (out.reshape(x.shape[:-1]), capped.reshape(x.shape[:-1])) if return_capped \
+            else out.reshape(x.shape[:-1])
     g = autocovariance(flat)
-    lag_cap = min(n - 1, max_lag)
+    lag_cap = n - 1 if max_lag is None else min(n - 1, max_lag)
     for i in range(flat.shape[0]):
         gi = g[i]
         if not gi[0] > 0:
@@ -42,5 +46,26 @@ def ess(x, max_lag=2000):
                 break
             var += 2.0 * pair
             lag += 2
+        capped[i] = lag >= lag_cap and lag_cap < n - 1
         out[i] = n * gi[0] / var
+    if return_capped:
+        return out.reshape(x.shape[:-1]), capped.reshape(x.shape[:-1])
     return out.reshape(x.shape[:-1])
+
+
+def logged_trace(trace, n_samples=1000):
+    """The samples the reference logs from a per-step trace [..., n_steps]: after every step i
+    with i % ceil(n_steps / n_samples) == 0 (MCMCGenerative.generate_samples,
+    sbayes/sampling/mcmc_generative.py:205-218; N_SAMPLES 1000 in config/default_config.json)."""
+    trace = np.asarray(trace)
+    sps = int(np.ceil(trace.shape[-1] / n_samples))
+    return trace[..., ::sps], sps
+
+
+def logged_ess(trace, n_samples=1000, max_lag=2000):
+    """Tracer's ESS (its lag cap, 2000 samples) of the log-likelihood samples the reference would
+    log from this per-step trace, in units of logged samples, plus the thinning step and the
+    chains whose estimate hit the cap."""
+    logged, sps = logged_trace(trace, n_samples)
+    e, capped = ess(logged, max_lag, return_capped=True)
+    return e, sps, capped

@@ -66,6 +66,10 @@ class LikelihoodEngine:
     def synchronize(self):
         check(self._lib.sbz_synchronize(self.ctx), self.ctx)
 
+    def last_kernels(self):
+        """Names of the kernels the last likelihood launch ran (sbz_last_kernels)."""
+        return self._lib.sbz_last_kernels(self.ctx).decode()
+
     def lds_bytes(self, source_mode=False):
         return int(self._lib.sbz_lik_lds_bytes(ctypes.byref(self.dims), int(bool(source_mode))))
 

@@ -16,7 +16,7 @@ import ctypes
 
 import numpy as np
 
-from ._lib import check, sbz_chains, sbz_mh_config
+from ._lib import check, sbz_chains, sbz_mh_config, sbz_state, sbz_tape, sbz_trace
 
 OPS = ["shrink_zone", "grow_zone", "swap_zone", "alter_weights", "alter_p_global",
        "alter_p_zones", "alter_p_families", "gibbsish_sample_zones",
@@ -264,3 +264,62 @@ class Sampler:
                                          ctypes.byref(ch)), eng.ctx)
         out["_keep"] = keep  # the launch is asynchronous: keep its inputs alive
         return out
+
+
+def run_host(sampler, state, n_steps, max_size, p_grow_connected, seed=0, chain_id0=0, tape=None,
+             tape_len=None, trace=False):
+    """The host-form sampler entry (sbz_mh_run): `state` is a dict of numpy arrays (zone_of_site,
+    w, p_global, p_zones, p_fam, source, prior, counter, accepted, proposed), updated in place
+    except for 'll' and 'status', which are (re)filled.  No torch tensors are involved: this is
+    what a reference-side ctypes binding without a device allocator calls."""
+    eng = sampler.engine
+    B = int(np.asarray(state["zone_of_site"]).shape[0])
+    keep = []
+
+    def arr(name, dtype, shape=None, fill=None):
+        a = state.get(name)
+        if a is None:
+            if fill is None:
+                return None
+            a = np.full(shape, fill, dtype)
+        a = np.ascontiguousarray(a, dtype)
+        state[name] = a
+        keep.append(a)
+        return a.ctypes.data
+
+    st = sbz_state()
+    st.zone_of_site = arr("zone_of_site", np.uint8)
+    st.w = arr("w", np.float64)
+    st.p_global = arr("p_global", np.float64)
+    st.p_zones = arr("p_zones", np.float64)
+    st.p_fam = arr("p_fam", np.float64) if eng.inheritance else None
+    st.source = arr("source", np.uint8) if sampler.sample_source else None
+    st.ll = arr("ll", np.float64, (B,), 0.0)
+    st.prior = arr("prior", np.float64)
+    ms = np.ascontiguousarray(np.broadcast_to(np.asarray(max_size, np.int32), (B,)))
+    pg = np.ascontiguousarray(np.broadcast_to(np.asarray(p_grow_connected, np.float64), (B,)))
+    keep += [ms, pg]
+    st.max_size = ms.ctypes.data
+    st.p_grow_connected = pg.ctypes.data
+    st.chain_id0 = int(chain_id0)
+    st.counter = arr("counter", np.uint64, (B,), 0)
+    st.accepted = arr("accepted", np.int64, (B, N_OPS_MAX), 0)
+    st.proposed = arr("proposed", np.int64, (B, N_OPS_MAX), 0)
+    st.status = arr("status", np.int32, (B,), 0)
+    tp = None
+    if tape is not None:
+        tv = np.ascontiguousarray(tape, np.float64)
+        tl = np.ascontiguousarray(tape_len, np.int64)
+        pos = arr("tape_pos", np.int64, (B,), 0)
+        keep += [tv, tl]
+        tp = sbz_tape(tv.ctypes.data, int(tv.shape[1]), tl.ctypes.data, pos)
+    tr = None
+    out = {}
+    if trace:
+        out = {"op": np.zeros((B, n_steps), np.int8), "accept": np.zeros((B, n_steps), np.uint8),
+               "ll": np.zeros((B, n_steps), np.float64)}
+        tr = sbz_trace(out["op"].ctypes.data, out["accept"].ctypes.data, out["ll"].ctypes.data)
+    check(eng._lib.sbz_mh_run(eng.ctx, B, int(n_steps), ctypes.byref(sampler.cfg),
+                              int(seed) & (2**64 - 1), ctypes.byref(tp) if tp is not None else None,
+                              ctypes.byref(st), ctypes.byref(tr) if tr is not None else None), eng.ctx)
+    return out

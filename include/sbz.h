@@ -9,7 +9,7 @@
  *       replaces  Likelihood.__call__(sample, caching=False)      sbayes/model.py:145-171
  *       (incl.    update_component_likelihoods :230-249, update_weights :257-294,
  *                 normalize_weights :436-452, combine_lh :173-184)  — B chains per call
- *   sbz_set_network / sbz_mh_run_device
+ *   sbz_set_network / sbz_mh_run (host arrays) / sbz_mh_run_device
  *       replaces  MCMCGenerative.step (the generate_samples hot loops) sbayes/sampling/mcmc_generative.py:149-351
  *       with the  operators of ZoneMCMC / ZoneMCMCWarmup           sbayes/sampling/zone_sampling.py:408-933,1272-1577
  *
@@ -124,11 +124,16 @@ int sbz_memcpy_d2h(sbz_ctx *ctx, void *dst, const void *src, uint64_t bytes);
 /* Bytes of LDS the likelihood kernel needs per workgroup for these dims (0 if unsupported). */
 uint64_t sbz_lik_lds_bytes(const sbz_dims *dims, int source_mode);
 
+/* Diagnostics: the kernels the context's last likelihood launch ran, space-separated (e.g.
+ * "repack_source_kernel lik_source_rc_kernel"), "" before the first. */
+const char *sbz_last_kernels(const sbz_ctx *ctx);
+
 /* ------------------------------------------------------------------------------------------
  * Metropolis-Hastings sampler  (MCMCGenerative.step, sbayes/sampling/mcmc_generative.py:282-351,
  * operators of ZoneMCMC / ZoneMCMCWarmup, sbayes/sampling/zone_sampling.py:408-933, 1272-1577;
- * SAMPLE_SOURCE = false; zero, 'counts' and zone-size priors).  One wave runs one chain for
- * n_steps in one launch.
+ * SAMPLE_SOURCE = false (sbz_mh.hip) and true (sbz_mh_src.hip); zero, 'counts', zone-size and
+ * 'cost_based' geo priors).  One workgroup (4 waves; SAMPLE_SOURCE = true: 8) runs one chain
+ * for n_steps in one launch.
  * ------------------------------------------------------------------------------------------ */
 
 /* Canonical operator order of sbz_mh_config.op_prob. */
@@ -227,6 +232,43 @@ int sbz_set_gibbs_counts(sbz_ctx *ctx, const double *counts_global, const double
 /* Run n_steps MH steps on B device-resident chains; asynchronous on ctx's stream. */
 int sbz_mh_run_device(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg,
                       const sbz_chains *chains);
+
+/* ---- Host-form sampler (SURVEY.md §8b's sbz_mh_run): the same run on HOST arrays, for a
+ * reference-side binding without a device allocator (ctypes + numpy only).  The state is staged
+ * to the device, each chain's log-likelihood is evaluated from it (the reference's initial
+ * _ll[c] = likelihood(sample), mcmc_generative.py:159-170), the chains run n_steps steps, and the
+ * state, counters and traces are copied back.  Blocks until done. ---- */
+typedef struct sbz_state {
+    uint8_t *zone_of_site;            /* [B][N] in/out */
+    double *w, *p_global, *p_zones, *p_fam;  /* in/out, layouts as sbz_loglik_batch */
+    uint8_t *source;                  /* [B][N][F] in/out with cfg->sample_source, else NULL */
+    double *ll;                       /* [B] out: each chain's log-likelihood after the run */
+    double *prior;                    /* [B] in/out log prior (sbz_set_priors), or NULL when every
+                                         prior term is 0 */
+    const int32_t *max_size;          /* [B] MAX_M per chain */
+    const double *p_grow_connected;   /* [B] */
+    uint64_t chain_id0;               /* global id of chain 0 (Philox key) */
+    uint64_t *counter;                /* [B] in/out Philox counters, or NULL (start at 0) */
+    int64_t *accepted, *proposed;     /* [B][SBZ_N_OPS] accumulated, or NULL */
+    int32_t *status;                  /* [B] out (1 = tape exhausted), or NULL */
+} sbz_state;
+
+typedef struct sbz_tape {             /* replay of the reference's recorded decisions */
+    const double *values;             /* [B][stride] (tests/golden/make_golden_mh.py) */
+    int64_t stride;
+    const int64_t *len;               /* [B] */
+    int64_t *pos;                     /* [B] in/out cursor, or NULL (start at 0) */
+} sbz_tape;
+
+typedef struct sbz_trace {            /* per-step trace, [B][n_steps] each, or NULL members */
+    int8_t *op;                       /* operator (sbz_op) */
+    uint8_t *accept;
+    double *ll;                       /* log-likelihood after the step */
+} sbz_trace;
+
+/* tape == NULL: Philox4x32-10 draws keyed by (seed, chain_id0 + b, counter[b]). */
+int sbz_mh_run(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg, uint64_t seed,
+               const sbz_tape *tape, sbz_state *io_state, sbz_trace *out_trace);
 
 /* Bytes of LDS the sampler needs per chain for these dims (0 if above the 64 KiB limit). */
 uint64_t sbz_mh_lds_bytes(const sbz_dims *dims);

@@ -184,3 +184,54 @@ def test_philox_large_shapes_carried_ll(gpu_available, N, F, S, Z, Fam, inh):
         assert np.all(sizes >= 3) and np.all(sizes <= 40)
     np.testing.assert_allclose(s["w"].sum(-1), 1.0, rtol=1e-12)
     np.testing.assert_allclose(s["p_zones"].sum(-1), 1.0, rtol=1e-12)
+
+
+@pytest.mark.parametrize("case", ["mh_small_priors", "mh_cfg1_sim_inh_z2"])
+def test_host_form_run_replays_reference(gpu_available, case):
+    """sbz_mh_run (SURVEY.md §8b's host-form entry: numpy arrays in, numpy arrays out, no device
+    buffers on the caller's side) replays the reference's decision tape exactly as the device
+    entry does: operators, accepts, final zones and parameters, ll within 1e-9."""
+    from contact_zones_amd.sampler import run_host
+    fx = load_golden(case)
+    eng, smp, st = _setup(fx)
+    n_steps = fx["step_op"].shape[1]
+    inh = bool(fx["inheritance"])
+    host = {"zone_of_site": fx["init_zone_of_site"].copy(), "w": fx["init_w"].copy(),
+            "p_global": fx["init_p_global"].copy(), "p_zones": fx["init_p_zones"].copy(),
+            "p_fam": fx["init_p_fam"].copy() if inh else None,
+            "prior": np.broadcast_to(np.asarray(fx["init_prior"], np.float64), (st.B,)).copy()}
+    tr = run_host(smp, host, n_steps, fx["max_size"], fx["p_grow_connected"], tape=fx["tape"],
+                  tape_len=fx["tape_len"], trace=True)
+    assert host["status"].tolist() == [0] * st.B
+    np.testing.assert_array_equal(host["tape_pos"], fx["tape_len"])
+    np.testing.assert_array_equal(tr["op"], fx["step_op"])
+    np.testing.assert_array_equal(tr["accept"].astype(bool), fx["step_accept"])
+    np.testing.assert_array_equal(host["zone_of_site"], fx["step_zone_of_site"][:, -1])
+    assert np.max(np.abs(tr["ll"] - fx["step_ll"]) / np.abs(fx["step_ll"])) <= REL_TOL
+    # the device entry on the same inputs ends in the same state, bit for bit
+    out = smp.run(st, n_steps, fx["max_size"], fx["p_grow_connected"], tape=fx["tape"],
+                  tape_len=fx["tape_len"], trace=True)
+    dev = st.to_numpy()
+    for k in ("zone_of_site", "w", "p_global", "p_zones", "ll", "prior") + (("p_fam",) if inh else ()):
+        np.testing.assert_array_equal(host[k], dev[k], err_msg=k)
+    np.testing.assert_array_equal(tr["ll"], out["ll"].cpu().numpy())
+    np.testing.assert_array_equal(host["proposed"], st.proposed.cpu().numpy())
+
+
+def test_host_form_philox_matches_device_form(gpu_available):
+    """Philox draws: host-form and device-form runs of the same chains, seed and chain ids are
+    bit-identical, including the counters a continued run starts from."""
+    from contact_zones_amd.sampler import run_host
+    fx = load_golden("mh_small_priors")
+    eng, smp, st = _setup(fx)
+    inh = bool(fx["inheritance"])
+    host = {k: v.copy() for k, v in st.to_numpy().items() if k != "ll"}
+    for _ in range(2):
+        run_host(smp, host, 300, fx["max_size"], fx["p_grow_connected"], seed=77, chain_id0=5)
+        st.refresh_ll()  # sbz_mh_run starts every run from a full evaluation of the state
+        out = smp.run(st, 300, fx["max_size"], fx["p_grow_connected"], seed=77, chain_id0=5)
+    assert host["status"].tolist() == out["status"].cpu().numpy().tolist() == [0] * st.B
+    dev = st.to_numpy()
+    for k in ("zone_of_site", "w", "p_global", "p_zones", "ll", "prior") + (("p_fam",) if inh else ()):
+        np.testing.assert_array_equal(host[k], dev[k], err_msg=k)
+    np.testing.assert_array_equal(host["counter"], st.counter.cpu().numpy())

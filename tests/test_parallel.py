@@ -80,3 +80,31 @@ def test_collectives_world_size_2():
         assert o["bcast"][1] == ("|b1", (1, 2), [[True, False]])
         assert o["bcast"][2][1] == (0, 3)
         assert o["gather"] == np.arange(70, dtype=np.float64).reshape(7, 10).tolist()
+
+
+def test_bench_self_launch_two_ranks():
+    """`bench.py --gpus 2` without WORLD_SIZE starts its own two ranks (torch.distributed.run as
+    a child process, no exec) and prints rank 0's line; --launch-check stops after the ranks met
+    over gloo, so this runs on the CPU."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--launch-check"],
+                       capture_output=True, text=True, timeout=180, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line == {"launch_check": True, "world_size": 2, "rank_sum": 1, "ranks": 2}
+
+
+def test_bench_cpu_baseline_processes():
+    """The CPU baseline runs one spawned single-threaded process per core and reports per-core and
+    all-core rates, here on a small shape."""
+    import argparse
+    import bench
+    args = argparse.Namespace(sites=200, features=40, states=5, zones=2, families=2, zone_size=20,
+                              seed=3, cpu_procs=2)
+    r = bench.cpu_baseline(args, 0.5)
+    assert r["cores"] == 2 and r["kind"] == "port" and r["host_cpu_count"] == os.cpu_count()
+    assert r["value"] > 0 and abs(r["per_core"] * 2 - r["value"]) < 1e-9 * r["value"]
