@@ -79,14 +79,16 @@ def _iter_items(d, prefix=""):
             yield prefix + k, v
 
 
-def load_config(config_file, custom_settings=None):
-    """The reference's load_config + verify_config for data-based experiments: returns the
-    verified config (paths made relative to the config's directory) and that directory."""
+def load_config(config_file, custom_settings=None, simulated=False):
+    """The reference's load_config + verify_config: returns the verified config (paths made
+    relative to the config's directory) and that directory.  A simulation config (a 'simulation'
+    section, experiments/simulation/*/config.json) needs `simulated=True`: its data then come as
+    SimulatedData (the runner's --sim-data), since simulating them is not part of this path."""
     base = os.path.dirname(os.path.abspath(config_file))
     with open(config_file) as f:
         cfg = json.load(f)
-    if "simulation" in cfg:
-        raise NotImplementedError("simulation experiments are not supported by this runner")
+    if "simulation" in cfg and not simulated:
+        raise NotImplementedError("simulation config: pass the simulated data (--sim-data, SimulatedData)")
     data = cfg.setdefault("data", {})
     for low, up in (("features", "FEATURES"), ("feature_states", "FEATURE_STATES")):
         if low in data and up not in data:  # experiments/balkan/config.json spells them lowercase
@@ -94,6 +96,10 @@ def load_config(config_file, custom_settings=None):
     set_defaults(cfg, DEFAULT_CONFIG)
     if custom_settings:
         update_recursive(cfg, custom_settings)
+    if simulated:  # the data come from the simulation (Simulation, not read from files)
+        for k in ("FEATURES", "FEATURE_STATES"):
+            if data.get(k) == REQUIRED:
+                del data[k]
 
     def fix(p):
         return p if os.path.isabs(p) else os.path.join(base, p)
@@ -137,8 +143,9 @@ def load_config(config_file, custom_settings=None):
     res = cfg.setdefault("results", {})
     res.setdefault("RESULTS_PATH", "results")
     res.setdefault("FILE_INFO", "n")
-    data["FEATURES"] = fix(data["FEATURES"])
-    data["FEATURE_STATES"] = fix(data["FEATURE_STATES"])
+    for k in ("FEATURES", "FEATURE_STATES"):
+        if k in data:
+            data[k] = fix(data[k])
     res["RESULTS_PATH"] = fix(res["RESULTS_PATH"])
     return cfg, base
 
@@ -210,6 +217,66 @@ class ExperimentData:
             self.inheritance_counts, lg = io.read_inheritance_counts(
                 t, pri["inheritance"]["files"], pri["inheritance"]["file_type"], d["FEATURE_STATES"])
             self.log.append(lg)
+
+
+class SimulatedData:
+    """Simulated data with its ground truth, in the attributes of the reference's Simulation
+    (simulation.py:30-160) that MCMC, eval_ground_truth and samples2file read: features, states,
+    names, network, is_simulated = True, and the truth — areas (Z_true, N), weights (F, C),
+    p_universal (F, S), p_contact (Z_true, F, S), p_inheritance (Fam, F, S) or None, families.
+    The simulation itself (simulate_features etc.) is not part of the hot path: the arrays come
+    from the reference's own Simulation or any other source (see from_npz)."""
+
+    def __init__(self, obs, states, locations, areas, weights, p_universal, p_contact,
+                 p_inheritance=None, fam_of_site=None, feature_names=None, state_names=None,
+                 family_names=None, geo_cost=None):
+        import scipy.sparse as sp
+        from . import io, packing
+        obs = np.asarray(obs, np.int8)
+        N, F = obs.shape
+        states = np.asarray(states, bool)
+        S = states.shape[1]
+        fam = np.full(N, 255, np.uint8) if fam_of_site is None else np.asarray(fam_of_site, np.uint8)
+        Fam = int(fam[fam != 255].max()) + 1 if np.any(fam != 255) else 0
+        feature_names = list(feature_names) if feature_names is not None else [f"f{f + 1}" for f in range(F)]
+        state_names = ([list(x) for x in state_names] if state_names is not None else
+                       [[f"s{x + 1}" for x in range(int(states[f].sum()))] for f in range(F)])
+        family_names = list(family_names) if family_names is not None else [f"fam{i + 1}" for i in range(Fam)]
+        self.table = types.SimpleNamespace(
+            obs=obs, applicable=states, fam_of_site=fam, n_sites=N, n_features=F, n_states=S,
+            feature_names=feature_names, state_names=state_names, family_names=family_names,
+            locations=np.asarray(locations, np.float64))
+        self.features = packing.obs_to_features(obs, S)
+        self.states = states
+        self.families = packing.index_to_groups(fam, Fam) if Fam else np.zeros((0, N), bool)
+        self.feature_names = {"external": feature_names, "internal": list(range(F))}
+        self.state_names = {"external": state_names, "internal": [list(range(len(x))) for x in state_names]}
+        self.family_names = {"external": family_names, "internal": list(range(Fam))}
+        indptr, indices, dist = io.compute_network(self.table.locations)
+        self.network = {"adj_mat": sp.csr_matrix((np.ones(indices.size, int), indices, indptr), shape=(N, N)),
+                        "dist_mat": dist, "locations": self.table.locations}
+        self.is_simulated = True
+        self.log = [f"simulated data: {N} sites, {F} features, {np.asarray(areas).shape[0]} true areas"]
+        self.universal_counts = self.inheritance_counts = None
+        self.geo_cost = dist if geo_cost is None else np.asarray(geo_cost, np.float64)
+        self.areas = np.asarray(areas, bool)
+        self.weights = np.asarray(weights, np.float64)
+        self.p_universal = np.asarray(p_universal, np.float64)
+        self.p_contact = np.asarray(p_contact, np.float64)
+        self.p_inheritance = None if p_inheritance is None else np.asarray(p_inheritance, np.float64)
+
+    @classmethod
+    def from_npz(cls, path):
+        """Arrays saved with keys obs, states, locations, areas, weights, p_universal, p_contact
+        [, p_inheritance, fam_of_site, geo_cost] and optional JSON-encoded names ('names':
+        {"features": [...], "states": [[...]], "families": [...]})."""
+        import json
+        with np.load(path, allow_pickle=False) as z:
+            d = {k: z[k] for k in z.files}
+        names = json.loads(str(d.pop("names"))) if "names" in d else {}
+        return cls(d["obs"], d["states"], d["locations"], d["areas"], d["weights"], d["p_universal"],
+                   d["p_contact"], d.get("p_inheritance"), d.get("fam_of_site"), names.get("features"),
+                   names.get("states"), names.get("families"), d.get("geo_cost"))
 
 
 def build_priors(config, data):
@@ -292,7 +359,7 @@ def run_experiment(config, data, n_zones, run=0, name="experiment", seed=None, d
     across ranks); the phases draw from independent streams derived from (seed, run, n_zones)."""
     from . import io
     from .mcmc import BatchedZoneMCMC, BatchedZoneMCMCWarmup
-    from .postprocessing import contribution_per_area, match_areas, rank_areas
+    from .postprocessing import contribution_per_area, eval_ground_truth, match_areas, rank_areas
     logger = logger or logging.getLogger("sbz")
     mc = config["mcmc"]
     cfg = copy.deepcopy(config)
@@ -321,15 +388,28 @@ def run_experiment(config, data, n_zones, run=0, name="experiment", seed=None, d
         return smp.statistics, None
     contribution_per_area(smp)
     stats = rank_areas(match_areas(smp.statistics))
-    fi = {"n": f"n{n_zones}", "i": f"i{int(cfg['model']['INHERITANCE'])}",
-          "p": f"p{0 if cfg['model']['PRIOR']['universal']['type'] == 'uniform' else 1}"}.get(
-              cfg["results"]["FILE_INFO"])
-    if fi is None:
-        raise ValueError("file_info must be 'n', 'i' or 'p'")
+    info = cfg["results"]["FILE_INFO"]
+    if info == "n":
+        fi = f"n{n_zones}"
+    elif info == "s":
+        fi = f"s{cfg['simulation']['STRENGTH']}a{cfg['simulation']['AREA']}"
+    elif info == "i":
+        fi = f"i{int(cfg['model']['INHERITANCE'])}"
+    elif info == "p":
+        # mcmc_setup.py:208 compares the PRIOR['universal'] dict with the string "uniform", which
+        # is never equal: the reference always names these results p1
+        fi = "p1"
+    else:
+        raise ValueError("file_info must be 'n', 's', 'i' or 'p'")
     pth = os.path.join(cfg["results"]["RESULTS_PATH"], name, fi)
     os.makedirs(pth, exist_ok=True)
     paths = {"parameters": os.path.join(pth, f"stats_{fi}_{run}.txt"),
-             "areas": os.path.join(pth, f"areas_{fi}_{run}.txt")}
+             "areas": os.path.join(pth, f"areas_{fi}_{run}.txt"),
+             "gt": os.path.join(pth, "ground_truth", "stats.txt"),
+             "gt_areas": os.path.join(pth, "ground_truth", "areas.txt")}
+    if getattr(data, "is_simulated", False):  # MCMC.save_samples (mcmc_setup.py:227-229)
+        eval_ground_truth(smp, data, bool(cfg["model"]["INHERITANCE"]), stats)
+        os.makedirs(os.path.dirname(paths["gt"]), exist_ok=True)
     io.samples2file(stats, data, cfg, paths)
     logger.info("sampling: %d steps, acceptance %.3f, %.2f s; results in %s", mc["N_STEPS"],
                 stats["acceptance_ratio"], stats["sampling_time"], pth)
@@ -344,13 +424,15 @@ def main(argv=None):
     p.add_argument("--seed", type=int, default=None)
     p.add_argument("--device", type=int, default=None)
     p.add_argument("--set", default=None, help="JSON object merged into the config (custom settings)")
+    p.add_argument("--sim-data", default=None,
+                   help="simulation config: the simulated data and its ground truth (.npz, SimulatedData.from_npz)")
     a = p.parse_args(argv)
     rank, device = init_distributed(a.device)
     logging.basicConfig(level=logging.INFO if rank == 0 else logging.WARNING, format="%(message)s")
     logger = logging.getLogger("sbz")
-    config, _ = load_config(a.config, json.loads(a.set) if a.set else None)
+    config, _ = load_config(a.config, json.loads(a.set) if a.set else None, simulated=a.sim_data is not None)
     name = a.name or time.strftime("%Y%m%d-%H%M%S")
-    data = ExperimentData(config)
+    data = SimulatedData.from_npz(a.sim_data) if a.sim_data else ExperimentData(config)
     for line in data.log:
         logger.info(line)
     n_areas = config["model"]["N_AREAS"]

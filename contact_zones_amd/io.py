@@ -328,14 +328,88 @@ def stats_columns(feature_names, state_names, family_names, n_zones, inheritance
     return cols
 
 
+def _ext(x):
+    return x["external"] if isinstance(x, dict) else x
+
+
+def collect_gt_for_writing(samples, data, config):
+    """util.collect_gt_for_writing (util.py:657-738): the ground-truth row of simulated data —
+    posterior / likelihood / prior, weights, alpha, gamma of every TRUE area (len(data.areas)),
+    beta when the simulation had inheritance (config['simulation']['INHERITANCE']) and the single
+    areas' lh / prior / posterior.  Returns (row dict, column names)."""
+    feature_names = list(_ext(data.feature_names))
+    state_names = [list(s) for s in _ext(data.state_names)]
+    gt = {"posterior": samples["true_prior"] + samples["true_ll"], "likelihood": samples["true_ll"],
+          "prior": samples["true_prior"]}
+    cols = ["posterior", "likelihood", "prior"]
+    tw = samples["true_weights"]
+    for f, fn in enumerate(feature_names):
+        names = ["w_universal_" + str(fn), "w_contact_" + str(fn)]
+        if config["model"]["INHERITANCE"]:
+            names.append("w_inheritance_" + str(fn))
+        for c, name in enumerate(names):
+            if name not in cols:
+                cols.append(name)
+            gt[name] = tw[f][c]
+    pg = samples["true_p_global"][0]
+    for f, fn in enumerate(feature_names):
+        for st in range(len(state_names[f])):
+            name = "alpha_" + str(fn) + "_" + str(state_names[f][st])
+            if name not in cols:
+                cols.append(name)
+            gt[name] = pg[f][st]
+    pz = samples["true_p_zones"]
+    for a in range(len(data.areas)):
+        for f, fn in enumerate(feature_names):
+            for st in range(len(state_names[f])):
+                name = "gamma_a" + str(a + 1) + "_" + str(fn) + "_" + str(state_names[f][st])
+                if name not in cols:
+                    cols.append(name)
+                gt[name] = pz[a][f][st]
+    sim_inh = config.get("simulation", {}).get("INHERITANCE", getattr(data, "p_inheritance", None) is not None)
+    if sim_inh:
+        pf = samples["true_p_families"]
+        for fam, famn in enumerate(_ext(data.family_names)):
+            for f, fn in enumerate(feature_names):
+                for st in range(len(state_names[f])):
+                    name = "beta_" + str(famn) + "_" + str(fn) + "_" + str(state_names[f][st])
+                    if name not in cols:
+                        cols.append(name)
+                    gt[name] = pf[fam][f][st]
+    if "true_lh_single_zones" in samples:
+        for a in range(len(data.areas)):
+            for key, name in (("true_lh_single_zones", f"lh_a{a + 1}"),
+                              ("true_prior_single_zones", f"prior_a{a + 1}"),
+                              ("true_posterior_single_zones", f"post_a{a + 1}")):
+                cols.append(name)
+                gt[name] = samples[key][a]
+    return gt, cols
+
+
+def collect_gt_areas_for_writing(samples):
+    """util.collect_gt_areas_for_writing (util.py:741-742)."""
+    return format_area_columns(samples["true_zones"])
+
+
+def recall_precision(sample_zones, true_zones):
+    """The stats file's recall and precision of one sample against the true zones (util.py:811-825):
+    over the union of the zones, |sample & true| / |true| and |sample & true| / |sample| (NaN for
+    an empty sample, as numpy's 0 / 0)."""
+    sample_z = np.any(sample_zones, axis=0)
+    true_z = np.any(true_zones, axis=0)
+    inter = np.sum(np.minimum(sample_z, true_z), axis=0)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        return inter / np.sum(true_z), inter / np.sum(sample_z, axis=0)
+
+
 def samples2file(samples, data, config, paths):
     """sbayes.util.samples2file (util.py:846-907): the stats file (tab-separated, one row per
     logged sample, csv.DictWriter formatting) and the areas file (one line of area bit strings
-    per sample).  ``data`` needs feature_names / state_names / family_names (reference dicts or
-    plain lists) and is_simulated.  Ground-truth files (simulated data) are not written here."""
-    def ext(x):
-        return x["external"] if isinstance(x, dict) else x
-
+    per sample); for simulated data (data.is_simulated) also the ground-truth stats and areas
+    files (paths 'gt', 'gt_areas') and the stats file's recall / precision columns.  ``data``
+    needs feature_names / state_names / family_names (reference dicts or plain lists),
+    is_simulated and, simulated, areas."""
+    ext = _ext
     print("Writing results to file ...")
     feature_names = list(ext(data.feature_names))
     state_names = [list(s) for s in ext(data.state_names)]
@@ -343,7 +417,13 @@ def samples2file(samples, data, config, paths):
     family_names = list(ext(data.family_names)) if inheritance else []
     simulated = bool(getattr(data, "is_simulated", False))
     if simulated:
-        raise NotImplementedError("ground-truth files of simulated data are not written by samples2file here")
+        gt, gt_cols = collect_gt_for_writing(samples, data, config)
+        with open(paths["gt"], "w", newline="") as fh:
+            writer = csv.writer(fh, delimiter="\t")
+            writer.writerow(gt_cols)
+            writer.writerow([_fmt(gt[c]) for c in gt_cols])
+        with open(paths["gt_areas"], "w", newline="") as fh:
+            fh.write(collect_gt_areas_for_writing(samples))
     zones = samples["sample_zones"]
     n = len(zones)
     steps_per_sample = float(config["mcmc"]["N_STEPS"] / config["mcmc"]["N_SAMPLES"])
@@ -380,6 +460,8 @@ def samples2file(samples, data, config, paths):
                 for fam in range(len(family_names)):
                     for f in range(n_f):
                         row += [_fmt(pf[fam][f][i]) for i in st_idx[f]]
+            if simulated:
+                row += [_fmt(v) for v in recall_precision(z, samples["true_zones"])]
             if single:
                 for a in range(n_zones):
                     row += [_fmt(samples["sample_lh_single_zones"][s][a]),
@@ -394,6 +476,7 @@ def samples2file(samples, data, config, paths):
 __all__ = ["FeatureTable", "read_features_packed", "read_features_from_csv",
            "read_feature_occurrence_from_csv", "read_universal_counts", "read_inheritance_counts",
            "compute_network", "read_geo_cost_matrix", "format_area_columns", "stats_columns", "samples2file",
+           "collect_gt_for_writing", "collect_gt_areas_for_writing", "recall_precision",
            "extract_feature_states"]
 
 

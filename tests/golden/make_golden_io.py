@@ -195,6 +195,95 @@ def capture_model_setup(out):
             os.chdir(cwd)
 
 
+SIM_CASES = {  # simulated-data result files: (experiment, simulation overrides, model config)
+    "sim1": ("experiments/simulation/sim_exp1",
+             {"I_CONTACT": 3, "E_CONTACT": 0.5, "STRENGTH": 1, "AREA": 4},
+             {"N_AREAS": 2, "INHERITANCE": False}),
+    "sim2": ("experiments/simulation/sim_exp2", {}, {"N_AREAS": 1, "INHERITANCE": True}),
+}
+
+
+def capture_results_files_simulated():
+    """samples2file on simulated data (util.py:846-907): the ground-truth stats and areas files
+    (collect_gt_for_writing / collect_gt_areas_for_writing, util.py:657-742) and the stats file's
+    recall / precision columns (:811-825), for the reference's own simulations sim_exp1 (no
+    inheritance; model with 2 zones against 1 true zone) and sim_exp2 (simulated inheritance),
+    with a seeded statistics dict and the simulation's true parameters."""
+    import random
+    import types
+    from sbayes import util
+    from sbayes.experiment_setup import Experiment
+    from sbayes.simulation import Simulation
+    for case, (rel_dir, sim_over, model) in SIM_CASES.items():
+        exp_dir = refenv.scratch_copy(rel_dir)
+        np.random.seed(1)
+        random.seed(1)
+        exp = Experiment(experiment_name="golden", config_file=os.path.join(exp_dir, "config.json"), log=False)
+        exp.load_config(os.path.join(exp_dir, "config.json"), custom_settings={"simulation": sim_over} if sim_over else None)
+        sim = Simulation(experiment=exp)
+        sim.run_simulation()
+        Z, inh = model["N_AREAS"], model["INHERITANCE"]
+        sim_inh = bool(exp.config["simulation"]["INHERITANCE"])
+        N, F = np.asarray(sim.features).shape[:2]
+        S = np.asarray(sim.features).shape[2]
+        fam_names = sim.family_names if sim_inh else {"external": [], "internal": []}
+        Fam = len(fam_names["external"])
+        rng = np.random.default_rng(21 if case == "sim1" else 22)
+        n = 9
+        C = 3 if inh else 2
+        stats = {k: [] for k in ("sample_zones", "sample_weights", "sample_p_global", "sample_p_zones",
+                                 "sample_p_families", "sample_likelihood", "sample_prior")}
+        true_z = np.any(sim.areas, axis=0)
+        for i in range(n):
+            if i == 0:  # an empty sample: precision 0 / 0 = nan
+                zones = np.zeros((Z, N), bool)
+            else:  # zones that partly overlap the true one
+                lab = np.where(true_z & (rng.random(N) < 0.7), rng.integers(0, Z, N), -1)
+                lab[rng.random(N) < 0.02] = Z - 1
+                zones = np.stack([lab == z for z in range(Z)])
+            stats["sample_zones"].append(zones)
+            stats["sample_weights"].append(rng.dirichlet(np.ones(C), size=F))
+            stats["sample_p_global"].append(rng.dirichlet(np.ones(S), size=(1, F)))
+            stats["sample_p_zones"].append(rng.dirichlet(np.ones(S), size=(Z, F)))
+            stats["sample_p_families"].append(rng.dirichlet(np.ones(S), size=(max(Fam, 1), F))[:Fam])
+            stats["sample_likelihood"].append(float(-rng.random() * 1000))
+            stats["sample_prior"].append(float(-rng.random() * 10))
+        if not inh:
+            del stats["sample_p_families"]
+        w = np.asarray(sim.weights, np.float64)
+        stats["true_zones"] = sim.areas
+        stats["true_weights"] = w.copy() if inh else w[:, :2] / w[:, :2].sum(-1, keepdims=True)
+        stats["true_p_global"] = sim.p_universal[np.newaxis, ...]
+        stats["true_p_zones"] = sim.p_contact
+        if sim_inh:
+            stats["true_p_families"] = sim.p_inheritance
+        stats["true_ll"] = float(-rng.random() * 1e4)
+        stats["true_prior"] = float(-rng.random() * 10)
+        Zt = np.asarray(sim.areas).shape[0]
+        stats["true_lh_single_zones"] = list(-rng.random(Zt) * 500)
+        stats["true_prior_single_zones"] = list(-rng.random(Zt) * 5)
+        stats["true_posterior_single_zones"] = [a + b for a, b in zip(stats["true_lh_single_zones"],
+                                                                      stats["true_prior_single_zones"])]
+        np.savez_compressed(os.path.join(OUT, f"samples_{case}_in.npz"),
+                            **{k: np.asarray(v) for k, v in stats.items()})
+        meta = {"feature_names": [str(x) for x in sim.feature_names["external"]],
+                "state_names": [[str(s) for s in st] for st in sim.state_names["external"]],
+                "family_names": [str(x) for x in fam_names["external"]],
+                "config": {"model": model, "simulation": {"INHERITANCE": sim_inh},
+                           "mcmc": {"N_STEPS": 900, "N_SAMPLES": n}}}
+        with open(os.path.join(OUT, f"samples_{case}_meta.json"), "w") as f:
+            json.dump(meta, f)
+        config = {"model": dict(model), "simulation": {"INHERITANCE": sim_inh},
+                  "mcmc": {"N_STEPS": 900, "N_SAMPLES": n}}
+        data = types.SimpleNamespace(feature_names=sim.feature_names, state_names=sim.state_names,
+                                     family_names=fam_names, areas=sim.areas, is_simulated=True)
+        paths = {"parameters": os.path.join(OUT, f"stats_{case}_expected.txt"),
+                 "areas": os.path.join(OUT, f"areas_{case}_expected.txt"),
+                 "gt": os.path.join(OUT, f"gt_stats_{case}_expected.txt"),
+                 "gt_areas": os.path.join(OUT, f"gt_areas_{case}_expected.txt")}
+        util.samples2file(stats, data, config, paths)
+
+
 def main():
     refenv.setup()
     os.makedirs(OUT, exist_ok=True)
@@ -203,8 +292,12 @@ def main():
     capture_model_setup(out)
     np.savez_compressed(os.path.join(OUT, "io_expected.npz"), **out)
     capture_results_files()
+    capture_results_files_simulated()
     print("wrote", sorted(os.listdir(OUT)))
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and sys.argv[1:] == ["simulated"]:
+    refenv.setup()
+    capture_results_files_simulated()
+elif __name__ == "__main__":
     main()

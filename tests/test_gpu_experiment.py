@@ -96,3 +96,41 @@ def test_runs_are_independent_and_reproducible(gpu_available, tmp_path):
     c, _ = experiment.run_experiment(cfg, data, 2, run=0, name="r2", seed=11)
     assert a["sample_likelihood"] != b["sample_likelihood"]
     assert a["sample_likelihood"] == c["sample_likelihood"]
+
+
+SIM_CFG = os.path.join(os.path.dirname(__file__), "golden", "io", "data", "experiments", "simulation",
+                       "sim_exp1", "config.json")
+
+
+@pytest.mark.parametrize("source", [False, True])
+def test_simulated_experiment_ground_truth(gpu_available, tmp_path, source):
+    """The reference's sim_exp1 config on its own simulation (tests/golden/data_cfg1_sim.npz, the
+    truth of tests/golden/truth_sim.npz): MCMC.save_samples' simulated branch writes the
+    ground-truth stats / areas files, whose likelihood and prior equal the reference's
+    eval_ground_truth values, and the stats file carries recall / precision against the truth."""
+    from conftest import load_golden
+    d, t = load_golden("data_cfg1_sim"), load_golden("truth_sim")
+    data = experiment.SimulatedData(d["obs"], d["states"], d["locations"], t["areas"], t["data_weights"],
+                                    t["p_universal"], t["p_contact"])
+    np.testing.assert_array_equal(data.network["adj_mat"].indptr, d["adj_indptr"])
+    np.testing.assert_array_equal(data.network["adj_mat"].indices, d["adj_indices"])
+    cfg, _ = experiment.load_config(SIM_CFG, {
+        "simulation": {"I_CONTACT": 3, "E_CONTACT": 0.5, "STRENGTH": 1, "AREA": 4},
+        "model": {"SAMPLE_SOURCE": source},
+        "mcmc": {"N_STEPS": 1500, "N_SAMPLES": 15, "WARM_UP": {"N_WARM_UP_STEPS": 300, "N_WARM_UP_CHAINS": 4}},
+        "results": {"RESULTS_PATH": str(tmp_path)}}, simulated=True)
+    stats, paths = experiment.run_experiment(cfg, data, 1, name="sim", seed=4)
+    assert os.path.dirname(paths["parameters"]).endswith(os.path.join("sim", "s1a4"))
+    head, rows = _read_stats(paths["gt"])
+    assert len(rows) == 1 and len(rows[0]) == len(head)
+    gt = dict(zip(head, rows[0]))
+    assert float(gt["likelihood"]) == pytest.approx(float(t["true_ll"]), rel=1e-9)
+    assert float(gt["prior"]) == float(t["true_prior"])
+    assert float(gt["lh_a1"]) == pytest.approx(float(t["true_lh_single_zones"][0]), rel=1e-9)
+    with open(paths["gt_areas"]) as f:
+        assert f.read() == io.format_area_columns(t["areas"])
+    head, rows = _read_stats(paths["parameters"])
+    assert head[-5:-3] == ["recall", "precision"] and len(rows) == 15
+    for s, r in enumerate(rows):
+        rec, prec = io.recall_precision(stats["sample_zones"][s], t["areas"])
+        assert float(r[-5]) == rec and float(r[-4]) == prec

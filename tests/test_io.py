@@ -127,6 +127,37 @@ def test_results_files_match_reference(gold, tmp_path):
             assert a.read() == b.read(), mine
 
 
+@pytest.mark.parametrize("case", ["sim1", "sim2"])
+def test_simulated_results_files_match_reference(tmp_path, case):
+    """samples2file on the reference's own simulations (sim_exp1: no inheritance, a 2-zone model
+    against 1 true area; sim_exp2: simulated inheritance): the ground-truth stats and areas files
+    (util.py:657-742) and the stats file with its recall / precision columns (:811-825, NaN
+    precision for an empty sample) equal the reference's byte for byte."""
+    with open(os.path.join(GOLD, f"samples_{case}_meta.json")) as f:
+        m = json.load(f)
+    with np.load(os.path.join(GOLD, f"samples_{case}_in.npz")) as z:
+        d = {k: z[k] for k in z.files}
+    stats = {k: list(d[k]) for k in d if k.startswith("sample_")}
+    stats["sample_likelihood"] = [float(v) for v in stats["sample_likelihood"]]
+    stats["sample_prior"] = [float(v) for v in stats["sample_prior"]]
+    for k in ("true_zones", "true_weights", "true_p_global", "true_p_zones", "true_p_families"):
+        if k in d:
+            stats[k] = d[k]
+    stats["true_ll"], stats["true_prior"] = float(d["true_ll"]), float(d["true_prior"])
+    for k in ("true_lh_single_zones", "true_prior_single_zones", "true_posterior_single_zones"):
+        stats[k] = [float(v) for v in d[k]]
+    data = types.SimpleNamespace(feature_names=m["feature_names"], state_names=m["state_names"],
+                                 family_names=m["family_names"], areas=d["true_zones"], is_simulated=True)
+    paths = {"parameters": tmp_path / "stats.txt", "areas": tmp_path / "areas.txt",
+             "gt": tmp_path / "gt_stats.txt", "gt_areas": tmp_path / "gt_areas.txt"}
+    io.samples2file(stats, data, m["config"], paths)
+    for mine, ref in (("stats.txt", f"stats_{case}_expected.txt"), ("areas.txt", f"areas_{case}_expected.txt"),
+                      ("gt_stats.txt", f"gt_stats_{case}_expected.txt"),
+                      ("gt_areas.txt", f"gt_areas_{case}_expected.txt")):
+        with open(tmp_path / mine, "rb") as a, open(os.path.join(GOLD, ref), "rb") as b:
+            assert a.read() == b.read(), mine
+
+
 # ---- experiment setup (contact_zones_amd/experiment.py) vs the reference's Experiment/Data/MCMC ----
 @pytest.mark.parametrize("name", ["balkan", "south_america"])
 def test_experiment_setup_matches_reference(gold, name):
