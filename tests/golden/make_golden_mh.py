@@ -461,9 +461,53 @@ def geo_cases():
              n_chains=2)
 
 
+def real_data(name, n_zones):
+    """The reference's own Experiment -> Data for experiments/<name>/config.json (features,
+    counts priors, network), N_AREAS = n_zones, from a scratch copy (load_universal_counts writes
+    into the CWD); South America with CRS = None.  Returns (data, model config,
+    mcmc config) as the reference's MCMC would use them."""
+    import json
+    from sbayes.experiment_setup import Experiment
+    from sbayes.load_data import Data
+    d = refenv.scratch_copy(f"experiments/{name}")
+    cwd = os.getcwd()
+    os.chdir(d)
+    try:
+        with open("config.json") as f:
+            raw = json.load(f)
+        custom = {"model": {"N_AREAS": n_zones}}
+        for low, up in (("features", "FEATURES"), ("feature_states", "FEATURE_STATES")):
+            if low in raw.get("data", {}):
+                custom.setdefault("data", {})[up] = raw["data"][low]
+        if name == "south_america":
+            custom.setdefault("data", {})["CRS"] = None
+        exp = Experiment(experiment_name="golden", log=False)
+        exp.load_config(config_file="config.json", custom_settings=custom)
+        data = Data(experiment=exp)
+        data.load_features()
+        data.load_universal_counts()
+        data.load_inheritance_counts()
+        return data, exp.config["model"], exp.config["mcmc"]
+    finally:
+        os.chdir(cwd)
+
+
+def real_cases():
+    """SAMPLE_SOURCE = true runs of the reference's own real-data configs (BASELINE configs[2]
+    and [3]): Balkan with 3 zones, South America with 1 and 6 zones, their counts priors,
+    STEPS, PROPOSAL_PRECISION, MIN_M / MAX_M / M_INITIAL, 2 chains x 100 steps."""
+    for name, z, seed in (("balkan", 3, 31), ("south_america", 1, 32), ("south_america", 6, 33)):
+        data, model, mcmc = real_data(name, z)
+        tag = "balkan" if name == "balkan" else "sa"
+        run_case(f"src_{tag}_z{z}", data, model, mcmc, steps=100, seed=seed, warmup=False, n_chains=2)
+
+
 def main():
     if len(sys.argv) > 1 and sys.argv[1] == "geo":
         geo_cases()
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "real":
+        real_cases()
         return
     d = sim_data()
     run_case("cfg1_sim", d, model_cfg(1, False), mcmc_cfg(inheritance=0.0), steps=300, seed=3,
@@ -494,6 +538,8 @@ def main():
     run_case("small_priors_warmup", sc,
              model_cfg(2, True, min_m=3, max_m=8, counts=True, size="quadratic"),
              mcmc_cfg(area=0.6, m_initial=4), steps=300, seed=10, warmup=True, n_chains=4)
+    geo_cases()
+    real_cases()
 
 
 if __name__ == "__main__":

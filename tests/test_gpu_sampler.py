@@ -129,13 +129,14 @@ def test_philox_carried_prior_matches_full_prior(gpu_available):
     assert np.any(s["prior"] != fx["init_prior"])  # the prior moved
 
 
-@pytest.mark.parametrize("N,F,S,Z,Fam,inh", [
-    (3000, 40, 12, 3, 3, True),    # two batches of observation chunks (Np = 4096)
-    (700, 30, 40, 2, 2, True),     # S + 1 > 32: observation bytes hold x, not x * 8
-    (2000, 50, 10, 8, 4, True),    # the bench shape's site count / zones / families
-    (300, 20, 5, 2, 0, False),     # no inheritance (C = 2)
+@pytest.mark.parametrize("N,F,S,Z,Fam,inh,B,steps", [
+    (3000, 40, 12, 3, 3, True, 6, 1500),    # two batches of observation chunks (Np = 4096)
+    (700, 30, 40, 2, 2, True, 6, 1500),     # S + 1 > 32: observation bytes hold x, not x * 8
+    (2000, 50, 10, 8, 4, True, 6, 1500),    # the bench shape's site count / zones / families
+    (300, 20, 5, 2, 0, False, 6, 1500),     # no inheritance (C = 2)
+    (2000, 500, 10, 8, 4, True, 256, 400),  # the bench's sampler leg: full cfg5 width, 256 chains
 ])
-def test_philox_large_shapes_carried_ll(gpu_available, N, F, S, Z, Fam, inh):
+def test_philox_large_shapes_carried_ll(gpu_available, N, F, S, Z, Fam, inh, B, steps):
     """Philox runs on shapes the golden tapes do not reach: the incrementally carried ll equals a
     fresh full evaluation (likelihood kernel) within 1e-9 after every operator type ran, zones
     stay disjoint and within bounds, and parameters stay normalised."""
@@ -160,7 +161,6 @@ def test_philox_large_shapes_carried_ll(gpu_available, N, F, S, Z, Fam, inh):
     init = InitialSamples(packing.obs_to_features(obs, S), states, indptr, indices,
                           packing.index_to_groups(fam, Fam) if Fam else None, Z, 5, inh, None,
                           random.Random(11))
-    B = 6
     zos = np.stack([packing.zones_to_zone_of_site(init.zones(), N) for _ in range(B)])
     w = rng.dirichlet(np.ones(3 if inh else 2), size=(B, F))
     pg = rng.dirichlet(np.ones(S), size=(B, F))
@@ -171,11 +171,12 @@ def test_philox_large_shapes_carried_ll(gpu_available, N, F, S, Z, Fam, inh):
            "alter_p_global": 0.15, "alter_p_zones": 0.2, "alter_p_families": 0.1 if inh and Fam else 0.0}
     smp = Sampler(eng, states, indptr, indices, ops, [15, 40, 20, 20], 3)
     st = ChainState(eng, zos, w, pg, pz, pf)
-    out = smp.run(st, 1500, 40, 0.85, seed=5)
+    out = smp.run(st, steps, 40, 0.85, seed=5)
     torch.cuda.synchronize()
     assert out["status"].cpu().numpy().tolist() == [0] * B
     acc = st.accepted.cpu().numpy()
-    assert np.all(acc[:, :7].sum(0)[[0, 1, 3, 4, 5]] > 0)  # zone and parameter moves accepted
+    assert np.all(acc[:, :7].sum(0)[[1, 3, 4, 5]] > 0)  # zone and parameter moves accepted
+    assert np.all(st.proposed.cpu().numpy()[:, :7].sum(0)[[0, 1, 2]] > 0)  # every zone move ran
     s = st.to_numpy()
     fresh = st.refresh_ll().cpu().numpy()
     assert np.max(np.abs(s["ll"] - fresh) / np.abs(fresh)) <= REL_TOL
