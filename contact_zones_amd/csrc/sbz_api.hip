@@ -152,66 +152,12 @@ int sbz_open(int device, const sbz_dims *dims, const int8_t *obs, const uint8_t 
             obs_fm[(size_t)f * Np + p] = (uint8_t)((x < 0 ? S : x) * scale);
         }
     }
-    if (const char *v = getenv("SBZ_LIK_KERNEL"))
-        ctx->lik_kernel = strcmp(v, "zoned") == 0 ? 2 : strcmp(v, "db") == 0 ? 3 : strcmp(v, "ws") == 0 ? 4
-                        : strcmp(v, "zd") == 0 ? 5 : 1;
     if (const char *v = getenv("SBZ_LIK_BANKED")) ctx->lik_banked = atoi(v) != 0;
     if (const char *v = getenv("SBZ_SRC_RC")) ctx->src_rc = atoi(v) != 0;
     if (const char *v = getenv("SBZ_SRC_STAGE")) ctx->src_stage = atoi(v) != 0;
-    if (const char *v = getenv("SBZ_WS_NG")) ctx->ws_ng = std::min(2, std::max(1, atoi(v)));
-    if (const char *v = getenv("SBZ_WS_NB")) ctx->ws_nb = std::min(2, std::max(1, atoi(v)));
     if (const char *v = getenv("SBZ_SRC_HBM")) ctx->src_hbm = atoi(v) != 0;
     if (const char *v = getenv("SBZ_SRC_WAVES")) ctx->src_waves = atoi(v);
     if (const char *v = getenv("SBZ_LIK_TASKS")) ctx->tasks_per_cu = std::max(1, atoi(v));
-    if (const char *v = getenv("SBZ_LIK_ZSPL")) {
-        const int z = atoi(v);
-        ctx->zspl = (z == 4 || z == 16) ? z : 8;
-    } else {
-        ctx->zspl = N <= 4 * 64 ? 4 : 8;
-    }
-    // site counts by (family class, x) for the zone-sparse kernel: [F][128] int32
-    std::vector<int32_t> cnt;
-    if (lik_counts_apply(*dims)) {
-        const int S1 = S + 1;
-        cnt.assign((size_t)F * 128, 0);
-        for (int s = 0; s < N; s++)
-            for (int f = 0; f < F; f++)
-                cnt[(size_t)f * 128 + famc[s] * S1 + obs_fm[(size_t)f * Np + s] / scale]++;
-    }
-    if (!cnt.empty() &&
-        (hipMalloc(&ctx->d_cnt, cnt.size() * sizeof(int32_t)) != hipSuccess ||
-         hipMemcpy(ctx->d_cnt, cnt.data(), cnt.size() * sizeof(int32_t), hipMemcpyHostToDevice) !=
-             hipSuccess)) {
-        sbz_close(ctx);
-        return SBZ_ENOMEM;
-    }
-    // family presence over the sites (zone-sparse direct kernel: uniform weight patterns)
-    if (inh && dims->n_families > 0) {
-        int with = 0;
-        for (int s = 0; s < N; s++) with += famc_site[s] != 0;
-        ctx->hfm = with == 0 ? 0 : with == N ? 1 : 2;
-    }
-    // site-major x*8 observations, rows padded to a multiple of 4 features (one dword = 4
-    // features of a zoned site in the zone-sparse direct kernel)
-    if (!cnt.empty() && ctx->xs8) {
-        ctx->F4 = (F + 3) / 4 * 4;
-        // row N: all NA (the kernel's unused zoned-site slots)
-        std::vector<uint8_t> o8((size_t)(N + 1) * ctx->F4, (uint8_t)(S * 8));
-        for (int s = 0; s < N; s++)
-            for (int f = 0; f < F; f++) {
-                const int x = obs[(size_t)s * F + f];
-                o8[(size_t)s * ctx->F4 + f] = (uint8_t)((x < 0 ? S : x) * 8);
-            }
-        std::vector<double> ones((size_t)F * S + 8, 1.0);
-        if (hipMalloc(&ctx->d_obs8, o8.size()) != hipSuccess ||
-            hipMemcpy(ctx->d_obs8, o8.data(), o8.size(), hipMemcpyHostToDevice) != hipSuccess ||
-            hipMalloc(&ctx->d_ones, ones.size() * sizeof(double)) != hipSuccess ||
-            hipMemcpy(ctx->d_ones, ones.data(), ones.size() * sizeof(double), hipMemcpyHostToDevice) !=
-                hipSuccess) {
-            sbz_close(ctx);
-            return SBZ_ENOMEM;
-        }
-    }
     // site-major observations and family classes for the sampler's per-site deltas
     {
         std::vector<uint8_t> obs_sm((size_t)N * F);
@@ -254,14 +200,11 @@ void sbz_close(sbz_ctx *ctx) {
     if (ctx->d_obs_fm) (void)hipFree(ctx->d_obs_fm);
     if (ctx->d_famc) (void)hipFree(ctx->d_famc);
     if (ctx->d_perm) (void)hipFree(ctx->d_perm);
-    for (void *p : {(void *)ctx->d_obs_sm, (void *)ctx->d_fam_site, (void *)ctx->d_obs8, (void *)ctx->d_ones, (void *)ctx->d_adj_ptr,
+    for (void *p : {(void *)ctx->d_obs_sm, (void *)ctx->d_fam_site, (void *)ctx->d_adj_ptr,
                     (void *)ctx->d_adj_idx, (void *)ctx->d_app_list, (void *)ctx->d_app_cnt,
                     (void *)ctx->d_alpha_g, (void *)ctx->d_alpha_f, (void *)ctx->d_gc_g,
                     (void *)ctx->d_gc_f, (void *)ctx->d_geo_cost})
         if (p) (void)hipFree(p);
-    if (ctx->d_cnt) (void)hipFree(ctx->d_cnt);
-    free_buf(ctx->zl);
-    free_buf(ctx->nzs);
     free_buf(ctx->partial);
     free_buf(ctx->zflag);
     free_buf(ctx->mh_stage);

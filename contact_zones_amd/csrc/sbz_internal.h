@@ -32,13 +32,8 @@ struct LikArgs {
     const double *pg;       // [B][F][S]
     const double *pz;       // [B][Z][F][S]
     const double *pf;       // [B][Fam][F][S] (C == 3 only)
-    const uint8_t *src_fm;  // [B][F][Np] component index per cell, or nullptr (mixture)
-    const int *cnt;         // [F][128]   sites per (family class, x): fc * (S+1) + x (zone-sparse)
-    const uint32_t *zl;     // [B][N]     zoned sites: site | class << 24, first nzs[b] valid
-    const int *nzs;         // [B]        zoned sites per chain
-    const uint8_t *obs8;    // [N + 1][F4] x*8 by site (NA: S*8; row N all NA), rows padded to F4
-    const double *ones;     // [F*S + 8]  1.0: constant entries of the zone-sparse direct kernel
-    int F4;
+    const uint8_t *src_fm;  // [B][F][Np] row code per cell (lik_source_rc_kernel), or nullptr
+    const uint8_t *src_rm;  // [B][N][F]  the caller's sources (lik_source_generic_kernel)
     double *partial;        // [B][W]     task partial sums
     unsigned *ticket;       // [B]        finished tasks per chain (0 between launches)
     unsigned *zflag;        // [B]        source branch: a task saw a zero selected weight (0
@@ -58,14 +53,9 @@ struct sbz_ctx {
     uint8_t *d_obs_fm = nullptr;
     uint8_t *d_famc = nullptr;
     int *d_perm = nullptr;  // [Np] site index of each position (family-sorted order)
-    int *d_cnt = nullptr;  // [F][128] site counts by (family class, x), or null (dense kernel)
     // sampler data (sbz_open / sbz_set_network)
     uint8_t *d_obs_sm = nullptr;    // [N][F] x by site (S = NA)
     uint8_t *d_fam_site = nullptr;  // [N] family class by site
-    uint8_t *d_obs8 = nullptr;      // [N + 1][F4] x*8 by site, zone-sparse direct kernel (xs8 only)
-    double *d_ones = nullptr;       // [F*S + 8] ones, same kernel
-    int F4 = 0;
-    int hfm = 0;  // family presence over the sites: 0 none (or C = 2), 1 every site, 2 mixed
     int *d_adj_ptr = nullptr, *d_adj_idx = nullptr;  // CSR network
     int adj_nnz = 0;
     int *d_app_list = nullptr, *d_app_cnt = nullptr; // [F][S] applicable states, [F] counts
@@ -76,16 +66,9 @@ struct sbz_ctx {
     double geo_scale = 0.0;
     double *d_gc_g = nullptr;     // [F][S] Gibbs prior counts of p_global (sbz_set_gibbs_counts)
     double *d_gc_f = nullptr;     // [Fam][F][S] of p_families
-    int zspl = 8;          // zoned sites per lane and chunk of the zone-sparse kernel
-    int lik_kernel = 1;    // SBZ_LIK_KERNEL: 1 dense (default), 2 zone-sparse ("zoned"),
-                           // 3 dense double-buffered ("db", where the table fits 4 KiB),
-                           // 4 wave-specialised builder + gatherers ("ws", same condition),
-                           // 5 zone-sparse direct ("zd")
-    int lik_banked = 1;
-    int src_rc = 1;
-    int src_stage = 1;     // SBZ_SRC_STAGE=0: source-mode sampler passes read parameters from L2        // SBZ_SRC_RC=0: source-mode likelihood with the per-cell component select    // SBZ_LIK_BANKED=0: dense kernel with the packed [class][x] table
-    int ws_ng = 2;         // SBZ_WS_NG: gatherer waves of the wave-specialised kernel (1 or 2)
-    int ws_nb = 2;         // SBZ_WS_NB: its builder waves (1 or 2; 2 split the zone-class slots)
+    int lik_banked = 1;    // SBZ_LIK_BANKED=0: dense kernel with the packed [class][x] table
+    int src_rc = 1;        // SBZ_SRC_RC=0: source branch on the generic per-cell kernel
+    int src_stage = 1;     // SBZ_SRC_STAGE=0: source-mode sampler passes read parameters from L2
     const void *mix_occ_fn = nullptr;  // the kernel mix_occ was queried for
     int tasks_per_cu = 0;  // SBZ_LIK_TASKS: single-wave tasks per CU per launch (0: occupancy)
     int mix_occ = 0;       // resident mixture-kernel waves per CU (queried at first launch)
@@ -94,7 +77,7 @@ struct sbz_ctx {
     int src_hbm = 0;       // SBZ_SRC_HBM=1: source-mode sampler keeps sources in HBM even when they fit LDS
     std::string last_kernels;  // sbz_last_kernels
     sbz::DevBuf mh_stage;      // host-form sampler staging (sbz_mh_run)
-    sbz::DevBuf partial, ticket, zflag, src_t, zl, nzs, stage, out, src_cand, flags;
+    sbz::DevBuf partial, ticket, zflag, src_t, stage, out, src_cand, flags;
     std::string err;
 };
 
@@ -108,8 +91,6 @@ int hip_fail(sbz_ctx *ctx, hipError_t e, const char *what);
 size_t lik_lds_bytes(const sbz_dims &d, bool source_mode);
 // Raise the dynamic-LDS limit of the likelihood kernels (gfx950: 160 KiB per workgroup).
 int lik_configure(sbz_ctx *ctx);
-// Whether the zone-sparse (counts) mixture kernel applies to these dims.
-bool lik_counts_apply(const sbz_dims &d);
 // Sites per lane of the likelihood kernels for n_sites (4, 8, 16 or 32).
 int sites_per_lane(int n_sites);
 // Positions of the likelihood context: n_sites padded to a multiple of 64 * sites_per_lane.

@@ -34,27 +34,19 @@ def _assert_close(got, ref, tol=REL_TOL):
     return 0.0 if rel.size == 0 else float(rel.max())
 
 
-# Mixture-mode kernels: "dense" = every site gathered from the table (default), "db" = the
-# double-buffered dense kernel (where the table fits 4 KiB), "ws" / "ws1" = the wave-specialised
-# kernel (a builder wave + 2 / 1 gatherer waves, same condition), "zoned" = zone-sparse counts
-# kernel, "zd" = zone-sparse direct kernel (no class table) (SBZ_LIK_KERNEL and SBZ_WS_NG are
-# read when a context opens).
-MODES = [("mixture", "dense"), ("mixture", "db"), ("mixture", "ws"), ("mixture", "ws1"),
-         ("mixture", "zoned"), ("mixture", "zd"), ("source", "dense"), ("source", "src_select")]
+# Kernel paths: the dense mixture kernel with its banked table layout (the default where
+# S + 1 <= 16) and with the packed [class][x] layout (SBZ_LIK_BANKED=0, the layout of every
+# larger S); the source branch on the row-code table kernel (default) and on the generic per-cell
+# kernel (SBZ_SRC_RC=0, the path of shapes the table kernel does not take).  Both variables are
+# read when a context opens.
+MODES = [("mixture", "dense"), ("mixture", "packed"), ("source", "rc"), ("source", "generic")]
 
 
 @pytest.fixture
 def lik_kernel(request, monkeypatch):
     kernel = request.param
-    # "src_select": the source branch with the per-cell component select (lik_source_kernel)
-    # instead of the row-code table kernel (lik_source_rc_kernel, the default)
-    monkeypatch.setenv("SBZ_SRC_RC", "0" if kernel == "src_select" else "1")
-    if kernel == "src_select":
-        kernel = "dense"
-    if kernel.startswith("ws"):
-        monkeypatch.setenv("SBZ_WS_NG", "1" if kernel == "ws1" else "2")
-        kernel = "ws"
-    monkeypatch.setenv("SBZ_LIK_KERNEL", kernel)
+    monkeypatch.setenv("SBZ_LIK_BANKED", "0" if kernel == "packed" else "1")
+    monkeypatch.setenv("SBZ_SRC_RC", "0" if kernel == "generic" else "1")
     return request.param
 
 
@@ -188,44 +180,6 @@ def test_drop_in_likelihood_interface(gpu_available):
         assert lik(Sample(b, True)) == pytest.approx(d["ll_source"][b], rel=1e-12)
 
 
-@pytest.mark.parametrize("kernel,zspl", [("zoned", "4"), ("zoned", "8"), ("zoned", "16"),
-                                         ("zd", "4"), ("zd", "8")])
-def test_zone_sparse_paths(gpu_available, monkeypatch, kernel, zspl):
-    """Zone-sparse kernels: several chunks of zoned sites, no zoned sites, all sites zoned,
-    zero no-zone table entries (exact slow path, finite and -inf) and untamed inputs."""
-    from contact_zones_amd.likelihood import LikelihoodEngine
-    from oracle import oracle_c
-    monkeypatch.setenv("SBZ_LIK_ZSPL", zspl)
-    monkeypatch.setenv("SBZ_LIK_KERNEL", kernel)
-    N, F, S, Z, Fam, B = 1500, 40, 6, 4, 3, 7
-    rng = np.random.default_rng(11)
-    obs, fam, zos, w, pg, pz, pf, _ = _random_batch(rng, N, F, S, Z, Fam, B, True, 100)
-    zos[0] = rng.integers(0, Z, size=N)          # every site zoned (3 chunks at 8 per lane)
-    zos[1] = 255                                 # no zoned site
-    zos[2] = 255
-    zos[2, rng.permutation(N)[:700]] = rng.integers(0, Z, size=700)   # 700 zoned: 2 chunks at 8
-    # state 0 of feature 0 observed only at sites zoned in chains 3 and 4
-    zoned34 = (zos[3] != 255) & (zos[4] != 255)
-    obs[~zoned34 & (obs[:, 0] == 0), 0] = 1
-    for b in (3, 4):
-        pg[b, 0, 0] = 0.0
-        pf[b, :, 0, 0] = 0.0
-    # chain 4: one site outside every zone observes that state -> log 0 = -inf
-    s_out = int(np.flatnonzero(zos[4] == 255)[0])
-    obs[s_out, 0] = 0
-    zos[3, s_out] = 0                            # chain 3 keeps it zoned -> finite
-    # chain 5: untamed (tiny) parameters -> per-factor renormalisation
-    pg[5, :, 1] = 1e-200
-    # chain 6: a zero zone parameter on an observed state -> a zoned cell of exactly 0 (-inf
-    # unless another component covers it)
-    pz[6, :, :, 2] = 0.0
-    eng = LikelihoodEngine(obs, fam, S, Z, Fam, True)
-    got = eng.loglik(zos, w, pg, pz, pf)
-    ref = oracle_c.loglik_batch(obs, fam, zos, w, pg, pz, pf, inheritance=True)
-    assert np.isfinite(ref[3]) and ref[4] == -np.inf
-    _assert_close(got, ref, tol=1e-12)
-
-
 @pytest.mark.parametrize("banked", ["1", "0"])
 @pytest.mark.parametrize("shape", [(1500, 40, 6, 4, 3, 9), (2000, 64, 10, 8, 4, 9), (300, 21, 15, 3, 2, 9)])
 def test_dense_edge_paths(gpu_available, monkeypatch, banked, shape):
@@ -235,7 +189,6 @@ def test_dense_edge_paths(gpu_available, monkeypatch, banked, shape):
     and denormal parameters (per-feature renormalisation)."""
     from contact_zones_amd.likelihood import LikelihoodEngine
     from oracle import oracle_c
-    monkeypatch.setenv("SBZ_LIK_KERNEL", "dense")
     monkeypatch.setenv("SBZ_LIK_BANKED", banked)
     N, F, S, Z, Fam, B = shape
     rng = np.random.default_rng(N + F)
@@ -263,7 +216,7 @@ def test_dense_edge_paths(gpu_available, monkeypatch, banked, shape):
 @pytest.mark.parametrize("rc", ["1", "0"])
 @pytest.mark.parametrize("shape", [(2000, 64, 10, 8, 4, 8), (300, 21, 15, 3, 2, 8), (120, 30, 4, 0, 3, 8)])
 def test_source_edge_paths(gpu_available, monkeypatch, rc, shape):
-    """Source branch (row-code table kernel and the per-cell select kernel): a selected component
+    """Source branch (row-code table kernel and the generic per-cell kernel): a selected component
     of weight 0 (-inf, model.py:181-182), tiny parameters (products underflow -> task re-run),
     parameters above 1, denormal family parameters, sources past the site's components."""
     from contact_zones_amd.likelihood import LikelihoodEngine
@@ -290,27 +243,6 @@ def test_source_edge_paths(gpu_available, monkeypatch, rc, shape):
     got = eng.loglik(zos, w, pg, pz, pf, src)
     ref = oracle_c.loglik_batch(obs, fam, zos, w, pg, pz, pf, source=src, inheritance=True)
     assert ref[3] == -np.inf and ref[2] == -np.inf
-    _assert_close(got, ref, tol=1e-12)
-
-
-@pytest.mark.parametrize("nofam,Fam,inh", [(0.0, 4, True), (1.0, 4, True), (0.3, 4, True),
-                                           (0.0, 0, False), (0.0, 0, True)])
-@pytest.mark.parametrize("zspl", ["4", "8"])
-def test_zd_family_layouts(gpu_available, monkeypatch, nofam, Fam, inh, zspl):
-    """Zone-sparse direct kernel, every family-presence instantiation (every site with a family,
-    none, mixed; no inheritance; inheritance without families), partial slots, ragged F."""
-    from contact_zones_amd.likelihood import LikelihoodEngine
-    from oracle import oracle_c
-    monkeypatch.setenv("SBZ_LIK_ZSPL", zspl)
-    monkeypatch.setenv("SBZ_LIK_KERNEL", "zd")
-    N, F, S, Z, B = 900, 61, 7, 5, 9
-    rng = np.random.default_rng(int(nofam * 10) + Fam + 100 * inh + int(zspl))
-    obs, fam, zos, w, pg, pz, pf, _ = _random_batch(rng, N, F, S, Z, Fam, B, inh, 37, nofam=nofam)
-    zos[1] = 255
-    zos[2, :300] = rng.integers(0, Z, size=300)
-    eng = LikelihoodEngine(obs, fam, S, Z, Fam, inh)
-    got = eng.loglik(zos, w, pg, pz, pf)
-    ref = oracle_c.loglik_batch(obs, fam, zos, w, pg, pz, pf, inheritance=inh)
     _assert_close(got, ref, tol=1e-12)
 
 
