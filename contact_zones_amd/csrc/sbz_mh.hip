@@ -31,7 +31,10 @@ namespace sbz {
 
 #ifndef SBZ_MH_STAMP
 #define SBZ_MH_STAMP 0  // diagnostic builds only: trace_ll holds the shader cycles of phase k (1 move
-                        // draw, 2 proposal, 3 delta, 4 accept / apply, 5 whole step) instead of ll
+                        // draw, 2 proposal, 3 delta, 4 accept / apply, 5 whole step; sub-phases of a
+                        // parameter move: 6 wait for the altered pair, 7 Dirichlet draw, 8 lgamma /
+                        // log stage, 9 exp / log to the end of 2, 10 column store + weights,
+                        // 11 table build, 12 gathers + reductions) instead of ll
 #endif
 #ifndef SBZ_MH_ABLATE
 #define SBZ_MH_ABLATE 0  // diagnostic builds only (wrong results): 1 = no parameter-move delta,
@@ -428,7 +431,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
     // `o` holds the wave's first OB observation chunks (obs_load, issued early).  Returns this
     // thread's part of the delta (block_sum).
     auto delta_param = [&](int f, int comp, int row, int ia, int ib, double va, double vb,
-                           uint32_t (&o)[OB]) {
+                           uint32_t (&o)[OB], uint64_t *stamps) {
         const double *wc = col + (1 + Z + Fam) * S;
         // normalize_weights (model.py:436-452) for the 4 (has_zone, has_family) classes, before
         // (nw[0..15]) and after (nw[16..31]) the move; one division per weight as the reference
@@ -452,6 +455,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             o4[2] = C == 3 ? w2 / sum : 0.0;
         }
         bsync();
+        if (stamps) stamps[0] = __builtin_amdgcn_s_memtime();
         // tables: entry e = cls * S1 + x, threads step through e by NT (cls, x kept incrementally)
         int cls = tid / S1, x = tid - (tid / S1) * S1;
         const int dq = NT / S1, dr = NT - dq * S1;
@@ -491,6 +495,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             }
         }
         const bool wid = block_sum_i(wide) != 0;  // (its barrier publishes the tables)
+        if (stamps) stamps[1] = __builtin_amdgcn_s_memtime();
         // gathers: position p = 256 k + 4 lane + j of the wave's chunks k = wv + NWV * i
         double mn = 1.0, mo = 1.0;
         int en = 0, eo = 0;
@@ -527,7 +532,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
     //   3. delta log-likelihood;  4. accept / reject and apply.
     bool broken = false;  // a tape decision with no matching candidate (replay mismatch)
     for (int step = 0; step < a.n_steps; step++) {
-        uint64_t tph[6];
+        uint64_t tph[12] = {};
         tph[0] = SBZ_MH_STAMP ? __builtin_amdgcn_s_memtime() : 0;
         if (rng.bad || broken) break;
         const int op = rng.op(a.op_cdf, a.nops);
@@ -662,6 +667,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
         uint32_t ow[OB];
         if (comp >= 0) {
             const double c0 = uni(ldp(base + ia)), c1 = uni(ldp(base + ib));
+            if (SBZ_MH_STAMP) tph[5] = __builtin_amdgcn_s_memtime();
             // the move's column and observations: in flight during the proposal math
             col_load(f, cv);
             obs_load(f, 0, ow);
@@ -671,7 +677,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             const double t0 = raw ? c0 : c0 / sum, t1 = raw ? c1 : c1 / sum;
             double u0 = t0, u1 = t1;
             if (SBZ_MH_ABLATE & 2) log_q = log_q_back = 0.0;
-            else dirichlet_proposal2(rng, t0, t1, prec, u0, u1, log_q, log_q_back);
+            else dirichlet_proposal2(rng, t0, t1, prec, u0, u1, log_q, log_q_back, SBZ_MH_STAMP ? tph + 6 : nullptr);
             nv0 = raw ? u0 : u0 * sum;
             nv1 = raw ? u1 : u1 * sum;
             // 'counts' priors: dirichlet_logpdf(p[f, states], alpha) changes only in the two
@@ -697,7 +703,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                 if (sb >= 0) part = part + delta_site(sb, zna, NONE);
             } else if (comp >= 0 && !(SBZ_MH_ABLATE & 1)) {
                 col_store(f, cv);
-                part = delta_param(f, comp, row, ia, ib, nv0, nv1, ow);
+                part = delta_param(f, comp, row, ia, ib, nv0, nv1, ow, SBZ_MH_STAMP ? tph + 8 : nullptr);
             }
             delta = block_sum(part);
             if (block_sum_i(err != 0 ? 1 : 0) != 0) {  // a range check failed: stop before using the move
@@ -759,8 +765,11 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             ch.trace_ll[t] = ll;
             if (SBZ_MH_STAMP) {
                 tph[4] = __builtin_amdgcn_s_memtime();
-                ch.trace_ll[t] = SBZ_MH_STAMP == 5 ? (double)(tph[4] - tph[0])
-                                                   : (double)(tph[SBZ_MH_STAMP] - tph[SBZ_MH_STAMP > 0 ? SBZ_MH_STAMP - 1 : 0]);
+                // phase k = tph[k] - tph[k-1] (1..4); sub-phases: start / end stamp pairs
+                const int k = SBZ_MH_STAMP;
+                const int e_[13] = {0, 1, 2, 3, 4, 4, 5, 6, 7, 2, 8, 9, 3};
+                const int s_[13] = {0, 0, 1, 2, 3, 0, 1, 5, 6, 7, 2, 8, 9};
+                ch.trace_ll[t] = (double)(tph[e_[k]] - tph[s_[k]]);
             }
         }
         if (ch.trace_zos) {

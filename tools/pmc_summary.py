@@ -47,6 +47,29 @@ if mix:
                        "valu_insts_per_wave": (s.get("SQ_INSTS_VALU", 0) / s["SQ_WAVES"]) if s.get("SQ_WAVES") else None,
                        "correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM); WRITE_SIZE x1"}
     print("HBM per launch:", json.dumps(summary["_hbm"]))
+# every kernel's HBM traffic per dispatch (same correction), LDS conflicts, VALU per wave, waits
+summary["_per_kernel"] = {}
+for k, s in summary.items():
+    if k.startswith("_") or not isinstance(s, dict):
+        continue
+    e = {}
+    if "FETCH_SIZE" in s or "WRITE_SIZE" in s:
+        e["fetch_bytes"] = s.get("FETCH_SIZE", 0.0) * 1024 * 2
+        e["write_bytes"] = s.get("WRITE_SIZE", 0.0) * 1024
+        e["traffic_bytes"] = e["fetch_bytes"] + e["write_bytes"]
+    if s.get("SQ_LDS_IDX_ACTIVE"):
+        e["lds_bank_conflict_frac"] = s.get("SQ_LDS_BANK_CONFLICT", 0) / s["SQ_LDS_IDX_ACTIVE"]
+    if s.get("SQ_WAVES"):
+        e["valu_insts_per_wave"] = s.get("SQ_INSTS_VALU", 0) / s["SQ_WAVES"]
+        e["lds_insts_per_wave"] = s.get("SQ_INSTS_LDS", 0) / s["SQ_WAVES"]
+    if s.get("SQ_WAVE_CYCLES"):
+        e["wait_any_frac"] = s.get("SQ_WAIT_ANY", 0) / s["SQ_WAVE_CYCLES"]
+        e["active_inst_any_frac"] = s.get("SQ_ACTIVE_INST_ANY", 0) / s["SQ_WAVE_CYCLES"]
+        e["wait_inst_lds_frac"] = s.get("SQ_WAIT_INST_LDS", 0) / s["SQ_WAVE_CYCLES"]
+    if s.get("TCC_HIT", 0) + s.get("TCC_MISS", 0):
+        e["l2_hit_rate"] = s["TCC_HIT"] / (s["TCC_HIT"] + s["TCC_MISS"])
+    summary["_per_kernel"][k] = e
+    print(k, json.dumps(e))
 # the profiled bench run's workload (its JSON line in the pass logs), so bench.py can match it
 meta = {"command": "bash tools/pmc.sh (rocprofv3 --pmc <pass> --kernel-trace -- python3 bench.py ...)"}
 for log in sorted(glob.glob(os.path.join(out, "p*.log"))):
