@@ -43,12 +43,33 @@ namespace sbz {
 
 namespace {
 
+// Philox mode: step t of a launch draws its uniforms from the counter window
+// [ctr0 + WIN t, ctr0 + WIN (t + 1)) (operator at slot 0, the move's draws from slot 1 on, the
+// Dirichlet lane streams keyed by the slot that follows them, the acceptance uniform at slot
+// WIN - 1), so every step's operator, feature, pair and Dirichlet draws are known in advance.
+// The kernel computes the proposals of the parameter moves among the next LA steps at once, one
+// plan per lane (gammas, lgamma / log terms and densities of all plans in parallel lanes), and
+// a step whose plan is still valid (no earlier step of the batch accepted a change of the same
+// parameter row) skips its proposal phase.  A plan that went stale is recomputed in place, from
+// the same draws, so the trajectory does not depend on LA (tests/test_gpu_sampler.py).
+constexpr int WIN = 8;
+constexpr int LA = 6;  // most plans per batch (ten lgamma / log lanes per plan); a.la <= LA is used
+
+// The plans of one batch, in the wave's own LDS (each wave computes them, as every decision).
+struct Plans {
+    int op[LA], comp[LA], row[LA], f[LA], ia[LA], ib[LA], ok[LA], pad;
+    uint64_t cd[LA];  // Philox counter of the Dirichlet lane streams
+    double c0[LA], c1[LA], sum[LA], t0[LA], t1[LA], a0[LA], a1[LA], n0[LA], n1[LA];
+    double g[LA][2], v[LA][10];
+    double nv0[LA], nv1[LA], lq[LA], lqb[LA], dprior[LA];
+};
+
 // LDS layout of one chain's workgroup (byte offsets from the dynamic base), shared by the kernel
 // and mh_lds_bytes.  Site scans: thread t owns KT consecutive sites c * CH + t * KT + j of chunk
 // c (CH = NT * KT sites per chunk, nsc chunks); zos / nb / lst are padded to NpS = nsc * CH.
 struct MhLayout {
     int KT, CH, nsc, NpS, nent, ncol;
-    size_t col, zsize, red, nb, zos, selc, lst, stat, tabo, tabn, nw, rowp, ipos, clsinfo, geo, total;
+    size_t col, zsize, red, nb, zos, selc, lst, stat, tabo, tabn, nw, rowp, ipos, clsinfo, plans, geo, total;
     __host__ __device__ MhLayout(int N, int Np, int S, int Z, int Fam, int C, int FamC, int NT,
                                  bool with_geo = false) {
         KT = Np / NT;
@@ -79,6 +100,7 @@ struct MhLayout {
         ipos = take((size_t)N * 2);
         clsinfo = take((size_t)((Z + 1) * FamC + 1) * 2);
         // geo prior scratch (geo_zone_prior): key [N] doubles, mem [N] u16, cnt + redd / redi [16]
+        plans = take(sizeof(Plans) * (size_t)(NT / 64));  // one per wave
         geo = with_geo ? take(geo_scratch_bytes(N)) : o;
         total = o;
     }
@@ -531,11 +553,176 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
     //      the feature, component and pair of entries);  2. Dirichlet proposal (parameter moves);
     //   3. delta log-likelihood;  4. accept / reject and apply.
     bool broken = false;  // a tape decision with no matching candidate (replay mismatch)
+    const bool philox = rng.tape == nullptr;
+    const uint64_t ctr0 = rng.ctr;  // Philox: window of step t = ctr0 + WIN t
+    // plans (Philox): the steps plan_t0 .. plan_t0 + a.la - 1, in this wave's Plans
+    int plan_t0 = -(1 << 30);
+    Plans *pl = reinterpret_cast<Plans *>(lds + L.plans) + wv;
+    // The plans of steps t0 .. t0 + a.la - 1, in five lane-parallel stages with the results in LDS:
+    // (A) lane k evaluates step t0 + k's draws from its window (the operator, then the same draws
+    // in the same order as the sequential code below) and loads the altered pair; (B) the two
+    // gammas of plan k on lanes k and 32 + k; (C) the Dirichlet pair; (D) the ten lgamma / log
+    // terms of plan k on lanes 10 k .. 10 k + 9; (E) the two densities (exp, then log, as
+    // util.dirichlet_pdf) on lanes k and 32 + k, and the 'counts' prior change.
+    auto make_plans = [&](int t0) {
+        const uint32_t k0 = rng.key0, k1 = rng.key1;
+        const uint64_t chain = rng.chain;
+        const int la = a.la;
+        // precision of component comp (0 global, 1 zone, 2 family, 3 weights) by selects: a
+        // lane-varying index into the kernel arguments would copy them to scratch
+        const double pr_w = a.prec[0], pr_g = a.prec[1], pr_z = a.prec[2], pr_f = a.prec[3];
+        auto prec_of = [&](int comp) {
+            const double x = comp == 3 ? pr_w : pr_g;
+            const double y = comp == 1 ? pr_z : pr_f;
+            return (comp == 3 || comp == 0) ? x : y;
+        };
+        if (lane < la) {  // (A)
+            const int k = lane;
+            uint64_t c = ctr0 + (uint64_t)(t0 + k) * WIN;
+            int op = -1, comp = -1, row = 0, f = 0, ia = 0, ib = 0;
+            if (t0 + k < a.n_steps) {
+                const double u = philox_uniform(k0, k1, chain, c++);  // Rng::op
+                int n_le = 0;
+#pragma unroll
+                for (int q = 0; q < SBZ_N_OPS - 1; q++) n_le += (q < a.nops - 1 && !(u < a.op_cdf[q])) ? 1 : 0;
+                op = n_le;
+                auto below = [&](int n) { return min((int)(philox_uniform(k0, k1, chain, c++) * (double)n), n - 1); };
+                if (op >= WEIGHTS && op <= P_FAMILIES && !(op == P_FAMILIES && (C == 2 || Fam == 0)) &&
+                    !(op == P_ZONES && Z == 0)) {
+                    if (op == WEIGHTS) {
+                        f = below(F);
+                        comp = 3;
+                        if (C == 3) {
+                            ia = below(3);
+                            ib = below(2);
+                            if (ib >= ia) ib++;
+                        } else {
+                            ia = 0;
+                            ib = 1;
+                        }
+                    } else {
+                        if (op == P_ZONES) row = below(Z);
+                        if (op == P_FAMILIES) row = below(Fam);
+                        f = below(F);
+                        const int n = a.app_cnt[f];
+                        const int i0 = below(n);
+                        int j0 = below(n - 1);
+                        if (j0 >= i0) j0++;
+                        ia = a.app_list[(size_t)f * S + i0];
+                        ib = a.app_list[(size_t)f * S + j0];
+                        comp = op == P_GLOBAL ? 0 : (op == P_ZONES ? 1 : 2);
+                    }
+                }
+            }
+            pl->op[k] = op;
+            pl->comp[k] = comp;
+            pl->row[k] = row;
+            pl->f[k] = f;
+            pl->ia[k] = ia;
+            pl->ib[k] = ib;
+            pl->ok[k] = comp >= 0 ? 1 : 0;
+            pl->cd[k] = c;
+            if (comp >= 0) {
+                // the altered pair: one load per array with a valid index, then a select (a
+                // lane-varying choice of base pointer would go through a scratch table)
+                const int rz = comp == 1 ? row : 0, rf = comp == 2 ? row : 0;
+                const int sa = min(ia, S - 1), sb = min(ib, S - 1);
+                const long long og = (long long)f * S, oz = ((long long)rz * F + f) * S,
+                                ofm = ((long long)rf * F + f) * S, ow = (long long)f * C;
+                const double w0 = ldp(w + ow + min(ia, C - 1)), w1 = ldp(w + ow + min(ib, C - 1));
+                const double g0 = ldp(pg + og + sa), g1 = ldp(pg + og + sb);
+                const double z0 = ldp(pz + (Z > 0 ? oz + sa : 0)), z1 = ldp(pz + (Z > 0 ? oz + sb : 0));
+                const double f0 = ldp(pf + (C == 3 && Fam > 0 ? ofm + sa : og + sa));
+                const double f1 = ldp(pf + (C == 3 && Fam > 0 ? ofm + sb : og + sb));
+                const double c0 = comp == 3 ? w0 : comp == 0 ? g0 : comp == 1 ? z0 : f0;
+                const double c1 = comp == 3 ? w1 : comp == 0 ? g1 : comp == 1 ? z1 : f1;
+                const double pr = prec_of(comp);
+                const bool raw = C == 2 && comp == 3;  // the weight pair as is (zone_sampling.py:440-443)
+                const double sum = raw ? 1.0 : c0 + c1;
+                const double t0d = raw ? c0 : c0 / sum, t1d = raw ? c1 : c1 / sum;
+                pl->c0[k] = c0;
+                pl->c1[k] = c1;
+                pl->sum[k] = sum;
+                pl->t0[k] = t0d;
+                pl->t1[k] = t1d;
+                pl->a0[k] = 1.0 + pr * t0d;
+                pl->a1[k] = 1.0 + pr * t1d;
+            }
+        }
+        wsync();
+        {  // (B)
+            const int kk = lane & 31, g = lane >> 5;
+            if (kk < la && pl->comp[kk] >= 0) {
+                LaneRng lr;
+                lr.initk(k0, k1, chain, pl->cd[kk], g);
+                pl->g[kk][g] = lr.gamma(g ? pl->a1[kk] : pl->a0[kk]);
+            }
+        }
+        wsync();
+        if (lane < la && pl->comp[lane] >= 0) {  // (C)
+            const int k = lane;
+            const double g0 = pl->g[k][0], g1 = pl->g[k][1];
+            const double sg = g0 + g1;
+            const double n0 = g0 / sg, n1 = g1 / sg;
+            const bool raw = C == 2 && pl->comp[k] == 3;
+            pl->n0[k] = n0;
+            pl->n1[k] = n1;
+            pl->nv0[k] = raw ? n0 : n0 * pl->sum[k];
+            pl->nv1[k] = raw ? n1 : n1 * pl->sum[k];
+        }
+        wsync();
+        {  // (D) dirichlet_proposal2's terms {a0, a1, a0 + a1, b0, b1, b0 + b1, n0, n1, w0, w1}
+            const int k = lane / 10, q = lane - 10 * k;
+            if (k < la && pl->comp[k] >= 0) {
+                const double pr = prec_of(pl->comp[k]);
+                const double a0 = pl->a0[k], a1 = pl->a1[k];
+                const double b0 = 1.0 + pr * pl->n0[k], b1 = 1.0 + pr * pl->n1[k];
+                double arg = q == 0 ? a0 : q == 1 ? a1 : q == 2 ? a0 + a1 : q == 3 ? b0 : q == 4 ? b1
+                           : q == 5 ? b0 + b1 : q == 6 ? pl->n0[k] : q == 7 ? pl->n1[k] : q == 8 ? pl->t0[k] : pl->t1[k];
+                pl->v[k][q] = q < 6 ? lgamma(arg) : log(arg);
+            }
+        }
+        wsync();
+        {  // (E) -(sum gammaln(a) - gammaln(sum a)) + sum xlogy(a - 1, x); q = exp, log q
+            const int kk = lane & 31, g = lane >> 5;
+            if (kk < la && pl->comp[kk] >= 0) {
+                const double *v = pl->v[kk];
+                const int comp = pl->comp[kk];
+                const double pr = prec_of(comp);
+                const double x0 = g ? 1.0 + pr * pl->n0[kk] : pl->a0[kk];  // the density's alphas
+                const double x1 = g ? 1.0 + pr * pl->n1[kk] : pl->a1[kk];
+                const double t0 = (x0 - 1.0) == 0.0 ? 0.0 : (x0 - 1.0) * v[g ? 8 : 6];
+                const double t1 = (x1 - 1.0) == 0.0 ? 0.0 : (x1 - 1.0) * v[g ? 9 : 7];
+                const double lp = -((v[g ? 3 : 0] + v[g ? 4 : 1]) - v[g ? 5 : 2]) + (t0 + t1);
+                const double l = log(exp(lp));
+                if (g) pl->lqb[kk] = l;
+                else pl->lq[kk] = l;
+                if (!g) {
+                    double dp = 0.0;
+                    if ((comp == 0 && a.alpha_g) || (C == 3 && comp == 2 && a.alpha_f)) {
+                        const double *al = comp == 0 ? a.alpha_g : a.alpha_f;
+                        const long long off = ((long long)pl->row[kk] * F + pl->f[kk]) * S;
+                        const double al0 = al[off + pl->ia[kk]] - 1.0, al1 = al[off + pl->ib[kk]] - 1.0;
+                        dp = (xlogy(al0, pl->nv0[kk]) - xlogy(al0, pl->c0[kk])) +
+                             (xlogy(al1, pl->nv1[kk]) - xlogy(al1, pl->c1[kk]));
+                    }
+                    pl->dprior[kk] = dp;
+                }
+            }
+        }
+        wsync();
+        plan_t0 = t0;
+    };
+
     for (int step = 0; step < a.n_steps; step++) {
-        uint64_t tph[12] = {};
+        uint64_t tph[12];  // SBZ_MH_STAMP builds only
         tph[0] = SBZ_MH_STAMP ? __builtin_amdgcn_s_memtime() : 0;
         if (rng.bad || broken) break;
-        const int op = rng.op(a.op_cdf, a.nops);
+        if (philox) rng.ctr = ctr0 + (uint64_t)step * WIN;
+        if (philox && a.la > 1 && step >= plan_t0 + a.la) make_plans(step);
+        const int pk = step - plan_t0;  // this step's plan (Philox, a.la > 1)
+        const bool planned = philox && a.la > 1 && uni(pl->ok[pk]) != 0;
+        const int op = planned ? uni(pl->op[pk]) : rng.op(a.op_cdf, a.nops);
         if (op < 0 || op > P_FAMILIES || (op == P_FAMILIES && (C == 2 || Fam == 0)) ||
             (op <= SWAP && Z == 0) || (op == P_ZONES && Z == 0)) {
             broken = true;
@@ -623,7 +810,13 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                 zna = NONE;
             }
         } else {
-            if (op == WEIGHTS) {
+            if (planned) {
+                comp = uni(pl->comp[pk]);
+                row = uni(pl->row[pk]);
+                f = uni(pl->f[pk]);
+                ia = uni(pl->ia[pk]);
+                ib = uni(pl->ib[pk]);
+            } else if (op == WEIGHTS) {
                 f = rng.below(F);
                 comp = 3;
                 if (C == 3) rng.pair(nullptr, 3, ia, ib);
@@ -665,7 +858,15 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
         double nv0 = 0.0, nv1 = 0.0;
         double cv[NCV];
         uint32_t ow[OB];
-        if (comp >= 0) {
+        if (comp >= 0 && planned) {
+            col_load(f, cv);
+            obs_load(f, 0, ow);
+            nv0 = uni(pl->nv0[pk]);
+            nv1 = uni(pl->nv1[pk]);
+            log_q = uni(pl->lq[pk]);
+            log_q_back = uni(pl->lqb[pk]);
+            dprior = uni(pl->dprior[pk]);
+        } else if (comp >= 0) {
             const double c0 = uni(ldp(base + ia)), c1 = uni(ldp(base + ib));
             if (SBZ_MH_STAMP) tph[5] = __builtin_amdgcn_s_memtime();
             // the move's column and observations: in flight during the proposal math
@@ -729,6 +930,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             accept = true;
         } else {
             const double mh = (delta * 1.0) - (log_q - log_q_back) + dprior;
+            if (philox) rng.ctr = ctr0 + (uint64_t)step * WIN + (WIN - 1);
             accept = log(rng.real()) < mh;
         }
         if (tid == 0) stat[op]++;
@@ -751,10 +953,15 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                     }
                 }
                 occupied += (zna < Z ? 1 : -1) + (sb >= 0 ? -1 : 0);
-            } else if (tid == 0) {
-                stp(base + ia, nv0);
-                stp(base + ib, nv1);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            } else {
+                if (tid == 0) {
+                    stp(base + ia, nv0);
+                    stp(base + ib, nv1);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                // later plans that read this parameter row are stale: recomputed when reached
+                if (philox && lane < a.la && pl->comp[lane] == comp && pl->row[lane] == row && pl->f[lane] == f)
+                    pl->ok[lane] = 0;
             }
             bsync();
         }
@@ -784,7 +991,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
         ch.ll[b] = ll;
         if (ch.prior) ch.prior[b] = prior;
         if (ch.tape_pos) ch.tape_pos[b] = rng.pos;
-        if (ch.counter) ch.counter[b] = rng.ctr;
+        if (ch.counter) ch.counter[b] = philox ? ctr0 + (uint64_t)a.n_steps * WIN : rng.ctr;
         if (ch.status) ch.status[b] = broken ? 2 : (rng.bad ? 1 : 0);
     }
     if (tid < SBZ_N_OPS) {  // per-operator counters, one thread each
@@ -835,6 +1042,7 @@ int launch_mh(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg, const 
     a.n_steps = n_steps;
     a.min_size = cfg->min_size;
     a.warmup = cfg->warmup;
+    a.la = ctx->mh_la;
     // operators of the mode: zone moves + alter_* (mixture) or + Gibbs operators (source mode)
     bool allowed[SBZ_N_OPS] = {};
     allowed[SHRINK] = allowed[GROW] = allowed[SWAP] = true;

@@ -190,6 +190,15 @@ struct Rng {
     __device__ __forceinline__ void dirichlet2(double a0, double a1, double &x0, double &x1);
 };
 
+// Uniform number i of a chain's Rng stream, computed by one lane on its own (the value
+// Rng::uniform53 returns for counter i): half (i & 1) of Philox block (i >> 1, chain).
+__device__ __forceinline__ double philox_uniform(uint32_t key0, uint32_t key1, uint64_t chain, uint64_t i) {
+    const uint64_t blk = i >> 1;
+    uint32_t c[4] = {(uint32_t)blk, (uint32_t)(blk >> 32), (uint32_t)chain, (uint32_t)(chain >> 32)};
+    philox4x32_10(c, key0, key1);
+    return (i & 1) ? u53(c[2], c[3]) : u53(c[0], c[1]);
+}
+
 // Per-lane Philox stream: block (j, base lo, chain, base hi ^ (lane + 1) << 24), key = seed.
 // `base` is the wave's 64-bit counter when the phase started (the wave then advances it by one),
 // j counts the lane's draws in the phase.  The counter's high word goes into c3 (bits 0..19; a
@@ -397,6 +406,7 @@ struct Chain {
 struct MhArgs {
     int N, F, S, Z, Fam, C, FamC, Np, xs8;
     int n_steps, nops, min_size, warmup;
+    int la;     // mh_kernel, Philox draws: proposals planned ahead per batch (1 = none; <= 6)
     int stage;  // mh_src_kernel: parameters and normalised weights staged in LDS for the N*F passes
     double op_cdf[SBZ_N_OPS];
     double prec[4];

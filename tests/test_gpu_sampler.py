@@ -236,3 +236,32 @@ def test_host_form_philox_matches_device_form(gpu_available):
     for k in ("zone_of_site", "w", "p_global", "p_zones", "ll", "prior") + (("p_fam",) if inh else ()):
         np.testing.assert_array_equal(host[k], dev[k], err_msg=k)
     np.testing.assert_array_equal(host["counter"], st.counter.cpu().numpy())
+
+
+@pytest.mark.parametrize("case", ["mh_small_priors", "mh_cfg1_sim_inh_z2", "mh_small_bounds"])
+def test_philox_planned_proposals_do_not_change_trajectories(gpu_available, monkeypatch, case):
+    """Philox mode plans the proposals of the next parameter moves in parallel lanes (SBZ_MH_LA
+    steps at a time) and recomputes a plan that an accepted move made stale: the trajectory
+    (operators, accepts, ll, final state, counters) is bit-identical to the one-step-at-a-time
+    path (SBZ_MH_LA = 1), over launches of different lengths."""
+    import torch
+    fx = load_golden(case)
+    runs = []
+    for la in ("1", "6", "4"):
+        monkeypatch.setenv("SBZ_MH_LA", la)
+        eng, smp, st = _setup(fx)
+        outs = [smp.run(st, n, fx["max_size"], fx["p_grow_connected"], seed=4242, chain_id0=3, trace=True)
+                for n in (700, 5, 1301)]
+        torch.cuda.synchronize()
+        runs.append(([{k: v.cpu().numpy() for k, v in o.items() if hasattr(v, "cpu")} for o in outs], st.to_numpy(),
+                     st.counter.cpu().numpy(), st.accepted.cpu().numpy()))
+    base = runs[0]
+    assert base[3][:, 3:7].sum() > 50  # parameter moves were accepted (plans went stale)
+    for other in runs[1:]:
+        for o1, o2 in zip(base[0], other[0]):
+            for k in ("op", "accept", "ll", "status"):
+                np.testing.assert_array_equal(o1[k], o2[k], err_msg=k)
+        for k in base[1]:
+            np.testing.assert_array_equal(base[1][k], other[1][k], err_msg=k)
+        np.testing.assert_array_equal(base[2], other[2])
+        np.testing.assert_array_equal(base[3], other[3])
