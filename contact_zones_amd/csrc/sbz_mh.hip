@@ -173,6 +173,28 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
         rslot ^= 1;
         return uni(t);
     };
+    // a double sum and an int sum (the range-check flags) in one reduction
+    auto block_sum_di = [&](double v, int iv, int &isum) -> double {
+        v = wave_sum(v);
+        iv = wave_sum_i(iv);
+        double *r = redd + rslot * 16;
+        int *ri = redi + rslot * 16;
+        if (lane == 0) {
+            r[wv] = v;
+            ri[wv] = iv;
+        }
+        bsync();
+        double t = r[0];
+        int ti = ri[0];
+#pragma unroll
+        for (int i = 1; i < NWV; i++) {
+            t = t + r[i];
+            ti += ri[i];
+        }
+        rslot ^= 1;
+        isum = uni(ti);
+        return uni(t);
+    };
     auto block_sum_i = [&](int v) -> int {
         v = wave_sum_i(v);
         int *r = redi + rslot * 16;
@@ -714,12 +736,30 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
         plan_t0 = t0;
     };
 
+    // An accepted parameter move's store (thread 0) is not waited for at once: the next load of
+    // parameters (or the column store of a prefetched step) first waits for it and publishes it
+    // with a barrier (fence_params), by which time it has long completed.
+    bool store_pending = false;
+    auto fence_params = [&]() {
+        if (store_pending) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            bsync();
+            store_pending = false;
+        }
+    };
+    // prefetched column / observations of the next planned step (feature nx_f, -1 = none)
+    int nx_f = -1;
+    double nx_cv[NCV];
+    uint32_t nx_ow[OB];
     for (int step = 0; step < a.n_steps; step++) {
         uint64_t tph[12];  // SBZ_MH_STAMP builds only
         tph[0] = SBZ_MH_STAMP ? __builtin_amdgcn_s_memtime() : 0;
         if (rng.bad || broken) break;
         if (philox) rng.ctr = ctr0 + (uint64_t)step * WIN;
-        if (philox && a.la > 1 && step >= plan_t0 + a.la) make_plans(step);
+        if (philox && a.la > 1 && step >= plan_t0 + a.la) {
+            fence_params();
+            make_plans(step);
+        }
         const int pk = step - plan_t0;  // this step's plan (Philox, a.la > 1)
         const bool planned = philox && a.la > 1 && uni(pl->ok[pk]) != 0;
         const int op = planned ? uni(pl->op[pk]) : rng.op(a.op_cdf, a.nops);
@@ -855,12 +895,20 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
 
         if (SBZ_MH_STAMP) tph[1] = __builtin_amdgcn_s_memtime();
         // ---- 2. Dirichlet proposal of the pair (zone_sampling.py:421-438, :537-569)
+        if (!(planned && comp >= 0 && nx_f == f)) fence_params();
         double nv0 = 0.0, nv1 = 0.0;
         double cv[NCV];
         uint32_t ow[OB];
         if (comp >= 0 && planned) {
-            col_load(f, cv);
-            obs_load(f, 0, ow);
+            if (nx_f == f) {  // prefetched during the previous step, and still current
+#pragma unroll
+                for (int q = 0; q < NCV; q++) cv[q] = nx_cv[q];
+#pragma unroll
+                for (int q = 0; q < OB; q++) ow[q] = nx_ow[q];
+            } else {
+                col_load(f, cv);
+                obs_load(f, 0, ow);
+            }
             nv0 = uni(pl->nv0[pk]);
             nv1 = uni(pl->nv1[pk]);
             log_q = uni(pl->lq[pk]);
@@ -903,11 +951,24 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                 part = delta_site(sa, zoa, zna);
                 if (sb >= 0) part = part + delta_site(sb, zna, NONE);
             } else if (comp >= 0 && !(SBZ_MH_ABLATE & 1)) {
+                if (store_pending) {  // published by col_store's barrier
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    store_pending = false;
+                }
                 col_store(f, cv);
                 part = delta_param(f, comp, row, ia, ib, nv0, nv1, ow, SBZ_MH_STAMP ? tph + 8 : nullptr);
             }
-            delta = block_sum(part);
-            if (block_sum_i(err != 0 ? 1 : 0) != 0) {  // a range check failed: stop before using the move
+            // the next step's column and observations, when it is a planned parameter move: in
+            // flight during this step's reduction and acceptance
+            nx_f = -1;
+            if (philox && a.la > 1 && pk + 1 < a.la && step + 1 < a.n_steps && uni(pl->ok[pk + 1]) != 0) {
+                nx_f = uni(pl->f[pk + 1]);
+                col_load(nx_f, nx_cv);
+                obs_load(nx_f, 0, nx_ow);
+            }
+            int n_err = 0;
+            delta = block_sum_di(part, err != 0 ? 1 : 0, n_err);
+            if (n_err != 0) {  // a range check failed: stop before using the move
                 broken = true;
                 break;
             }
@@ -953,17 +1014,18 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                     }
                 }
                 occupied += (zna < Z ? 1 : -1) + (sb >= 0 ? -1 : 0);
+                bsync();
             } else {
                 if (tid == 0) {
                     stp(base + ia, nv0);
                     stp(base + ib, nv1);
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 }
+                store_pending = true;
                 // later plans that read this parameter row are stale: recomputed when reached
                 if (philox && lane < a.la && pl->comp[lane] == comp && pl->row[lane] == row && pl->f[lane] == f)
                     pl->ok[lane] = 0;
+                if (nx_f == f) nx_f = -1;  // the prefetched column holds the old values
             }
-            bsync();
         }
         if (ch.trace_op && tid == 0) {
             const size_t t = (size_t)b * a.n_steps + step;
