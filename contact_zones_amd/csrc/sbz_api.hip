@@ -158,7 +158,7 @@ int sbz_open(int device, const sbz_dims *dims, const int8_t *obs, const uint8_t 
     if (const char *v = getenv("SBZ_SRC_HBM")) ctx->src_hbm = atoi(v) != 0;
     if (const char *v = getenv("SBZ_SRC_WAVES")) ctx->src_waves = atoi(v);
     if (const char *v = getenv("SBZ_LIK_TASKS")) ctx->tasks_per_cu = std::max(1, atoi(v));
-    if (const char *v = getenv("SBZ_MH_LA")) ctx->mh_la = std::min(6, std::max(1, atoi(v)));
+    if (const char *v = getenv("SBZ_MH_LA")) ctx->mh_la = std::min(24, std::max(1, atoi(v)));
     // site-major observations and family classes for the sampler's per-site deltas
     {
         std::vector<uint8_t> obs_sm((size_t)N * F);

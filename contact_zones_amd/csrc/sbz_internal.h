@@ -74,7 +74,7 @@ struct sbz_ctx {
     int mix_occ = 0;       // resident mixture-kernel waves per CU (queried at first launch)
     int n_cu = 256;        // compute units of the device
     int src_waves = 0;     // SBZ_SRC_WAVES: waves per chain of the source-mode sampler (0: by N x F)
-    int mh_la = 6;         // SBZ_MH_LA: sampler proposals planned ahead per batch (1..6; 1 = none)
+    int mh_la = 24;        // SBZ_MH_LA: sampler proposals planned ahead per batch (1..24; 1 = none)
     int src_hbm = 0;       // SBZ_SRC_HBM=1: source-mode sampler keeps sources in HBM even when they fit LDS
     std::string last_kernels;  // sbz_last_kernels
     sbz::DevBuf mh_stage;      // host-form sampler staging (sbz_mh_run)

@@ -34,7 +34,8 @@ namespace sbz {
                         // draw, 2 proposal, 3 delta, 4 accept / apply, 5 whole step; sub-phases of a
                         // parameter move: 6 wait for the altered pair, 7 Dirichlet draw, 8 lgamma /
                         // log stage, 9 exp / log to the end of 2, 10 column store + weights,
-                        // 11 table build, 12 gathers + reductions) instead of ll
+                        // 11 table build, 12 gathers + reductions; 13-17 the plan stages A-E,
+                        // 0 on steps that make no plans) instead of ll
 #endif
 #ifndef SBZ_MH_ABLATE
 #define SBZ_MH_ABLATE 0  // diagnostic builds only (wrong results): 1 = no parameter-move delta,
@@ -48,16 +49,20 @@ namespace {
 // Dirichlet lane streams keyed by the slot that follows them, the acceptance uniform at slot
 // WIN - 1), so every step's operator, feature, pair and Dirichlet draws are known in advance.
 // The kernel computes the proposals of the parameter moves among the next LA steps at once, one
-// plan per lane (gammas, lgamma / log terms and densities of all plans in parallel lanes), and
+// plan per lane or lane group (gammas, lgamma / log terms and densities of all plans in parallel
+// lanes of the workgroup), and
 // a step whose plan is still valid (no earlier step of the batch accepted a change of the same
 // parameter row) skips its proposal phase.  A plan that went stale is recomputed in place, from
 // the same draws, so the trajectory does not depend on LA (tests/test_gpu_sampler.py).
 constexpr int WIN = 8;
-constexpr int LA = 6;  // most plans per batch (ten lgamma / log lanes per plan); a.la <= LA is used
+constexpr int LA = 24;  // most plans per batch (ten lgamma / log threads per plan: NT >= 10 LA)
+constexpr int MAX_NWV = 8;
 
-// The plans of one batch, in the wave's own LDS (each wave computes them, as every decision).
+// The plans of one batch, shared by the workgroup's waves (written between barriers); the
+// validity flags are per wave, so a wave invalidates its own copy without a barrier.
 struct Plans {
-    int op[LA], comp[LA], row[LA], f[LA], ia[LA], ib[LA], ok[LA], pad;
+    int op[LA], comp[LA], row[LA], f[LA], ia[LA], ib[LA];
+    int ok[MAX_NWV][LA];
     uint64_t cd[LA];  // Philox counter of the Dirichlet lane streams
     double c0[LA], c1[LA], sum[LA], t0[LA], t1[LA], a0[LA], a1[LA], n0[LA], n1[LA];
     double g[LA][2], v[LA][10];
@@ -100,7 +105,7 @@ struct MhLayout {
         ipos = take((size_t)N * 2);
         clsinfo = take((size_t)((Z + 1) * FamC + 1) * 2);
         // geo prior scratch (geo_zone_prior): key [N] doubles, mem [N] u16, cnt + redd / redi [16]
-        plans = take(sizeof(Plans) * (size_t)(NT / 64));  // one per wave
+        plans = take(sizeof(Plans));
         geo = with_geo ? take(geo_scratch_bytes(N)) : o;
         total = o;
     }
@@ -162,17 +167,6 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
     // alternately: a slot is rewritten only after every wave passed the barrier of the next
     // reduction, so no wave still reads it.
     int rslot = 0;
-    auto block_sum = [&](double v) -> double {
-        v = wave_sum(v);
-        double *r = redd + rslot * 16;
-        if (lane == 0) r[wv] = v;
-        bsync();
-        double t = r[0];
-#pragma unroll
-        for (int i = 1; i < NWV; i++) t = t + r[i];
-        rslot ^= 1;
-        return uni(t);
-    };
     // a double sum and an int sum (the range-check flags) in one reduction
     auto block_sum_di = [&](double v, int iv, int &isum) -> double {
         v = wave_sum(v);
@@ -577,19 +571,25 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
     bool broken = false;  // a tape decision with no matching candidate (replay mismatch)
     const bool philox = rng.tape == nullptr;
     const uint64_t ctr0 = rng.ctr;  // Philox: window of step t = ctr0 + WIN t
-    // plans (Philox): the steps plan_t0 .. plan_t0 + a.la - 1, in this wave's Plans
+    // plans (Philox): the steps plan_t0 .. plan_t0 + LAe - 1
+    static_assert(NWV <= MAX_NWV && NT >= 10 * LA, "plan stage D needs ten threads per plan");
+    const int LAe = min(a.la, LA);
     int plan_t0 = -(1 << 30);
-    Plans *pl = reinterpret_cast<Plans *>(lds + L.plans) + wv;
-    // The plans of steps t0 .. t0 + a.la - 1, in five lane-parallel stages with the results in LDS:
-    // (A) lane k evaluates step t0 + k's draws from its window (the operator, then the same draws
-    // in the same order as the sequential code below) and loads the altered pair; (B) the two
-    // gammas of plan k on lanes k and 32 + k; (C) the Dirichlet pair; (D) the ten lgamma / log
-    // terms of plan k on lanes 10 k .. 10 k + 9; (E) the two densities (exp, then log, as
-    // util.dirichlet_pdf) on lanes k and 32 + k, and the 'counts' prior change.
-    auto make_plans = [&](int t0) {
+    Plans *pl = reinterpret_cast<Plans *>(lds + L.plans);
+    int *okw = pl->ok[wv];  // this wave's validity flags
+    // The plans of steps t0 .. t0 + LAe - 1, in five thread-parallel stages with the results in
+    // LDS, separated by barriers: (A) thread k evaluates step t0 + k's draws from its window (the
+    // operator, then the same draws in the same order as the sequential code below) and loads the
+    // altered pair; (B) the two gammas of plan k on threads k and 32 + k; (C) the Dirichlet pair;
+    // (D) the ten lgamma / log terms of plan k on threads 10 k .. 10 k + 9 (all waves); (E) the
+    // two densities (exp, then log, as util.dirichlet_pdf) on threads k and 32 + k, and the
+    // 'counts' prior change.  Stages A-C and E run in wave 0.
+    auto make_plans = [&](int t0, uint64_t *stamps) {
+        bsync();  // every wave is done with the previous batch
+        if (stamps) stamps[0] = __builtin_amdgcn_s_memtime();
         const uint32_t k0 = rng.key0, k1 = rng.key1;
         const uint64_t chain = rng.chain;
-        const int la = a.la;
+        const int la = LAe;
         // precision of component comp (0 global, 1 zone, 2 family, 3 weights) by selects: a
         // lane-varying index into the kernel arguments would copy them to scratch
         const double pr_w = a.prec[0], pr_g = a.prec[1], pr_z = a.prec[2], pr_f = a.prec[3];
@@ -598,8 +598,8 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             const double y = comp == 1 ? pr_z : pr_f;
             return (comp == 3 || comp == 0) ? x : y;
         };
-        if (lane < la) {  // (A)
-            const int k = lane;
+        if (tid < la) {  // (A)
+            const int k = tid;
             uint64_t c = ctr0 + (uint64_t)(t0 + k) * WIN;
             int op = -1, comp = -1, row = 0, f = 0, ia = 0, ib = 0;
             if (t0 + k < a.n_steps) {
@@ -642,7 +642,8 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             pl->f[k] = f;
             pl->ia[k] = ia;
             pl->ib[k] = ib;
-            pl->ok[k] = comp >= 0 ? 1 : 0;
+#pragma unroll
+            for (int w = 0; w < NWV; w++) pl->ok[w][k] = comp >= 0 ? 1 : 0;
             pl->cd[k] = c;
             if (comp >= 0) {
                 // the altered pair: one load per array with a valid index, then a select (a
@@ -671,18 +672,20 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                 pl->a1[k] = 1.0 + pr * t1d;
             }
         }
-        wsync();
+        bsync();
+        if (stamps) stamps[1] = __builtin_amdgcn_s_memtime();
         {  // (B)
-            const int kk = lane & 31, g = lane >> 5;
-            if (kk < la && pl->comp[kk] >= 0) {
+            const int kk = tid & 31, g = tid >> 5;
+            if (tid < 64 && kk < la && pl->comp[kk] >= 0) {
                 LaneRng lr;
                 lr.initk(k0, k1, chain, pl->cd[kk], g);
                 pl->g[kk][g] = lr.gamma(g ? pl->a1[kk] : pl->a0[kk]);
             }
         }
-        wsync();
-        if (lane < la && pl->comp[lane] >= 0) {  // (C)
-            const int k = lane;
+        bsync();
+        if (stamps) stamps[2] = __builtin_amdgcn_s_memtime();
+        if (tid < la && pl->comp[tid] >= 0) {  // (C)
+            const int k = tid;
             const double g0 = pl->g[k][0], g1 = pl->g[k][1];
             const double sg = g0 + g1;
             const double n0 = g0 / sg, n1 = g1 / sg;
@@ -692,9 +695,10 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             pl->nv0[k] = raw ? n0 : n0 * pl->sum[k];
             pl->nv1[k] = raw ? n1 : n1 * pl->sum[k];
         }
-        wsync();
+        bsync();
+        if (stamps) stamps[3] = __builtin_amdgcn_s_memtime();
         {  // (D) dirichlet_proposal2's terms {a0, a1, a0 + a1, b0, b1, b0 + b1, n0, n1, w0, w1}
-            const int k = lane / 10, q = lane - 10 * k;
+            const int k = tid / 10, q = tid - 10 * k;
             if (k < la && pl->comp[k] >= 0) {
                 const double pr = prec_of(pl->comp[k]);
                 const double a0 = pl->a0[k], a1 = pl->a1[k];
@@ -704,10 +708,11 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                 pl->v[k][q] = q < 6 ? lgamma(arg) : log(arg);
             }
         }
-        wsync();
+        bsync();
+        if (stamps) stamps[4] = __builtin_amdgcn_s_memtime();
         {  // (E) -(sum gammaln(a) - gammaln(sum a)) + sum xlogy(a - 1, x); q = exp, log q
-            const int kk = lane & 31, g = lane >> 5;
-            if (kk < la && pl->comp[kk] >= 0) {
+            const int kk = tid & 31, g = tid >> 5;
+            if (tid < 64 && kk < la && pl->comp[kk] >= 0) {
                 const double *v = pl->v[kk];
                 const int comp = pl->comp[kk];
                 const double pr = prec_of(comp);
@@ -732,7 +737,8 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                 }
             }
         }
-        wsync();
+        bsync();
+        if (stamps) stamps[5] = __builtin_amdgcn_s_memtime();
         plan_t0 = t0;
     };
 
@@ -752,16 +758,18 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
     double nx_cv[NCV];
     uint32_t nx_ow[OB];
     for (int step = 0; step < a.n_steps; step++) {
-        uint64_t tph[12];  // SBZ_MH_STAMP builds only
+        uint64_t tph[16];  // SBZ_MH_STAMP builds only
+        if (SBZ_MH_STAMP)
+            for (int q = 10; q < 16; q++) tph[q] = 0;  // plan stages: 0 on steps without plans
         tph[0] = SBZ_MH_STAMP ? __builtin_amdgcn_s_memtime() : 0;
         if (rng.bad || broken) break;
         if (philox) rng.ctr = ctr0 + (uint64_t)step * WIN;
-        if (philox && a.la > 1 && step >= plan_t0 + a.la) {
+        if (philox && LAe > 1 && step >= plan_t0 + LAe) {
             fence_params();
-            make_plans(step);
+            make_plans(step, SBZ_MH_STAMP ? tph + 10 : nullptr);
         }
-        const int pk = step - plan_t0;  // this step's plan (Philox, a.la > 1)
-        const bool planned = philox && a.la > 1 && uni(pl->ok[pk]) != 0;
+        const int pk = step - plan_t0;  // this step's plan (Philox, LAe > 1)
+        const bool planned = philox && LAe > 1 && uni(okw[pk]) != 0;
         const int op = planned ? uni(pl->op[pk]) : rng.op(a.op_cdf, a.nops);
         if (op < 0 || op > P_FAMILIES || (op == P_FAMILIES && (C == 2 || Fam == 0)) ||
             (op <= SWAP && Z == 0) || (op == P_ZONES && Z == 0)) {
@@ -961,7 +969,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             // the next step's column and observations, when it is a planned parameter move: in
             // flight during this step's reduction and acceptance
             nx_f = -1;
-            if (philox && a.la > 1 && pk + 1 < a.la && step + 1 < a.n_steps && uni(pl->ok[pk + 1]) != 0) {
+            if (philox && LAe > 1 && pk + 1 < LAe && step + 1 < a.n_steps && uni(okw[pk + 1]) != 0) {
                 nx_f = uni(pl->f[pk + 1]);
                 col_load(nx_f, nx_cv);
                 obs_load(nx_f, 0, nx_ow);
@@ -1022,8 +1030,8 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                 }
                 store_pending = true;
                 // later plans that read this parameter row are stale: recomputed when reached
-                if (philox && lane < a.la && pl->comp[lane] == comp && pl->row[lane] == row && pl->f[lane] == f)
-                    pl->ok[lane] = 0;
+                if (philox && lane < LAe && pl->comp[lane] == comp && pl->row[lane] == row && pl->f[lane] == f)
+                    okw[lane] = 0;
                 if (nx_f == f) nx_f = -1;  // the prefetched column holds the old values
             }
         }
@@ -1036,8 +1044,9 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                 tph[4] = __builtin_amdgcn_s_memtime();
                 // phase k = tph[k] - tph[k-1] (1..4); sub-phases: start / end stamp pairs
                 const int k = SBZ_MH_STAMP;
-                const int e_[13] = {0, 1, 2, 3, 4, 4, 5, 6, 7, 2, 8, 9, 3};
-                const int s_[13] = {0, 0, 1, 2, 3, 0, 1, 5, 6, 7, 2, 8, 9};
+                // 13..17: make_plans stages A..E (0 on steps without plans)
+                const int e_[18] = {0, 1, 2, 3, 4, 4, 5, 6, 7, 2, 8, 9, 3, 11, 12, 13, 14, 15};
+                const int s_[18] = {0, 0, 1, 2, 3, 0, 1, 5, 6, 7, 2, 8, 9, 10, 11, 12, 13, 14};
                 ch.trace_ll[t] = (double)(tph[e_[k]] - tph[s_[k]]);
             }
         }

@@ -247,7 +247,7 @@ def test_philox_planned_proposals_do_not_change_trajectories(gpu_available, monk
     import torch
     fx = load_golden(case)
     runs = []
-    for la in ("1", "6", "4"):
+    for la in ("1", "24", "6"):
         monkeypatch.setenv("SBZ_MH_LA", la)
         eng, smp, st = _setup(fx)
         outs = [smp.run(st, n, fx["max_size"], fx["p_grow_connected"], seed=4242, chain_id0=3, trace=True)
