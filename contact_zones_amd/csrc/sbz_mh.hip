@@ -67,6 +67,7 @@ struct Plans {
     double c0[LA], c1[LA], sum[LA], t0[LA], t1[LA], a0[LA], a1[LA], n0[LA], n1[LA];
     double g[LA][2], v[LA][10];
     double nv0[LA], nv1[LA], lq[LA], lqb[LA], dprior[LA];
+    double lu[LA];  // log of each step's acceptance uniform (every step of the batch)
 };
 
 // LDS layout of one chain's workgroup (byte offsets from the dynamic base), shared by the kernel
@@ -287,15 +288,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
     };
     // exclusive prefix of n over the block's threads (thread order) from the per-wave totals in
     // cnt[0..NWV); incl = the inclusive prefix within the wave
-    auto wave_incl = [&](int n) -> int {
-        int incl = n;
-#pragma unroll
-        for (int off = 1; off < WAVE; off <<= 1) {
-            const int t = __shfl_up(incl, off, WAVE);
-            if (lane >= off) incl += t;
-        }
-        return incl;
-    };
+    auto wave_incl = [&](int n) -> int { return wave_incl_scan(n); };
     uint32_t msk[4];  // this thread's masks of the last scan (chunks 0..3; more chunks rescan)
     int scan_mode = 0, scan_z = 0;
     // number of selected sites; leaves per-wave counts in selc and the masks in msk
@@ -305,7 +298,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
         for (int c = 0; c < nsc; c++) {
             const uint32_t m = scan_mask(mode, z, c);
             if (c < 4) msk[c & 3] = m;
-            const int wt = uni(__shfl(wave_incl(__popc(m)), WAVE - 1, WAVE));
+            const int wt = uni((int)__builtin_amdgcn_readlane((uint32_t)wave_incl(__popc(m)), 63));
             if (lane == 0) selc[c * 16 + wv] = wt;
         }
         bsync();
@@ -681,6 +674,11 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                 lr.initk(k0, k1, chain, pl->cd[kk], g);
                 pl->g[kk][g] = lr.gamma(g ? pl->a1[kk] : pl->a0[kk]);
             }
+            // wave 1: the acceptance uniforms (slot WIN - 1 of each window), as rng.real() draws them
+            if (tid >= 64 && tid < 64 + la) {
+                const int k = tid - 64;
+                pl->lu[k] = log(philox_uniform(k0, k1, chain, ctr0 + (uint64_t)(t0 + k) * WIN + (WIN - 1)));
+            }
         }
         bsync();
         if (stamps) stamps[2] = __builtin_amdgcn_s_memtime();
@@ -999,8 +997,12 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             accept = true;
         } else {
             const double mh = (delta * 1.0) - (log_q - log_q_back) + dprior;
-            if (philox) rng.ctr = ctr0 + (uint64_t)step * WIN + (WIN - 1);
-            accept = log(rng.real()) < mh;
+            if (philox && LAe > 1) {
+                accept = uni(pl->lu[pk]) < mh;
+            } else {
+                if (philox) rng.ctr = ctr0 + (uint64_t)step * WIN + (WIN - 1);
+                accept = log(rng.real()) < mh;
+            }
         }
         if (tid == 0) stat[op]++;
         if (accept) {

@@ -23,15 +23,55 @@ __device__ __forceinline__ void wsync() {
     __builtin_amdgcn_wave_barrier();
 }
 
+// Wave reductions and scans on DPP lane moves (VALU, a few cycles each) instead of LDS-crossbar
+// shuffles: butterflies inside each 16-lane row (quad_perm, half-mirror, mirror), then the row
+// totals combined by row_bcast15 / row_bcast31, which leave the total in lane 63 (read back as a
+// wave-uniform value).  Fixed order, so the double sum is deterministic.  All 64 lanes active.
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v) {  // lanes without a source read 0
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xf, false);
+}
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ double dpp64(double v) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = dpp32<CTRL, ROWS>((uint32_t)b), hi = dpp32<CTRL, ROWS>((uint32_t)(b >> 32));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+enum : int { DPP_QP_1032 = 0xb1, DPP_QP_2301 = 0x4e, DPP_ROW_MIRROR = 0x140,
+             DPP_ROW_HALF_MIRROR = 0x141, DPP_BCAST15 = 0x142, DPP_BCAST31 = 0x143,
+             DPP_ROW_SHR1 = 0x111, DPP_ROW_SHR2 = 0x112, DPP_ROW_SHR4 = 0x114, DPP_ROW_SHR8 = 0x118 };
+
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
+    v = v + dpp64<DPP_QP_1032>(v);
+    v = v + dpp64<DPP_QP_2301>(v);
+    v = v + dpp64<DPP_ROW_HALF_MIRROR>(v);
+    v = v + dpp64<DPP_ROW_MIRROR>(v);        // every lane of a row: the row total
+    v = v + dpp64<DPP_BCAST15, 0xa>(v);      // rows 1, 3: + rows 0, 2
+    v = v + dpp64<DPP_BCAST31, 0xc>(v);      // rows 2, 3: + rows 0 + 1
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)b, 63);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(b >> 32), 63);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
 __device__ __forceinline__ int wave_sum_i(int v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    v += (int)dpp32<DPP_QP_1032>((uint32_t)v);
+    v += (int)dpp32<DPP_QP_2301>((uint32_t)v);
+    v += (int)dpp32<DPP_ROW_HALF_MIRROR>((uint32_t)v);
+    v += (int)dpp32<DPP_ROW_MIRROR>((uint32_t)v);
+    v += (int)dpp32<DPP_BCAST15, 0xa>((uint32_t)v);
+    v += (int)dpp32<DPP_BCAST31, 0xc>((uint32_t)v);
+    return (int)__builtin_amdgcn_readlane((uint32_t)v, 63);
+}
+
+// inclusive prefix sum over the wave's lanes (lane order); the wave total is in lane 63
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    v += (int)dpp32<DPP_ROW_SHR1>((uint32_t)v);
+    v += (int)dpp32<DPP_ROW_SHR2>((uint32_t)v);
+    v += (int)dpp32<DPP_ROW_SHR4>((uint32_t)v);
+    v += (int)dpp32<DPP_ROW_SHR8>((uint32_t)v);
+    v += (int)dpp32<DPP_BCAST15, 0xa>((uint32_t)v);
+    v += (int)dpp32<DPP_BCAST31, 0xc>((uint32_t)v);
     return v;
 }
 
