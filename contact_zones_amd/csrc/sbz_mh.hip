@@ -62,6 +62,7 @@ constexpr int MAX_NWV = 8;
 // validity flags are per wave, so a wave invalidates its own copy without a barrier.
 struct Plans {
     int op[LA], comp[LA], row[LA], f[LA], ia[LA], ib[LA];
+    int ci0[LA], ci1[LA];  // column positions of the altered pair
     int ok[MAX_NWV][LA];
     uint64_t cd[LA];  // Philox counter of the Dirichlet lane streams
     double c0[LA], c1[LA], sum[LA], t0[LA], t1[LA], a0[LA], a1[LA], n0[LA], n1[LA];
@@ -75,9 +76,11 @@ struct Plans {
 // c (CH = NT * KT sites per chunk, nsc chunks); zos / nb / lst are padded to NpS = nsc * CH.
 struct MhLayout {
     int KT, CH, nsc, NpS, nent, ncol;
-    size_t col, zsize, red, nb, zos, selc, lst, stat, tabo, tabn, nw, rowp, ipos, clsinfo, plans, geo, total;
+    uint32_t col, zsize, red, nb, zos, selc, lst, stat, tabo, tabn, nw, rowp, ipos, clsinfo, plans, plcol,
+        plnw, geo;
+    size_t total;
     __host__ __device__ MhLayout(int N, int Np, int S, int Z, int Fam, int C, int FamC, int NT,
-                                 bool with_geo = false) {
+                                 bool with_geo = false, int la = 1) {
         KT = Np / NT;
         KT = KT < 4 ? 4 : (KT > 32 ? 32 : KT);
         CH = NT * KT;
@@ -89,7 +92,7 @@ struct MhLayout {
         auto take = [&](size_t bytes) {
             const size_t at = o;
             o = (o + bytes + 15) & ~(size_t)15;
-            return at;
+            return (uint32_t)at;
         };
         col = take((size_t)ncol * 8);
         zsize = take((size_t)(Z + 1) * 4);
@@ -107,6 +110,9 @@ struct MhLayout {
         clsinfo = take((size_t)((Z + 1) * FamC + 1) * 2);
         // geo prior scratch (geo_zone_prior): key [N] doubles, mem [N] u16, cnt + redd / redi [16]
         plans = take(sizeof(Plans));
+        // the planned steps' parameter columns [la][ncol] and normalised weights [la][2][4][4]
+        plcol = take(la > 1 ? (size_t)la * ncol * 8 : 0);
+        plnw = take(la > 1 ? (size_t)la * 32 * 8 : 0);
         geo = with_geo ? take(geo_scratch_bytes(N)) : o;
         total = o;
     }
@@ -132,7 +138,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
     const int N = a.N, F = a.F, S = a.S, Z = a.Z, Fam = (C == 3) ? a.Fam : 0;
     const sbz_chains &ch = a.ch;
 
-    const MhLayout L(N, a.Np, S, Z, a.Fam, C, a.FamC, NT, a.geo_cost != nullptr);
+    const MhLayout L(N, a.Np, S, Z, a.Fam, C, a.FamC, NT, a.geo_cost != nullptr, a.la);
     const int KT = L.KT, CH = L.CH, nsc = L.nsc, ncol = L.ncol;
     double *col = reinterpret_cast<double *>(lds + L.col);  // staged parameter column
     int *zsize = reinterpret_cast<int *>(lds + L.zsize);     // [Z]
@@ -154,6 +160,8 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
     uint32_t *rowp = reinterpret_cast<uint32_t *>(lds + L.rowp); // [Np] table row (bytes) by position
     uint16_t *ipos = reinterpret_cast<uint16_t *>(lds + L.ipos); // [N] position of each site
     uint16_t *clsinfo = reinterpret_cast<uint16_t *>(lds + L.clsinfo);  // [ncls + 1] zone class | fc << 8
+    double *plcol = reinterpret_cast<double *>(lds + L.plcol);  // [la][ncol] planned steps' columns
+    double *plnw = reinterpret_cast<double *>(lds + L.plnw);    // [la][32] their normalised weights
 
     uint8_t *gzos = ch.zone_of_site + (size_t)b * N;
     double *w = ch.w + (size_t)b * F * C;
@@ -461,31 +469,37 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
     // weights, state ia / ib of the component's rows otherwise (NA cells do not change).
     // `o` holds the wave's first OB observation chunks (obs_load, issued early).  Returns this
     // thread's part of the delta (block_sum).
-    auto delta_param = [&](int f, int comp, int row, int ia, int ib, double va, double vb,
-                           uint32_t (&o)[OB], uint64_t *stamps) {
-        const double *wc = col + (1 + Z + Fam) * S;
-        // normalize_weights (model.py:436-452) for the 4 (has_zone, has_family) classes, before
-        // (nw[0..15]) and after (nw[16..31]) the move; one division per weight as the reference
-        if (tid < 8) {
-            const int h = tid & 3, nu = tid >> 2;
-            double wv3[3];
+    // normalize_weights (model.py:436-452) of class h (bit 0: has a zone, bit 1: has a family) for
+    // feature weights wc, after the move when nu (weights move: entries ia / ib become va / vb);
+    // one division per weight, as the reference
+    auto norm_w = [&](const double *wc, int comp, int ia, int ib, double va, double vb, int h, int nu,
+                      double *o4) {
+        double wv3[3];
 #pragma unroll
-            for (int i = 0; i < 3; i++) {
-                const double wo = (C == 3 || i < 2) ? wc[i] : 0.0;
-                wv3[i] = (nu && comp == 3 && i == ia) ? va : ((nu && comp == 3 && i == ib) ? vb : wo);
-            }
-            const double w0 = wv3[0] * 1.0, w1 = wv3[1] * ((h & 1) ? 1.0 : 0.0);
-            double sum = w0 + w1, w2 = 0.0;
-            if (C == 3) {
-                w2 = wv3[2] * ((h & 2) ? 1.0 : 0.0);
-                sum = sum + w2;
-            }
-            double *o4 = nw + nu * 16 + h * 4;
-            o4[0] = w0 / sum;
-            o4[1] = w1 / sum;
-            o4[2] = C == 3 ? w2 / sum : 0.0;
+        for (int i = 0; i < 3; i++) {
+            const double wo = (C == 3 || i < 2) ? wc[i] : 0.0;
+            wv3[i] = (nu && comp == 3 && i == ia) ? va : ((nu && comp == 3 && i == ib) ? vb : wo);
         }
-        bsync();
+        const double w0 = wv3[0] * 1.0, w1 = wv3[1] * ((h & 1) ? 1.0 : 0.0);
+        double sum = w0 + w1, w2 = 0.0;
+        if (C == 3) {
+            w2 = wv3[2] * ((h & 2) ? 1.0 : 0.0);
+            sum = sum + w2;
+        }
+        o4[0] = w0 / sum;
+        o4[1] = w1 / sum;
+        o4[2] = C == 3 ? w2 / sum : 0.0;
+    };
+    // `cl` is feature f's column in LDS (the staged col, or a planned step's column) and `nwp` its
+    // normalised weights before (nwp[0..15]) and after (nwp[16..31]) the move, or null: computed
+    // here into nw.
+    auto delta_param = [&](const double *cl, const double *nwp, int f, int comp, int row, int ia, int ib,
+                           double va, double vb, uint32_t (&o)[OB], uint64_t *stamps) {
+        if (!nwp) {
+            if (tid < 8) norm_w(cl + (1 + Z + Fam) * S, comp, ia, ib, va, vb, tid & 3, tid >> 2, nw + tid * 4);
+            bsync();
+            nwp = nw;
+        }
         if (stamps) stamps[0] = __builtin_amdgcn_s_memtime();
         // tables: entry e = cls * S1 + x, threads step through e by NT (cls, x kept incrementally)
         int cls = tid / S1, x = tid - (tid / S1) * S1;
@@ -498,9 +512,9 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                 const int zcl = (int)(ci & 0xffu), fc = (int)(ci >> 8);
                 const bool na = x == S, hz = zcl > 0, hf = fc > 0;
                 const int xc = na ? 0 : x, h = (hz ? 1 : 0) | (hf ? 2 : 0);
-                const double l0 = col[xc];
-                const double l1 = hz ? col[zcl * S + xc] : 0.0;
-                const double l2 = hf ? col[(Z + fc) * S + xc] : 0.0;
+                const double l0 = cl[xc];
+                const double l1 = hz ? cl[zcl * S + xc] : 0.0;
+                const double l2 = hf ? cl[(Z + fc) * S + xc] : 0.0;
                 const bool pick = !na && (x == ia || x == ib);
                 const bool changed = comp == 3 || (pick && (comp == 0 || (comp == 1 && zcl == row + 1) ||
                                                             (comp == 2 && fc == row + 1)));
@@ -508,7 +522,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                 const double n0 = comp == 0 && pick ? nv : l0;
                 const double n1 = comp == 1 && pick ? nv : l1;
                 const double n2 = comp == 2 && pick ? nv : l2;
-                const double *wo = nw + h * 4, *wn = nw + 16 + h * 4;
+                const double *wo = nwp + h * 4, *wn = nwp + 16 + h * 4;
                 const double wold[3] = {wo[0], wo[1], wo[2]}, wnew[3] = {wn[0], wn[1], wn[2]};
                 const double vo = cell_nw<C>(wold, hz, hf, na, l0, l1, l2);
                 const double vn = cell_nw<C>(wnew, hz, hf, na, n0, n1, n2);
@@ -554,7 +568,16 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                 renorm(mn, en);
             }
         }
-        return (log(mn) - log(mo)) + (double)(en - eo) * LN2;
+        if (stamps) {
+            asm volatile("" ::"v"(mn), "v"(mo));
+            stamps[8] = __builtin_amdgcn_s_memtime();
+        }
+        const double r = (log(mn) - log(mo)) + (double)(en - eo) * LN2;
+        if (stamps) {
+            asm volatile("" ::"v"(r));
+            stamps[9] = __builtin_amdgcn_s_memtime();
+        }
+        return r;
     };
 
     // One MH step per iteration, in four phases with one call site each (keeps the kernel small):
@@ -570,13 +593,16 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
     int plan_t0 = -(1 << 30);
     Plans *pl = reinterpret_cast<Plans *>(lds + L.plans);
     int *okw = pl->ok[wv];  // this wave's validity flags
-    // The plans of steps t0 .. t0 + LAe - 1, in five thread-parallel stages with the results in
-    // LDS, separated by barriers: (A) thread k evaluates step t0 + k's draws from its window (the
-    // operator, then the same draws in the same order as the sequential code below) and loads the
-    // altered pair; (B) the two gammas of plan k on threads k and 32 + k; (C) the Dirichlet pair;
-    // (D) the ten lgamma / log terms of plan k on threads 10 k .. 10 k + 9 (all waves); (E) the
-    // two densities (exp, then log, as util.dirichlet_pdf) on threads k and 32 + k, and the
-    // 'counts' prior change.  Stages A-C and E run in wave 0.
+    // The plans of steps t0 .. t0 + LAe - 1, in thread-parallel stages with the results in LDS:
+    // (A) thread k evaluates step t0 + k's draws from its window (the operator, then the same
+    // draws in the same order as the sequential code below); (COL) every thread gathers part of
+    // the planned features' parameter columns into plcol (all loads in flight at once); (A2) the
+    // altered pair read from the column; (B) the two gammas of plan k on threads k and 32 + k, the
+    // acceptance uniforms on wave 1; (C) the Dirichlet pair; (D) the ten lgamma / log terms of plan
+    // k on threads 10 k .. 10 k + 9 (all waves); (E) the two densities (exp, then log, as
+    // util.dirichlet_pdf) on threads k and 32 + k, the 'counts' prior change, and the normalised
+    // weights before / after each move on waves 1-3.  A later accepted move patches the columns of
+    // the plans it affects (step loop, phase 4), so a step never reloads its column.
     auto make_plans = [&](int t0, uint64_t *stamps) {
         bsync();  // every wave is done with the previous batch
         if (stamps) stamps[0] = __builtin_amdgcn_s_memtime();
@@ -638,35 +664,45 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
 #pragma unroll
             for (int w = 0; w < NWV; w++) pl->ok[w][k] = comp >= 0 ? 1 : 0;
             pl->cd[k] = c;
-            if (comp >= 0) {
-                // the altered pair: one load per array with a valid index, then a select (a
-                // lane-varying choice of base pointer would go through a scratch table)
-                const int rz = comp == 1 ? row : 0, rf = comp == 2 ? row : 0;
-                const int sa = min(ia, S - 1), sb = min(ib, S - 1);
-                const long long og = (long long)f * S, oz = ((long long)rz * F + f) * S,
-                                ofm = ((long long)rf * F + f) * S, ow = (long long)f * C;
-                const double w0 = ldp(w + ow + min(ia, C - 1)), w1 = ldp(w + ow + min(ib, C - 1));
-                const double g0 = ldp(pg + og + sa), g1 = ldp(pg + og + sb);
-                const double z0 = ldp(pz + (Z > 0 ? oz + sa : 0)), z1 = ldp(pz + (Z > 0 ? oz + sb : 0));
-                const double f0 = ldp(pf + (C == 3 && Fam > 0 ? ofm + sa : og + sa));
-                const double f1 = ldp(pf + (C == 3 && Fam > 0 ? ofm + sb : og + sb));
-                const double c0 = comp == 3 ? w0 : comp == 0 ? g0 : comp == 1 ? z0 : f0;
-                const double c1 = comp == 3 ? w1 : comp == 0 ? g1 : comp == 1 ? z1 : f1;
-                const double pr = prec_of(comp);
-                const bool raw = C == 2 && comp == 3;  // the weight pair as is (zone_sampling.py:440-443)
-                const double sum = raw ? 1.0 : c0 + c1;
-                const double t0d = raw ? c0 : c0 / sum, t1d = raw ? c1 : c1 / sum;
-                pl->c0[k] = c0;
-                pl->c1[k] = c1;
-                pl->sum[k] = sum;
-                pl->t0[k] = t0d;
-                pl->t1[k] = t1d;
-                pl->a0[k] = 1.0 + pr * t0d;
-                pl->a1[k] = 1.0 + pr * t1d;
-            }
+            const int cb = comp == 3 ? (1 + Z + Fam) * S : (comp == 0 ? 0 : (comp == 1 ? (1 + row) * S : (1 + Z + row) * S));
+            pl->ci0[k] = cb + ia;
+            pl->ci1[k] = cb + ib;
         }
         bsync();
         if (stamps) stamps[1] = __builtin_amdgcn_s_memtime();
+        {  // (COL) element e = k * ncol + i: unconditional loads with valid indices, then the stores
+            const int tot = la * ncol;
+            for (int e0 = 0; e0 < tot; e0 += 8 * NT) {
+                double v[8];
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    const int e = min(e0 + j * NT + tid, tot - 1);
+                    const int k = e / ncol;
+                    v[j] = ldp(col_src(pl->f[k], e - k * ncol));
+                }
+#pragma unroll
+                for (int j = 0; j < 8; j++)
+                    if (e0 + j * NT + tid < tot) plcol[e0 + j * NT + tid] = v[j];
+            }
+        }
+        bsync();
+        if (stamps) stamps[2] = __builtin_amdgcn_s_memtime();
+        if (tid < la && pl->comp[tid] >= 0) {  // (A2)
+            const int k = tid, comp = pl->comp[k];
+            const double c0 = plcol[k * ncol + pl->ci0[k]], c1 = plcol[k * ncol + pl->ci1[k]];
+            const double pr = prec_of(comp);
+            const bool raw = C == 2 && comp == 3;  // the weight pair as is (zone_sampling.py:440-443)
+            const double sum = raw ? 1.0 : c0 + c1;
+            const double t0d = raw ? c0 : c0 / sum, t1d = raw ? c1 : c1 / sum;
+            pl->c0[k] = c0;
+            pl->c1[k] = c1;
+            pl->sum[k] = sum;
+            pl->t0[k] = t0d;
+            pl->t1[k] = t1d;
+            pl->a0[k] = 1.0 + pr * t0d;
+            pl->a1[k] = 1.0 + pr * t1d;
+        }
+        wsync();
         {  // (B)
             const int kk = tid & 31, g = tid >> 5;
             if (tid < 64 && kk < la && pl->comp[kk] >= 0) {
@@ -680,8 +716,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                 pl->lu[k] = log(philox_uniform(k0, k1, chain, ctr0 + (uint64_t)(t0 + k) * WIN + (WIN - 1)));
             }
         }
-        bsync();
-        if (stamps) stamps[2] = __builtin_amdgcn_s_memtime();
+        wsync();
         if (tid < la && pl->comp[tid] >= 0) {  // (C)
             const int k = tid;
             const double g0 = pl->g[k][0], g1 = pl->g[k][1];
@@ -734,6 +769,15 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                     pl->dprior[kk] = dp;
                 }
             }
+            // waves 1-3: thread 64 + 8 k + 4 nu + h, the normalised weights of plan k (class h,
+            // before / after the move)
+            if (tid >= 64 && tid < 64 + 8 * la) {
+                const int q = tid - 64, k = q >> 3;
+                const int comp = pl->comp[k];
+                if (comp >= 0)
+                    norm_w(plcol + k * ncol + (1 + Z + Fam) * S, comp, pl->ia[k], pl->ib[k], pl->nv0[k],
+                           pl->nv1[k], q & 3, (q >> 2) & 1, plnw + k * 32 + (q & 7) * 4);
+            }
         }
         bsync();
         if (stamps) stamps[5] = __builtin_amdgcn_s_memtime();
@@ -751,14 +795,13 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             store_pending = false;
         }
     };
-    // prefetched column / observations of the next planned step (feature nx_f, -1 = none)
+    // prefetched observations of the next planned step (feature nx_f, -1 = none)
     int nx_f = -1;
-    double nx_cv[NCV];
     uint32_t nx_ow[OB];
     for (int step = 0; step < a.n_steps; step++) {
-        uint64_t tph[16];  // SBZ_MH_STAMP builds only
+        uint64_t tph[20];  // SBZ_MH_STAMP builds only
         if (SBZ_MH_STAMP)
-            for (int q = 10; q < 16; q++) tph[q] = 0;  // plan stages: 0 on steps without plans
+            for (int q = 10; q < 20; q++) tph[q] = 0;  // plan stages: 0 on steps without plans
         tph[0] = SBZ_MH_STAMP ? __builtin_amdgcn_s_memtime() : 0;
         if (rng.bad || broken) break;
         if (philox) rng.ctr = ctr0 + (uint64_t)step * WIN;
@@ -901,18 +944,15 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
 
         if (SBZ_MH_STAMP) tph[1] = __builtin_amdgcn_s_memtime();
         // ---- 2. Dirichlet proposal of the pair (zone_sampling.py:421-438, :537-569)
-        if (!(planned && comp >= 0 && nx_f == f)) fence_params();
+        if (!(planned && comp >= 0)) fence_params();  // planned steps read no parameters from HBM
         double nv0 = 0.0, nv1 = 0.0;
         double cv[NCV];
         uint32_t ow[OB];
         if (comp >= 0 && planned) {
-            if (nx_f == f) {  // prefetched during the previous step, and still current
-#pragma unroll
-                for (int q = 0; q < NCV; q++) cv[q] = nx_cv[q];
+            if (nx_f == f) {  // prefetched during the previous step
 #pragma unroll
                 for (int q = 0; q < OB; q++) ow[q] = nx_ow[q];
             } else {
-                col_load(f, cv);
                 obs_load(f, 0, ow);
             }
             nv0 = uni(pl->nv0[pk]);
@@ -957,21 +997,25 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                 part = delta_site(sa, zoa, zna);
                 if (sb >= 0) part = part + delta_site(sb, zna, NONE);
             } else if (comp >= 0 && !(SBZ_MH_ABLATE & 1)) {
-                if (store_pending) {  // published by col_store's barrier
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    store_pending = false;
-                }
-                col_store(f, cv);
-                part = delta_param(f, comp, row, ia, ib, nv0, nv1, ow, SBZ_MH_STAMP ? tph + 8 : nullptr);
+                // a planned step's column and weights are in plcol / plnw; otherwise staged here
+                if (!planned) col_store(f, cv);
+                part = delta_param(planned ? plcol + pk * ncol : col, planned ? plnw + pk * 32 : nullptr, f, comp,
+                                   row, ia, ib, nv0, nv1, ow, SBZ_MH_STAMP ? tph + 8 : nullptr);
             }
-            // the next step's column and observations, when it is a planned parameter move: in
-            // flight during this step's reduction and acceptance
+            // the next step's observations, when it is a planned parameter move: in flight during
+            // this step's reduction and acceptance
             nx_f = -1;
+#ifdef SBZ_MH_MARK
+            asm volatile("; PREFETCH_BEGIN");
+#endif
             if (philox && LAe > 1 && pk + 1 < LAe && step + 1 < a.n_steps && uni(okw[pk + 1]) != 0) {
                 nx_f = uni(pl->f[pk + 1]);
-                col_load(nx_f, nx_cv);
                 obs_load(nx_f, 0, nx_ow);
             }
+#ifdef SBZ_MH_MARK
+            asm volatile("; PREFETCH_END");
+#endif
+            if (SBZ_MH_STAMP) tph[18] = __builtin_amdgcn_s_memtime();
             int n_err = 0;
             delta = block_sum_di(part, err != 0 ? 1 : 0, n_err);
             if (n_err != 0) {  // a range check failed: stop before using the move
@@ -1031,10 +1075,21 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                     stp(base + ib, nv1);
                 }
                 store_pending = true;
-                // later plans that read this parameter row are stale: recomputed when reached
-                if (philox && lane < LAe && pl->comp[lane] == comp && pl->row[lane] == row && pl->f[lane] == f)
-                    okw[lane] = 0;
-                if (nx_f == f) nx_f = -1;  // the prefetched column holds the old values
+                if (philox && LAe > 1) {
+                    // later plans of the batch on this feature: their columns take the new values
+                    // (wave 0 writes, a barrier publishes them); a plan whose proposal read the
+                    // altered row (same component and row), or whose weights changed, is stale and
+                    // recomputed when reached
+                    const int k = min(lane, LA - 1);
+                    const bool in = lane < LAe && lane > pk && pl->comp[k] >= 0 && pl->f[k] == f;
+                    const int cb = comp == 3 ? (1 + Z + Fam) * S : (comp == 0 ? 0 : (comp == 1 ? (1 + row) * S : (1 + Z + row) * S));
+                    if (wv == 0 && in) {
+                        plcol[k * ncol + cb + ia] = nv0;
+                        plcol[k * ncol + cb + ib] = nv1;
+                    }
+                    if (in && (comp == 3 || (pl->comp[k] == comp && pl->row[k] == row))) okw[k] = 0;
+                    if (__ballot(in) != 0) bsync();  // the same ballot in every wave
+                }
             }
         }
         if (ch.trace_op && tid == 0) {
@@ -1047,8 +1102,10 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                 // phase k = tph[k] - tph[k-1] (1..4); sub-phases: start / end stamp pairs
                 const int k = SBZ_MH_STAMP;
                 // 13..17: make_plans stages A..E (0 on steps without plans)
-                const int e_[18] = {0, 1, 2, 3, 4, 4, 5, 6, 7, 2, 8, 9, 3, 11, 12, 13, 14, 15};
-                const int s_[18] = {0, 0, 1, 2, 3, 0, 1, 5, 6, 7, 2, 8, 9, 10, 11, 12, 13, 14};
+                // 18 gather loop, 19 the two logs, 20 next-step prefetch issue, 21 reduction to the
+                // end of phase 3 (parameter moves)
+                const int e_[22] = {0, 1, 2, 3, 4, 4, 5, 6, 7, 2, 8, 9, 3, 11, 12, 13, 14, 15, 16, 17, 18, 3};
+                const int s_[22] = {0, 0, 1, 2, 3, 0, 1, 5, 6, 7, 2, 8, 9, 10, 11, 12, 13, 14, 9, 16, 17, 18};
                 ch.trace_ll[t] = (double)(tph[e_[k]] - tph[s_[k]]);
             }
         }
@@ -1115,7 +1172,6 @@ int launch_mh(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg, const 
     a.n_steps = n_steps;
     a.min_size = cfg->min_size;
     a.warmup = cfg->warmup;
-    a.la = ctx->mh_la;
     // operators of the mode: zone moves + alter_* (mixture) or + Gibbs operators (source mode)
     bool allowed[SBZ_N_OPS] = {};
     allowed[SHRINK] = allowed[GROW] = allowed[SWAP] = true;
@@ -1180,10 +1236,26 @@ int launch_mh(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg, const 
         return fail(ctx, SBZ_EINVAL, "tape mode needs tape_pos and tape_len");
     if (src) return launch_mh_source(ctx, B, a);
     if (d.n_sites > 65535) return fail(ctx, SBZ_EINVAL, "sampler supports at most 65535 sites");
-    const size_t lds = mh_lds_bytes(d, ctx->C, a.geo_cost != nullptr);
-    if (lds > 64 * 1024) return fail(ctx, SBZ_EINVAL, "sampler state exceeds 64 KiB of LDS (too many sites)");
-    if (ctx->C == 3) mh_kernel<3, MH_WAVES><<<B, MH_WAVES * WAVE, lds, ctx->stream>>>(a);
-    else mh_kernel<2, MH_WAVES><<<B, MH_WAVES * WAVE, lds, ctx->stream>>>(a);
+    const bool geo = a.geo_cost != nullptr;
+    if (mh_lds_bytes(d, ctx->C, geo) > 64 * 1024)
+        return fail(ctx, SBZ_EINVAL, "sampler state exceeds 64 KiB of LDS (too many sites)");
+    // planned steps per batch (Philox only): as many as SBZ_MH_LA asks whose columns fit the LDS
+    auto lds_of = [&](int la) {
+        return MhLayout(d.n_sites, np_of(d.n_sites), d.n_states, d.n_zones, d.n_families, ctx->C, ctx->FamC,
+                        MH_WAVES * WAVE, geo, la).total;
+    };
+    constexpr size_t LDS_MAX = 160 * 1024;
+    int la = a.ch.tape ? 1 : std::min(ctx->mh_la, LA);
+    while (la > 1 && lds_of(la) > LDS_MAX) la--;
+    a.la = la;
+    const size_t lds = lds_of(la);
+    auto fn = ctx->C == 3 ? mh_kernel<3, MH_WAVES> : mh_kernel<2, MH_WAVES>;
+    if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX);
+        if (e != hipSuccess) return hip_fail(ctx, e, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
+    }
+    fn<<<B, MH_WAVES * WAVE, lds, ctx->stream>>>(a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(ctx, e, "sampler launch");
     return SBZ_OK;
