@@ -541,29 +541,47 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
         }
         const bool wid = block_sum_i(wide) != 0;  // (its barrier publishes the tables)
         if (stamps) stamps[1] = __builtin_amdgcn_s_memtime();
-        // gathers: position p = 256 k + 4 lane + j of the wave's chunks k = wv + NWV * i
+        // gathers: position p = 256 k + 4 lane + j of the wave's chunks k = wv + NWV * i, two
+        // chunks (8 positions per lane) at a time, all 16 table reads issued together.  Safe tables
+        // (every factor 0 or within 2^+-120): the 8 factors multiply as a tree, one renormalisation
+        // per pair of chunks; otherwise renormalise after every factor.
         double mn = 1.0, mo = 1.0;
         int en = 0, eo = 0;
         const int nci = (nch - wv + NWV - 1) / NWV;  // this wave's chunks
-        for (int i0 = 0; i0 < nci; i0 += OB) {
-            if (i0 > 0) obs_load(f, i0, o);
+        const unsigned char *tbo = reinterpret_cast<const unsigned char *>(tabo);
+        const unsigned char *tbn = reinterpret_cast<const unsigned char *>(tabn);
+        const uint32_t xsh = a.xs8 ? 0u : 3u;
+        for (int i0 = 0; i0 < nci; i0 += 2) {
+            if (i0 > 0 && (i0 & (OB - 1)) == 0) obs_load(f, i0, o);
+            const bool two = i0 + 1 < nci;
+            const int ka = wv + NWV * i0, kb = wv + NWV * (two ? i0 + 1 : i0);
+            const uint4 ra = *reinterpret_cast<const uint4 *>(rowp + ka * 256 + 4 * lane);
+            const uint4 rb = *reinterpret_cast<const uint4 *>(rowp + kb * 256 + 4 * lane);
+            const uint32_t oa = (i0 & 2) ? o[2] : o[0], ob = (i0 & 2) ? o[3] : o[1];
+            const uint32_t r8[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
+            double vo[8], vn[8];
 #pragma unroll
-            for (int i = 0; i < OB; i++) {
-                if (i0 + i >= nci) break;
-                const int k = wv + NWV * (i0 + i);
-                const uint4 rp = *reinterpret_cast<const uint4 *>(rowp + k * 256 + 4 * lane);
-                const uint32_t r4[4] = {rp.x, rp.y, rp.z, rp.w};
+            for (int j = 0; j < 8; j++) {
+                const uint32_t xb = ((j < 4 ? oa : ob) >> (8 * (j & 3))) & 0xffu;
+                const uint32_t ad = r8[j] + (xb << xsh);
+                vo[j] = *reinterpret_cast<const double *>(tbo + ad);
+                vn[j] = *reinterpret_cast<const double *>(tbn + ad);
+            }
+            if (!two) {
 #pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const uint32_t xb = (o[i] >> (8 * j)) & 0xffu;
-                    const uint32_t ad = r4[j] + (a.xs8 ? xb : (xb << 3));
-                    mo *= *reinterpret_cast<const double *>(reinterpret_cast<const unsigned char *>(tabo) + ad);
-                    mn *= *reinterpret_cast<const double *>(reinterpret_cast<const unsigned char *>(tabn) + ad);
-                    if (wid) {
-                        renorm(mo, eo);
-                        renorm(mn, en);
-                    }
+                for (int j = 4; j < 8; j++) vo[j] = vn[j] = 1.0;
+            }
+            if (wid) {
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    mo *= vo[j];
+                    renorm(mo, eo);
+                    mn *= vn[j];
+                    renorm(mn, en);
                 }
+            } else {
+                mo *= ((vo[0] * vo[1]) * (vo[2] * vo[3])) * ((vo[4] * vo[5]) * (vo[6] * vo[7]));
+                mn *= ((vn[0] * vn[1]) * (vn[2] * vn[3])) * ((vn[4] * vn[5]) * (vn[6] * vn[7]));
                 renorm(mo, eo);
                 renorm(mn, en);
             }
@@ -810,8 +828,29 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             make_plans(step, SBZ_MH_STAMP ? tph + 10 : nullptr);
         }
         const int pk = step - plan_t0;  // this step's plan (Philox, LAe > 1)
-        const bool planned = philox && LAe > 1 && uni(okw[pk]) != 0;
-        const int op = planned ? uni(pl->op[pk]) : rng.op(a.op_cdf, a.nops);
+        // the plan's fields, read in one batch (one LDS round trip)
+        int p_ok = 0, p_op = 0, p_comp = 0, p_row = 0, p_f = 0, p_ia = 0, p_ib = 0, p_okn = 0, p_fn = 0;
+        double p_nv0 = 0.0, p_nv1 = 0.0, p_lq = 0.0, p_lqb = 0.0, p_dp = 0.0, p_lu = 0.0;
+        if (philox && LAe > 1) {
+            const int pn = min(pk + 1, LA - 1);
+            p_ok = okw[pk];
+            p_op = pl->op[pk];
+            p_comp = pl->comp[pk];
+            p_row = pl->row[pk];
+            p_f = pl->f[pk];
+            p_ia = pl->ia[pk];
+            p_ib = pl->ib[pk];
+            p_okn = okw[pn];
+            p_fn = pl->f[pn];
+            p_nv0 = pl->nv0[pk];
+            p_nv1 = pl->nv1[pk];
+            p_lq = pl->lq[pk];
+            p_lqb = pl->lqb[pk];
+            p_dp = pl->dprior[pk];
+            p_lu = pl->lu[pk];
+        }
+        const bool planned = philox && LAe > 1 && uni(p_ok) != 0;
+        const int op = planned ? uni(p_op) : rng.op(a.op_cdf, a.nops);
         if (op < 0 || op > P_FAMILIES || (op == P_FAMILIES && (C == 2 || Fam == 0)) ||
             (op <= SWAP && Z == 0) || (op == P_ZONES && Z == 0)) {
             broken = true;
@@ -900,11 +939,11 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             }
         } else {
             if (planned) {
-                comp = uni(pl->comp[pk]);
-                row = uni(pl->row[pk]);
-                f = uni(pl->f[pk]);
-                ia = uni(pl->ia[pk]);
-                ib = uni(pl->ib[pk]);
+                comp = uni(p_comp);
+                row = uni(p_row);
+                f = uni(p_f);
+                ia = uni(p_ia);
+                ib = uni(p_ib);
             } else if (op == WEIGHTS) {
                 f = rng.below(F);
                 comp = 3;
@@ -955,11 +994,11 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             } else {
                 obs_load(f, 0, ow);
             }
-            nv0 = uni(pl->nv0[pk]);
-            nv1 = uni(pl->nv1[pk]);
-            log_q = uni(pl->lq[pk]);
-            log_q_back = uni(pl->lqb[pk]);
-            dprior = uni(pl->dprior[pk]);
+            nv0 = uni(p_nv0);
+            nv1 = uni(p_nv1);
+            log_q = uni(p_lq);
+            log_q_back = uni(p_lqb);
+            dprior = uni(p_dp);
         } else if (comp >= 0) {
             const double c0 = uni(ldp(base + ia)), c1 = uni(ldp(base + ib));
             if (SBZ_MH_STAMP) tph[5] = __builtin_amdgcn_s_memtime();
@@ -1008,8 +1047,8 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
 #ifdef SBZ_MH_MARK
             asm volatile("; PREFETCH_BEGIN");
 #endif
-            if (philox && LAe > 1 && pk + 1 < LAe && step + 1 < a.n_steps && uni(okw[pk + 1]) != 0) {
-                nx_f = uni(pl->f[pk + 1]);
+            if (philox && LAe > 1 && pk + 1 < LAe && step + 1 < a.n_steps && uni(p_okn) != 0) {
+                nx_f = uni(p_fn);
                 obs_load(nx_f, 0, nx_ow);
             }
 #ifdef SBZ_MH_MARK
@@ -1042,7 +1081,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
         } else {
             const double mh = (delta * 1.0) - (log_q - log_q_back) + dprior;
             if (philox && LAe > 1) {
-                accept = uni(pl->lu[pk]) < mh;
+                accept = uni(p_lu) < mh;
             } else {
                 if (philox) rng.ctr = ctr0 + (uint64_t)step * WIN + (WIN - 1);
                 accept = log(rng.real()) < mh;

@@ -423,7 +423,7 @@ __device__ __forceinline__ double cell_nw(const double (&n)[3], bool hz, bool hf
     return v;
 }
 
-// A table factor that keeps a 4-factor product of mantissas in the normal range: 0 or within
+// A table factor that keeps an 8-factor product of mantissas in the normal range: 0 or within
 // [2^-120, 2^120]; otherwise the gathers renormalise after every factor.
 __device__ __forceinline__ bool safe_cell(double v) { return v == 0.0 || (v >= 0x1p-120 && v <= 0x1p120); }
 
