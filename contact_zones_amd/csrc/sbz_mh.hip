@@ -76,7 +76,7 @@ struct Plans {
 // c (CH = NT * KT sites per chunk, nsc chunks); zos / nb / lst are padded to NpS = nsc * CH.
 struct MhLayout {
     int KT, CH, nsc, NpS, nent, ncol;
-    uint32_t col, zsize, red, nb, zos, selc, lst, stat, tabo, tabn, nw, rowp, ipos, clsinfo, plans, plcol,
+    uint32_t col, zsize, red, nb, zos, selc, lst, tabo, tabn, nw, rowp, ipos, plans, plcol,
         plnw, geo;
     size_t total;
     __host__ __device__ MhLayout(int N, int Np, int S, int Z, int Fam, int C, int FamC, int NT,
@@ -101,13 +101,11 @@ struct MhLayout {
         zos = take((size_t)NpS);
         selc = take((size_t)nsc * 16 * 4);  // per chunk: selected sites per wave of the last scan
         lst = take((size_t)NpS * 2);
-        stat = take(MH_STAT_INTS * 4);
         tabo = take((size_t)nent * 8);
         tabn = take((size_t)nent * 8);
         nw = take(32 * 8);
         rowp = take((size_t)Np * 4);
         ipos = take((size_t)N * 2);
-        clsinfo = take((size_t)((Z + 1) * FamC + 1) * 2);
         // geo prior scratch (geo_zone_prior): key [N] doubles, mem [N] u16, cnt + redd / redi [16]
         plans = take(sizeof(Plans));
         // the planned steps' parameter columns [la][ncol] and normalised weights [la][2][4][4]
@@ -149,7 +147,6 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
     uint8_t *zos = lds + L.zos;                                // [NpS] zone of site (NONE = none)
     int *selc = reinterpret_cast<int *>(lds + L.selc);         // [nsc][16] per-wave counts
     uint16_t *lst = reinterpret_cast<uint16_t *>(lds + L.lst); // [NpS] compacted members
-    int *stat = reinterpret_cast<int *>(lds + L.stat);         // [MH_STAT_INTS] proposed | accepted
     // Parameter moves gather from two per-step tables (see delta_param): T[cls][x], cls = zone
     // class * FamC + family class, one neutral row (cls = ncls) for padding positions.
     const int S1 = S + 1, FamC = a.FamC, ncls = (Z + 1) * FamC, row_bytes = S1 * 8;
@@ -159,7 +156,6 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
     double *nw = reinterpret_cast<double *>(lds + L.nw);         // [2][4][4] normalised weights
     uint32_t *rowp = reinterpret_cast<uint32_t *>(lds + L.rowp); // [Np] table row (bytes) by position
     uint16_t *ipos = reinterpret_cast<uint16_t *>(lds + L.ipos); // [N] position of each site
-    uint16_t *clsinfo = reinterpret_cast<uint16_t *>(lds + L.clsinfo);  // [ncls + 1] zone class | fc << 8
     double *plcol = reinterpret_cast<double *>(lds + L.plcol);  // [la][ncol] planned steps' columns
     double *plnw = reinterpret_cast<double *>(lds + L.plnw);    // [la][32] their normalised weights
 
@@ -212,7 +208,6 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
 
     // load the zone assignment; sizes
     for (int z = tid; z < Z; z += NT) zsize[z] = 0;
-    if (tid < MH_STAT_INTS) stat[tid] = 0;
     for (int s = tid; s < L.NpS; s += NT) nb[s] = 0;
     bsync();
     int occ = 0;
@@ -224,9 +219,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             occ++;
         }
     }
-    for (int c = tid; c <= ncls; c += NT)
-        clsinfo[c] = c == ncls ? (uint16_t)0xffffu : (uint16_t)((c / FamC) | ((c % FamC) << 8));
-    int occupied = block_sum_i(occ);  // (its barrier publishes zos / zsize / clsinfo)
+    int occupied = block_sum_i(occ);  // (its barrier publishes zos / zsize)
     // positions (family-sorted order of the likelihood context): site of each, its table row
     for (int p = tid; p < a.Np; p += NT) {
         uint32_t r = (uint32_t)(ncls * row_bytes);  // padding: the neutral row
@@ -501,23 +494,27 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             nwp = nw;
         }
         if (stamps) stamps[0] = __builtin_amdgcn_s_memtime();
-        // tables: entry e = cls * S1 + x, threads step through e by NT (cls, x kept incrementally)
-        int cls = tid / S1, x = tid - (tid / S1) * S1;
-        const int dq = NT / S1, dr = NT - dq * S1;
+        // tables: entry e = cls * S1 + x (zone class cls / FamC, family class cls % FamC; the
+        // neutral row cls = ncls).  Thread tid takes e = tid + NT u, two entries at a time with the
+        // LDS reads of both in flight (unconditional, valid indices; selects discard).
         int wide = 0;
-        for (int e = tid; e < nent; e += NT) {
-            const uint32_t ci = clsinfo[cls];
-            double to = 1.0, tn = 1.0;
-            if (ci != 0xffffu) {
-                const int zcl = (int)(ci & 0xffu), fc = (int)(ci >> 8);
+        for (int e0 = tid; e0 < nent; e0 += 2 * NT) {
+            double to[2], tn[2];
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const int e = min(e0 + u * NT, nent - 1);
+                const int cls = e / S1, x = e - cls * S1;
+                const bool real = cls < ncls;
+                const int zcl = real ? cls / FamC : 0, fc = real ? cls - (cls / FamC) * FamC : 0;
                 const bool na = x == S, hz = zcl > 0, hf = fc > 0;
                 const int xc = na ? 0 : x, h = (hz ? 1 : 0) | (hf ? 2 : 0);
                 const double l0 = cl[xc];
-                const double l1 = hz ? cl[zcl * S + xc] : 0.0;
-                const double l2 = hf ? cl[(Z + fc) * S + xc] : 0.0;
+                const double l1v = cl[zcl * S + xc], l2v = cl[(Z + fc) * S + xc];
+                const double l1 = hz ? l1v : 0.0;
+                const double l2 = hf ? l2v : 0.0;
                 const bool pick = !na && (x == ia || x == ib);
-                const bool changed = comp == 3 || (pick && (comp == 0 || (comp == 1 && zcl == row + 1) ||
-                                                            (comp == 2 && fc == row + 1)));
+                const bool changed = real && (comp == 3 || (pick && (comp == 0 || (comp == 1 && zcl == row + 1) ||
+                                                                     (comp == 2 && fc == row + 1))));
                 const double nv = x == ia ? va : vb;
                 const double n0 = comp == 0 && pick ? nv : l0;
                 const double n1 = comp == 1 && pick ? nv : l1;
@@ -526,18 +523,16 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                 const double wold[3] = {wo[0], wo[1], wo[2]}, wnew[3] = {wn[0], wn[1], wn[2]};
                 const double vo = cell_nw<C>(wold, hz, hf, na, l0, l1, l2);
                 const double vn = cell_nw<C>(wnew, hz, hf, na, n0, n1, n2);
-                to = changed ? vo : 1.0;
-                tn = changed ? vn : 1.0;
-                wide |= !(safe_cell(to) && safe_cell(tn)) ? 1 : 0;
+                to[u] = changed ? vo : 1.0;
+                tn[u] = changed ? vn : 1.0;
+                wide |= !(safe_cell(to[u]) && safe_cell(tn[u])) ? 1 : 0;
             }
-            tabo[e] = to;
-            tabn[e] = tn;
-            cls += dq;
-            x += dr;
-            if (x >= S1) {
-                x -= S1;
-                cls++;
-            }
+#pragma unroll
+            for (int u = 0; u < 2; u++)
+                if (e0 + u * NT < nent) {
+                    tabo[e0 + u * NT] = to[u];
+                    tabn[e0 + u * NT] = tn[u];
+                }
         }
         const bool wid = block_sum_i(wide) != 0;  // (its barrier publishes the tables)
         if (stamps) stamps[1] = __builtin_amdgcn_s_memtime();
@@ -813,6 +808,8 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             store_pending = false;
         }
     };
+    // per-operator counts: lane op counts operator op's proposals / acceptances (every wave alike)
+    int cnt_prop = 0, cnt_acc = 0;
     // prefetched observations of the next planned step (feature nx_f, -1 = none)
     int nx_f = -1;
     uint32_t nx_ow[OB];
@@ -1087,9 +1084,9 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                 accept = log(rng.real()) < mh;
             }
         }
-        if (tid == 0) stat[op]++;
+        cnt_prop += lane == op ? 1 : 0;
         if (accept) {
-            if (tid == 0) stat[SBZ_N_OPS + op]++;
+            cnt_acc += lane == op ? 1 : 0;
             ll = ll + delta;
             prior = prior + dprior;
             geo_cur = geo_new;
@@ -1164,8 +1161,8 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
         if (ch.status) ch.status[b] = broken ? 2 : (rng.bad ? 1 : 0);
     }
     if (tid < SBZ_N_OPS) {  // per-operator counters, one thread each
-        if (ch.accepted) ch.accepted[(size_t)b * SBZ_N_OPS + tid] += stat[SBZ_N_OPS + tid];
-        if (ch.proposed) ch.proposed[(size_t)b * SBZ_N_OPS + tid] += stat[tid];
+        if (ch.accepted) ch.accepted[(size_t)b * SBZ_N_OPS + tid] += cnt_acc;
+        if (ch.proposed) ch.proposed[(size_t)b * SBZ_N_OPS + tid] += cnt_prop;
     }
     // the first range-check failure (lowest thread): status 16 + code
     {
