@@ -129,19 +129,10 @@ def test_philox_carried_prior_matches_full_prior(gpu_available):
     assert np.any(s["prior"] != fx["init_prior"])  # the prior moved
 
 
-@pytest.mark.parametrize("N,F,S,Z,Fam,inh,B,steps", [
-    (3000, 40, 12, 3, 3, True, 6, 1500),    # two batches of observation chunks (Np = 4096)
-    (700, 30, 40, 2, 2, True, 6, 1500),     # S + 1 > 32: observation bytes hold x, not x * 8
-    (2000, 50, 10, 8, 4, True, 6, 1500),    # the bench shape's site count / zones / families
-    (300, 20, 5, 2, 0, False, 6, 1500),     # no inheritance (C = 2)
-    (2000, 500, 10, 8, 4, True, 256, 400),  # the bench's sampler leg: full cfg5 width, 256 chains
-])
-def test_philox_large_shapes_carried_ll(gpu_available, N, F, S, Z, Fam, inh, B, steps):
-    """Philox runs on shapes the golden tapes do not reach: the incrementally carried ll equals a
-    fresh full evaluation (likelihood kernel) within 1e-9 after every operator type ran, zones
-    stay disjoint and within bounds, and parameters stay normalised."""
+def _synthetic_chains(N, F, S, Z, Fam, inh, B):
+    """A Delaunay network of random sites, random observations, reference-initialised zones
+    (InitialSamples) and random parameters: sampler, chain state and likelihood engine."""
     import random
-    import torch
     from scipy.spatial import Delaunay
     from contact_zones_amd import packing
     from contact_zones_amd.likelihood import LikelihoodEngine
@@ -171,6 +162,22 @@ def test_philox_large_shapes_carried_ll(gpu_available, N, F, S, Z, Fam, inh, B, 
            "alter_p_global": 0.15, "alter_p_zones": 0.2, "alter_p_families": 0.1 if inh and Fam else 0.0}
     smp = Sampler(eng, states, indptr, indices, ops, [15, 40, 20, 20], 3)
     st = ChainState(eng, zos, w, pg, pz, pf)
+    return smp, st
+
+
+@pytest.mark.parametrize("N,F,S,Z,Fam,inh,B,steps", [
+    (3000, 40, 12, 3, 3, True, 6, 1500),    # two batches of observation chunks (Np = 4096)
+    (700, 30, 40, 2, 2, True, 6, 1500),     # S + 1 > 32: observation bytes hold x, not x * 8
+    (2000, 50, 10, 8, 4, True, 6, 1500),    # the bench shape's site count / zones / families
+    (300, 20, 5, 2, 0, False, 6, 1500),     # no inheritance (C = 2)
+    (2000, 500, 10, 8, 4, True, 256, 400),  # the bench's sampler leg: full cfg5 width, 256 chains
+])
+def test_philox_large_shapes_carried_ll(gpu_available, N, F, S, Z, Fam, inh, B, steps):
+    """Philox runs on shapes the golden tapes do not reach: the incrementally carried ll equals a
+    fresh full evaluation (likelihood kernel) within 1e-9 after every operator type ran, zones
+    stay disjoint and within bounds, and parameters stay normalised."""
+    import torch
+    smp, st = _synthetic_chains(N, F, S, Z, Fam, inh, B)
     out = smp.run(st, steps, 40, 0.85, seed=5)
     torch.cuda.synchronize()
     assert out["status"].cpu().numpy().tolist() == [0] * B
@@ -265,3 +272,23 @@ def test_philox_planned_proposals_do_not_change_trajectories(gpu_available, monk
             np.testing.assert_array_equal(base[1][k], other[1][k], err_msg=k)
         np.testing.assert_array_equal(base[2], other[2])
         np.testing.assert_array_equal(base[3], other[3])
+
+
+def test_planned_batches_cut_by_lds(gpu_available, monkeypatch):
+    """Wide parameter columns (S = 60, Z = 6, Fam = 4: 663 doubles per planned step) leave room
+    in the 160 KiB for fewer than 24 planned steps (about 20 here): the host cuts the batch, and
+    the trajectory stays bit-identical to the one-step-at-a-time path."""
+    import torch
+    runs = []
+    for la in ("1", "24"):
+        monkeypatch.setenv("SBZ_MH_LA", la)
+        smp, st = _synthetic_chains(300, 30, 60, 6, 4, True, 8)
+        out = smp.run(st, 600, 40, 0.85, seed=9, trace=True)
+        torch.cuda.synchronize()
+        runs.append(({k: out[k].cpu().numpy() for k in ("op", "accept", "ll", "status")}, st.to_numpy()))
+    assert runs[0][0]["status"].tolist() == [0] * 8
+    assert runs[0][0]["accept"][:, :].sum() > 50
+    for k in runs[0][0]:
+        np.testing.assert_array_equal(runs[0][0][k], runs[1][0][k], err_msg=k)
+    for k in runs[0][1]:
+        np.testing.assert_array_equal(runs[0][1][k], runs[1][1][k], err_msg=k)
