@@ -39,7 +39,8 @@ namespace sbz {
 #endif
 #ifndef SBZ_MH_ABLATE
 #define SBZ_MH_ABLATE 0  // diagnostic builds only (wrong results): 1 = no parameter-move delta,
-                         // 2 = no Dirichlet proposal math, 4 = no zone-move delta
+                         // 2 = no Dirichlet proposal math, 4 = no zone-move delta, 8 = accepted
+                         // parameter moves not stored to HBM
 #endif
 
 namespace {
@@ -810,9 +811,6 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
     };
     // per-operator counts: lane op counts operator op's proposals / acceptances (every wave alike)
     int cnt_prop = 0, cnt_acc = 0;
-    // prefetched observations of the next planned step (feature nx_f, -1 = none)
-    int nx_f = -1;
-    uint32_t nx_ow[OB];
     for (int step = 0; step < a.n_steps; step++) {
         uint64_t tph[20];  // SBZ_MH_STAMP builds only
         if (SBZ_MH_STAMP)
@@ -824,12 +822,14 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             fence_params();
             make_plans(step, SBZ_MH_STAMP ? tph + 10 : nullptr);
         }
+#ifdef SBZ_MH_MARK
+        asm volatile("; PH1_BEGIN");
+#endif
         const int pk = step - plan_t0;  // this step's plan (Philox, LAe > 1)
         // the plan's fields, read in one batch (one LDS round trip)
-        int p_ok = 0, p_op = 0, p_comp = 0, p_row = 0, p_f = 0, p_ia = 0, p_ib = 0, p_okn = 0, p_fn = 0;
+        int p_ok = 0, p_op = 0, p_comp = 0, p_row = 0, p_f = 0, p_ia = 0, p_ib = 0;
         double p_nv0 = 0.0, p_nv1 = 0.0, p_lq = 0.0, p_lqb = 0.0, p_dp = 0.0, p_lu = 0.0;
         if (philox && LAe > 1) {
-            const int pn = min(pk + 1, LA - 1);
             p_ok = okw[pk];
             p_op = pl->op[pk];
             p_comp = pl->comp[pk];
@@ -837,8 +837,6 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             p_f = pl->f[pk];
             p_ia = pl->ia[pk];
             p_ib = pl->ib[pk];
-            p_okn = okw[pn];
-            p_fn = pl->f[pn];
             p_nv0 = pl->nv0[pk];
             p_nv1 = pl->nv1[pk];
             p_lq = pl->lq[pk];
@@ -846,6 +844,9 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             p_dp = pl->dprior[pk];
             p_lu = pl->lu[pk];
         }
+#ifdef SBZ_MH_MARK
+        asm volatile("; PH1_READ");
+#endif
         const bool planned = philox && LAe > 1 && uni(p_ok) != 0;
         const int op = planned ? uni(p_op) : rng.op(a.op_cdf, a.nops);
         if (op < 0 || op > P_FAMILIES || (op == P_FAMILIES && (C == 2 || Fam == 0)) ||
@@ -978,6 +979,9 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             poff = off;
         }
 
+#ifdef SBZ_MH_MARK
+        asm volatile("; PH1_END");
+#endif
         if (SBZ_MH_STAMP) tph[1] = __builtin_amdgcn_s_memtime();
         // ---- 2. Dirichlet proposal of the pair (zone_sampling.py:421-438, :537-569)
         if (!(planned && comp >= 0)) fence_params();  // planned steps read no parameters from HBM
@@ -985,12 +989,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
         double cv[NCV];
         uint32_t ow[OB];
         if (comp >= 0 && planned) {
-            if (nx_f == f) {  // prefetched during the previous step
-#pragma unroll
-                for (int q = 0; q < OB; q++) ow[q] = nx_ow[q];
-            } else {
-                obs_load(f, 0, ow);
-            }
+            obs_load(f, 0, ow);
             nv0 = uni(p_nv0);
             nv1 = uni(p_nv1);
             log_q = uni(p_lq);
@@ -1038,19 +1037,6 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                 part = delta_param(planned ? plcol + pk * ncol : col, planned ? plnw + pk * 32 : nullptr, f, comp,
                                    row, ia, ib, nv0, nv1, ow, SBZ_MH_STAMP ? tph + 8 : nullptr);
             }
-            // the next step's observations, when it is a planned parameter move: in flight during
-            // this step's reduction and acceptance
-            nx_f = -1;
-#ifdef SBZ_MH_MARK
-            asm volatile("; PREFETCH_BEGIN");
-#endif
-            if (philox && LAe > 1 && pk + 1 < LAe && step + 1 < a.n_steps && uni(p_okn) != 0) {
-                nx_f = uni(p_fn);
-                obs_load(nx_f, 0, nx_ow);
-            }
-#ifdef SBZ_MH_MARK
-            asm volatile("; PREFETCH_END");
-#endif
             if (SBZ_MH_STAMP) tph[18] = __builtin_amdgcn_s_memtime();
             int n_err = 0;
             delta = block_sum_di(part, err != 0 ? 1 : 0, n_err);
@@ -1106,7 +1092,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                 occupied += (zna < Z ? 1 : -1) + (sb >= 0 ? -1 : 0);
                 bsync();
             } else {
-                if (tid == 0) {
+                if (tid == 0 && !(SBZ_MH_ABLATE & 8)) {
                     stp(base + ia, nv0);
                     stp(base + ib, nv1);
                 }
@@ -1138,7 +1124,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                 // phase k = tph[k] - tph[k-1] (1..4); sub-phases: start / end stamp pairs
                 const int k = SBZ_MH_STAMP;
                 // 13..17: make_plans stages A..E (0 on steps without plans)
-                // 18 gather loop, 19 the two logs, 20 next-step prefetch issue, 21 reduction to the
+                // 18 gather loop, 19 the two logs, 20 logs to the reduction, 21 reduction to the
                 // end of phase 3 (parameter moves)
                 const int e_[22] = {0, 1, 2, 3, 4, 4, 5, 6, 7, 2, 8, 9, 3, 11, 12, 13, 14, 15, 16, 17, 18, 3};
                 const int s_[22] = {0, 0, 1, 2, 3, 0, 1, 5, 6, 7, 2, 8, 9, 10, 11, 12, 13, 14, 9, 16, 17, 18};
