@@ -39,8 +39,7 @@ namespace sbz {
 #endif
 #ifndef SBZ_MH_ABLATE
 #define SBZ_MH_ABLATE 0  // diagnostic builds only (wrong results): 1 = no parameter-move delta,
-                         // 2 = no Dirichlet proposal math, 4 = no zone-move delta, 8 = accepted
-                         // parameter moves not stored to HBM
+                         // 2 = no Dirichlet proposal math, 4 = no zone-move delta
 #endif
 
 namespace {
@@ -1092,7 +1091,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                 occupied += (zna < Z ? 1 : -1) + (sb >= 0 ? -1 : 0);
                 bsync();
             } else {
-                if (tid == 0 && !(SBZ_MH_ABLATE & 8)) {
+                if (tid == 0) {
                     stp(base + ia, nv0);
                     stp(base + ib, nv1);
                 }
