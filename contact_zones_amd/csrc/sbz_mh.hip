@@ -63,6 +63,7 @@ constexpr int MAX_NWV = 8;
 struct Plans {
     int op[LA], comp[LA], row[LA], f[LA], ia[LA], ib[LA];
     int ci0[LA], ci1[LA];  // column positions of the altered pair
+    int off[LA];           // offset of the altered row in its array (w / p_global / p_zones / p_fam)
     int ok[MAX_NWV][LA];
     uint64_t cd[LA];  // Philox counter of the Dirichlet lane streams
     double c0[LA], c1[LA], sum[LA], t0[LA], t1[LA], a0[LA], a1[LA], n0[LA], n1[LA];
@@ -663,19 +664,25 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                         int j0 = below(n - 1);
                         if (j0 >= i0) j0++;
                         ia = a.app_list[(size_t)f * S + i0];
-                        ib = a.app_list[(size_t)f * S + j0];
+                        ib = a.app_list[(size_t)f * S + max(j0, 0)];  // (n < 2: invalid below)
                         comp = op == P_GLOBAL ? 0 : (op == P_ZONES ? 1 : 2);
                     }
                 }
             }
+            // the sequential path's checks of the move (an invalid one is left to it: it stops
+            // the chain with the same status)
+            const int lim = comp == 3 ? C : S;
+            const bool valid = comp >= 0 && f >= 0 && f < F && ia >= 0 && ib >= 0 && ia != ib && ia < lim &&
+                               ib < lim && row >= 0 && !(comp == 1 && row >= Z) && !(comp == 2 && row >= Fam);
             pl->op[k] = op;
             pl->comp[k] = comp;
             pl->row[k] = row;
             pl->f[k] = f;
             pl->ia[k] = ia;
             pl->ib[k] = ib;
+            pl->off[k] = comp == 3 ? f * C : (row * F + f) * S;
 #pragma unroll
-            for (int w = 0; w < NWV; w++) pl->ok[w][k] = comp >= 0 ? 1 : 0;
+            for (int w = 0; w < NWV; w++) pl->ok[w][k] = valid ? 1 : 0;
             pl->cd[k] = c;
             const int cb = comp == 3 ? (1 + Z + Fam) * S : (comp == 0 ? 0 : (comp == 1 ? (1 + row) * S : (1 + Z + row) * S));
             pl->ci0[k] = cb + ia;
@@ -811,7 +818,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
     // per-operator counts: lane op counts operator op's proposals / acceptances (every wave alike)
     int cnt_prop = 0, cnt_acc = 0;
     for (int step = 0; step < a.n_steps; step++) {
-        uint64_t tph[20];  // SBZ_MH_STAMP builds only
+        uint64_t tph[22];  // SBZ_MH_STAMP builds only
         if (SBZ_MH_STAMP)
             for (int q = 10; q < 20; q++) tph[q] = 0;  // plan stages: 0 on steps without plans
         tph[0] = SBZ_MH_STAMP ? __builtin_amdgcn_s_memtime() : 0;
@@ -821,12 +828,13 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             fence_params();
             make_plans(step, SBZ_MH_STAMP ? tph + 10 : nullptr);
         }
+        if (SBZ_MH_STAMP) tph[20] = __builtin_amdgcn_s_memtime();
 #ifdef SBZ_MH_MARK
         asm volatile("; PH1_BEGIN");
 #endif
         const int pk = step - plan_t0;  // this step's plan (Philox, LAe > 1)
         // the plan's fields, read in one batch (one LDS round trip)
-        int p_ok = 0, p_op = 0, p_comp = 0, p_row = 0, p_f = 0, p_ia = 0, p_ib = 0;
+        int p_ok = 0, p_op = 0, p_comp = 0, p_row = 0, p_f = 0, p_ia = 0, p_ib = 0, p_off = 0;
         double p_nv0 = 0.0, p_nv1 = 0.0, p_lq = 0.0, p_lqb = 0.0, p_dp = 0.0, p_lu = 0.0;
         if (philox && LAe > 1) {
             p_ok = okw[pk];
@@ -836,6 +844,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             p_f = pl->f[pk];
             p_ia = pl->ia[pk];
             p_ib = pl->ib[pk];
+            p_off = pl->off[pk];
             p_nv0 = pl->nv0[pk];
             p_nv1 = pl->nv1[pk];
             p_lq = pl->lq[pk];
@@ -848,6 +857,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
 #endif
         const bool planned = philox && LAe > 1 && uni(p_ok) != 0;
         const int op = planned ? uni(p_op) : rng.op(a.op_cdf, a.nops);
+        if (SBZ_MH_STAMP) tph[21] = __builtin_amdgcn_s_memtime();
         if (op < 0 || op > P_FAMILIES || (op == P_FAMILIES && (C == 2 || Fam == 0)) ||
             (op <= SWAP && Z == 0) || (op == P_ZONES && Z == 0)) {
             broken = true;
@@ -934,14 +944,16 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                 zoa = z;
                 zna = NONE;
             }
+        } else if (planned) {
+            // checked when planned (make_plans stage A; an invalid move is never planned)
+            comp = uni(p_comp);
+            row = uni(p_row);
+            f = uni(p_f);
+            ia = uni(p_ia);
+            ib = uni(p_ib);
+            base = (comp == 3 ? w : (comp == 0 ? pg : (comp == 1 ? pz : pf))) + uni(p_off);
         } else {
-            if (planned) {
-                comp = uni(p_comp);
-                row = uni(p_row);
-                f = uni(p_f);
-                ia = uni(p_ia);
-                ib = uni(p_ib);
-            } else if (op == WEIGHTS) {
+            if (op == WEIGHTS) {
                 f = rng.below(F);
                 comp = 3;
                 if (C == 3) rng.pair(nullptr, 3, ia, ib);
@@ -1125,8 +1137,9 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                 // 13..17: make_plans stages A..E (0 on steps without plans)
                 // 18 gather loop, 19 the two logs, 20 logs to the reduction, 21 reduction to the
                 // end of phase 3 (parameter moves)
-                const int e_[22] = {0, 1, 2, 3, 4, 4, 5, 6, 7, 2, 8, 9, 3, 11, 12, 13, 14, 15, 16, 17, 18, 3};
-                const int s_[22] = {0, 0, 1, 2, 3, 0, 1, 5, 6, 7, 2, 8, 9, 10, 11, 12, 13, 14, 9, 16, 17, 18};
+                // 22 loop top and plans, 23 plan read and operator, 24 the rest of phase 1
+                const int e_[25] = {0, 1, 2, 3, 4, 4, 5, 6, 7, 2, 8, 9, 3, 11, 12, 13, 14, 15, 16, 17, 18, 3, 20, 21, 1};
+                const int s_[25] = {0, 0, 1, 2, 3, 0, 1, 5, 6, 7, 2, 8, 9, 10, 11, 12, 13, 14, 9, 16, 17, 18, 0, 20, 21};
                 ch.trace_ll[t] = (double)(tph[e_[k]] - tph[s_[k]]);
             }
         }

@@ -223,7 +223,7 @@ struct Rng {
         int j = below(n - 1);
         if (j >= i) j++;
         a = uni(pop ? pop[i] : i);
-        b = uni(pop ? pop[j] : j);
+        b = uni(pop ? pop[max(j, 0)] : j);  // n < 2: j = -1, a pair the caller's checks reject
     }
     // np.random.dirichlet(alpha) for 2 components; Philox mode: the two gammas run at once on
     // lanes 0 and 1, each on its own lane stream (LaneRng) based at the current counter
