@@ -484,6 +484,14 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
         o4[1] = w1 / sum;
         o4[2] = C == 3 ? w2 / sum : 0.0;
     };
+    // table entry e = cls * S1 + x as x | zone class << 8 | family class << 16 | (cls < ncls) << 24
+    auto tdecomp = [&](int e) -> uint32_t {
+        const int cls = e / S1, x = e - cls * S1;
+        const bool real = cls < ncls;
+        const int zcl = real ? cls / FamC : 0, fc = real ? cls - (cls / FamC) * FamC : 0;
+        return (uint32_t)x | ((uint32_t)zcl << 8) | ((uint32_t)fc << 16) | ((real ? 1u : 0u) << 24);
+    };
+    const uint32_t tdec[2] = {tdecomp(min(tid, nent - 1)), tdecomp(min(tid + NT, nent - 1))};
     // `cl` is feature f's column in LDS (the staged col, or a planned step's column) and `nwp` its
     // normalised weights before (nwp[0..15]) and after (nwp[16..31]) the move, or null: computed
     // here into nw.
@@ -499,14 +507,18 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
         // neutral row cls = ncls).  Thread tid takes e = tid + NT u, two entries at a time with the
         // LDS reads of both in flight (unconditional, valid indices; selects discard).
         int wide = 0;
-        for (int e0 = tid; e0 < nent; e0 += 2 * NT) {
+        int it = 0;
+        for (int e0 = tid; e0 < nent; e0 += 2 * NT, it++) {
             double to[2], tn[2];
 #pragma unroll
             for (int u = 0; u < 2; u++) {
                 const int e = min(e0 + u * NT, nent - 1);
-                const int cls = e / S1, x = e - cls * S1;
-                const bool real = cls < ncls;
-                const int zcl = real ? cls / FamC : 0, fc = real ? cls - (cls / FamC) * FamC : 0;
+                // the first pass's entries were decomposed once (tdec); later ones divide here
+                uint32_t dc;
+                if (it == 0) dc = tdec[u];
+                else dc = tdecomp(e);
+                const int x = (int)(dc & 0xffu), zcl = (int)((dc >> 8) & 0xffu), fc = (int)((dc >> 16) & 0xffu);
+                const bool real = (dc >> 24) != 0;
                 const bool na = x == S, hz = zcl > 0, hf = fc > 0;
                 const int xc = na ? 0 : x, h = (hz ? 1 : 0) | (hf ? 2 : 0);
                 const double l0 = cl[xc];
