@@ -64,6 +64,7 @@ struct Plans {
     int op[LA], comp[LA], row[LA], f[LA], ia[LA], ib[LA];
     int ci0[LA], ci1[LA];  // column positions of the altered pair
     int off[LA];           // offset of the altered row in its array (w / p_global / p_zones / p_fam)
+    uint32_t fm[LA];       // bit j: later plan j moves a parameter of the same feature
     int ok[MAX_NWV][LA];
     uint64_t cd[LA];  // Philox counter of the Dirichlet lane streams
     double c0[LA], c1[LA], sum[LA], t0[LA], t1[LA], a0[LA], a1[LA], n0[LA], n1[LA];
@@ -699,6 +700,13 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             const int cb = comp == 3 ? (1 + Z + Fam) * S : (comp == 0 ? 0 : (comp == 1 ? (1 + row) * S : (1 + Z + row) * S));
             pl->ci0[k] = cb + ia;
             pl->ci1[k] = cb + ib;
+            // later plans of the same feature (compared through the lanes of wave 0)
+            uint32_t fmask = 0;
+            for (int j = 1; j < la; j++) {
+                const int fj = __builtin_amdgcn_readlane(f, j), cj = __builtin_amdgcn_readlane(comp, j);
+                fmask |= (j > k && comp >= 0 && cj >= 0 && fj == f) ? (1u << j) : 0u;
+            }
+            pl->fm[k] = fmask;
         }
         bsync();
         if (stamps) stamps[1] = __builtin_amdgcn_s_memtime();
@@ -847,6 +855,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
         const int pk = step - plan_t0;  // this step's plan (Philox, LAe > 1)
         // the plan's fields, read in one batch (one LDS round trip)
         int p_ok = 0, p_op = 0, p_comp = 0, p_row = 0, p_f = 0, p_ia = 0, p_ib = 0, p_off = 0;
+        uint32_t p_fm = 0;
         double p_nv0 = 0.0, p_nv1 = 0.0, p_lq = 0.0, p_lqb = 0.0, p_dp = 0.0, p_lu = 0.0;
         if (philox && LAe > 1) {
             p_ok = okw[pk];
@@ -857,6 +866,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             p_ia = pl->ia[pk];
             p_ib = pl->ib[pk];
             p_off = pl->off[pk];
+            p_fm = pl->fm[pk];
             p_nv0 = pl->nv0[pk];
             p_nv1 = pl->nv1[pk];
             p_lq = pl->lq[pk];
@@ -1120,13 +1130,15 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                     stp(base + ib, nv1);
                 }
                 store_pending = true;
-                if (philox && LAe > 1) {
-                    // later plans of the batch on this feature: their columns take the new values
-                    // (wave 0 writes, a barrier publishes them); a plan whose proposal read the
-                    // altered row (same component and row), or whose weights changed, is stale and
-                    // recomputed when reached
+                // later plans of the batch on this feature (p_fm, made when planned; a step that is
+                // not planned compares them here): their columns take the new values (wave 0
+                // writes, a barrier publishes them); a plan whose proposal read the altered row
+                // (same component and row), or whose weights changed, is stale and recomputed when
+                // reached
+                const uint32_t later = !philox || LAe <= 1 ? 0u : planned ? (uint32_t)uni((int)p_fm) : ~0u;
+                if (later != 0) {
                     const int k = min(lane, LA - 1);
-                    const bool in = lane < LAe && lane > pk && pl->comp[k] >= 0 && pl->f[k] == f;
+                    const bool in = lane < LAe && lane > pk && ((later >> k) & 1u) && pl->comp[k] >= 0 && pl->f[k] == f;
                     const int cb = comp == 3 ? (1 + Z + Fam) * S : (comp == 0 ? 0 : (comp == 1 ? (1 + row) * S : (1 + Z + row) * S));
                     if (wv == 0 && in) {
                         plcol[k * ncol + cb + ia] = nv0;
