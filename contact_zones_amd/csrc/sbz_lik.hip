@@ -45,7 +45,10 @@ namespace {
 constexpr double LN2 = 0.69314718055994530941723212145818;
 constexpr int WAVE = 64;
 constexpr int ZR = 2;        // zone classes per lane held in registers
-constexpr int MIX_WAVES = 3; // launch bound of the dense kernel: waves per SIMD (162 VGPRs)
+#ifndef SBZ_MIX_WAVES
+#define SBZ_MIX_WAVES 3
+#endif
+constexpr int MIX_WAVES = SBZ_MIX_WAVES; // launch bound of the dense kernel: waves per SIMD
 constexpr int RN = 4;        // product chains checked and renormalised once per RN features
 constexpr int GIF = 16;      // table reads in flight per wave (scheduling barrier every GIF)
 
@@ -643,8 +646,11 @@ __global__ __launch_bounds__(WAVE) void lik_source_generic_kernel(LikArgs a) {
 // task re-run per factor when one left the normal range, e.g. a zero weight's -inf cell).
 // ---------------------------------------------------------------------------------------
 constexpr int SRC_NWC = 32;  // features per normalised-weight batch
+#ifndef SBZ_SRC_RC_WAVES
+#define SBZ_SRC_RC_WAVES 2  // launch bound: waves per SIMD (3 spills: 262 vs 246 us per launch)
+#endif
 template <int C, int SPL, bool XS8>
-__global__ __launch_bounds__(WAVE, 3) void lik_source_rc_kernel(LikArgs a) {
+__global__ __launch_bounds__(WAVE, SBZ_SRC_RC_WAVES) void lik_source_rc_kernel(LikArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     constexpr int NO = SPL / 4;
     const int lane = threadIdx.x;
