@@ -448,6 +448,8 @@ struct MhArgs {
     int n_steps, nops, min_size, warmup;
     int la;     // mh_kernel, Philox draws: proposals planned ahead per batch (1 = none; <= 6)
     int stage;  // mh_src_kernel: parameters and normalised weights staged in LDS for the N*F passes
+    int cstage; // mh_src_kernel (with stage): the constant tables (applicable states, Gibbs prior
+                //   counts, 'counts' prior) staged in LDS too
     double op_cdf[SBZ_N_OPS];
     double prec[4];
     const uint8_t *obs_fm;      // [F][Np] by position

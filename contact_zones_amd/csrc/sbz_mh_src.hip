@@ -33,6 +33,18 @@
 
 namespace sbz {
 
+#ifndef SBZ_SRC_STAMP
+#define SBZ_SRC_STAMP 0  // diagnostic builds only: trace_ll holds the shader cycles of phase k (1 op
+                         // draw, 2 operator body, 3 accept to step end, 4 whole step, 5 resample
+                         // loop, 6 resample reductions, 7 zone move: pass_logq, 8 zone move: site
+                         // selection, 9 Gibbs p: counts, 10 Gibbs p: redraw_rows, 11 Gibbs: pass_ll,
+                         // 12 accept + commit, 13 step trailer) instead of ll
+#endif
+#define SRC_TS(i) \
+    do {          \
+        if (SBZ_SRC_STAMP) tph[i] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+
 namespace {
 
 // The component likelihoods and normalised weights of observation (s, f) (update_component_
@@ -86,10 +98,19 @@ size_t mh_src_lds_bytes(const sbz_dims &d, int C, bool hbm_sources, bool geo, bo
            ((N + 1) & ~(size_t)1) * 2 +
            (hbm_sources ? 0 : ((N * F + 15) & ~(size_t)15) * 2) + ((N + 15) & ~(size_t)15) +
            ((F + 15) & ~(size_t)15) + (geo ? 16 + geo_scratch_bytes((int)N) : 0) +
-           // redraw_rows: draws [F][S] doubles, per-feature tape offsets and counter ranks [F] ints
-           16 + F * S * 8 + 2 * F * 4 + 8 +
+           // redraw_rows / weight gammas: draws [F][max(S, 2)] doubles, per-feature tape offsets and
+           // counter ranks [F] ints
+           16 + F * (S > 2 ? S : 2) * 8 + 2 * F * 4 + 8 + 8 + SBZ_N_OPS * 8 +
            // staged parameters: normalised weights [F][4][3], p_global, p_zones, p_families
            (stage ? 16 + (12 * F + (1 + Z + (C == 3 ? (size_t)d.n_families : 0)) * F * S) * 8 + N * F + N : 0);
+}
+
+// LDS bytes of the staged constant tables (a.cstage): 'counts' prior and Gibbs prior counts of
+// p_global / p_families where set, applicable states [F][S] and their counts [F] as bytes
+size_t mh_src_const_bytes(const sbz_dims &d, int C, bool alg, bool alf, bool gcg, bool gcf) {
+    const size_t FS = (size_t)d.n_features * d.n_states, Fam = C == 3 ? (size_t)d.n_families : 0;
+    return 16 + 8 * FS * ((alg ? 1 : 0) + (gcg ? 1 : 0) + Fam * ((alf ? 1 : 0) + (gcf ? 1 : 0))) + FS +
+           (size_t)d.n_features + 16;
 }
 
 namespace {
@@ -141,7 +162,11 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     uint8_t *zos = srcb + (GS ? 0 : ((NF + 15) & ~15));              // [N] zone of site
     uint8_t *sub = zos + ((N + 15) & ~15);                           // [F] feature subset
     // geo prior scratch (geo_zone_prior), 16-B aligned after the subset
-    const size_t geo_off = ((size_t)(sub + ((F + 15) & ~15) - lds) + 15) & ~(size_t)15;
+    // (offsets from sizes, not pointer differences against the LDS base)
+    const size_t sub_end = (size_t)2 * MH_SRC_MAX_WAVES * (8 + 4) + (size_t)ncnt * 4 + (size_t)((Z + 1) & ~1) * 4 +
+                           (size_t)MH_STAT_INTS * 4 + (size_t)((N + 1) & ~1) * 2 +
+                           (GS ? 0 : (size_t)2 * ((NF + 15) & ~15)) + (size_t)((N + 15) & ~15) + (size_t)((F + 15) & ~15);
+    const size_t geo_off = (sub_end + 15) & ~(size_t)15;
     double *geo_key = reinterpret_cast<double *>(lds + geo_off);
     uint16_t *geo_mem = reinterpret_cast<uint16_t *>(geo_key + N);
     int *geo_cnt = reinterpret_cast<int *>(geo_mem + ((N + 7) & ~7));
@@ -149,13 +174,19 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     int *geo_ri = reinterpret_cast<int *>(geo_rd + 16);
     // redraw_rows scratch, 16-B aligned after the geo scratch
     const size_t par_off = (geo_off + (a.geo_cost ? geo_scratch_bytes(N) : 0) + 15) & ~(size_t)15;
-    double *gbuf = reinterpret_cast<double *>(lds + par_off);  // [F][S] draws
-    int *fpre = reinterpret_cast<int *>(gbuf + (size_t)F * S);  // [F] tape offset of feature f
+    double *gbuf = reinterpret_cast<double *>(lds + par_off);  // [F][max(S, 2)] draws
+    int *fpre = reinterpret_cast<int *>(gbuf + (size_t)F * max(S, 2));  // [F] tape offset of feature f
     int *frank = fpre + F;                                      // [F] counter rank of feature f
     int *misc_i = frank + F;                                    // [2] totals of those scans
     // a.stage: the N*F passes read the chain's parameters and normalised weights from LDS copies
     // (staged when a pass starts after the parameters changed) instead of L2
-    const size_t stg_off = ((size_t)(reinterpret_cast<unsigned char *>(misc_i + 2) - lds) + 15) & ~(size_t)15;
+    // the operator CDF (once per launch), 8-B aligned after misc_i
+    const size_t cdf_off = (par_off + (size_t)F * max(S, 2) * 8 + (size_t)F * 8 + 8 + 7) & ~(size_t)7;
+    double *cdf = reinterpret_cast<double *>(lds + cdf_off);  // [SBZ_N_OPS]
+    // (read through a local-address-space pointer: ds_read, not a flat load)
+    const __attribute__((address_space(3))) double *cdf3 =
+        (const __attribute__((address_space(3))) double *)((__attribute__((address_space(3))) unsigned char *)lds + cdf_off);
+    const size_t stg_off = (cdf_off + (size_t)SBZ_N_OPS * 8 + 15) & ~(size_t)15;
     double *lnw = reinterpret_cast<double *>(lds + stg_off);  // [F][4][3] by h = hz | hf << 1
     double *lpg = lnw + (size_t)F * 12;                        // [F][S]
     double *lpz = lpg + (size_t)F * S;                         // [Z][F][S]
@@ -164,6 +195,32 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     uint8_t *lfam = lobs + NF;                                                 // [N] family class
     const bool stg = a.stage != 0;
     bool stg_ok = false;
+    // a.cstage: the constant tables, after the staged parameters (16-B aligned)
+    const bool cst = a.cstage != 0;
+    const size_t cst_off = (stg_off + ((size_t)F * 12 + (size_t)(1 + Z + Fam) * F * S) * 8 + (size_t)NF + N + 15) & ~(size_t)15;
+    const int FS = F * S;
+    // (the global tables are read with ldp, as before staging: a plain LDS load and an atomic
+    // global one are never merged into one load through a generic pointer)
+    double *c_alg = reinterpret_cast<double *>(lds + cst_off);   // [F][S] if alpha_g
+    double *c_alf = c_alg + (a.alpha_g ? FS : 0);                  // [Fam][F][S] if alpha_f
+    double *c_gcg = c_alf + (a.alpha_f ? Fam * FS : 0);            // [F][S] if gc_g
+    double *c_gcf = c_gcg + (a.gc_g ? FS : 0);                     // [Fam][F][S] if gc_f
+    uint8_t *c_app = reinterpret_cast<uint8_t *>(c_gcf + (a.gc_f ? Fam * FS : 0));  // [F][S]
+    uint8_t *c_acnt = c_app + FS;                                                   // [F]
+    auto app_cnt = [&](int f) -> int { return cst ? (int)c_acnt[f] : a.app_cnt[f]; };
+    auto app_list = [&](int f, int j) -> int { return cst ? (int)c_app[f * S + j] : a.app_list[(size_t)f * S + j]; };
+    // Gibbs prior count of component comp's row `row` at i = f * S + x (1 where none is set)
+    auto gcv = [&](int comp, int row, int i) -> double {
+        if (comp == 0 && a.gc_g) return cst ? c_gcg[i] : ldp(a.gc_g + i);
+        if (comp == 2 && a.gc_f) return cst ? c_gcf[(size_t)row * FS + i] : ldp(a.gc_f + (size_t)row * FS + i);
+        return 1.0;
+    };
+    // 'counts' prior alpha (p_global, p_families) at i, where set
+    auto has_al = [&](int comp) { return (comp == 0 && a.alpha_g) || (comp == 2 && a.alpha_f); };
+    auto alv = [&](int comp, int row, int i) -> double {
+        if (comp == 0) return cst ? c_alg[i] : ldp(a.alpha_g + i);
+        return cst ? c_alf[(size_t)row * FS + i] : ldp(a.alpha_f + (size_t)row * FS + i);
+    };
 
     uint8_t *gzos = ch.zone_of_site + (size_t)b * N;
     uint8_t *gsrc = ch.source + (size_t)b * NF;
@@ -224,6 +281,19 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         for (int c = tid; c < NF; c += NT) lobs[c] = a.obs_sm[c];
         for (int s = tid; s < N; s += NT) lfam[s] = C == 3 ? a.fam_site[s] : 0;
     }
+    if (tid < SBZ_N_OPS - 1) cdf[tid] = a.op_cdf[tid];
+    if (cst) {  // so do the constant tables
+        for (int i = tid; i < FS; i += NT) {
+            c_app[i] = (uint8_t)a.app_list[i];
+            if (a.alpha_g) c_alg[i] = a.alpha_g[i];
+            if (a.gc_g) c_gcg[i] = a.gc_g[i];
+        }
+        for (int i = tid; i < Fam * FS; i += NT) {
+            if (a.alpha_f) c_alf[i] = a.alpha_f[i];
+            if (a.gc_f) c_gcf[i] = a.gc_f[i];
+        }
+        for (int f = tid; f < F; f += NT) c_acnt[f] = (uint8_t)a.app_cnt[f];
+    }
     if (tid < MH_STAT_INTS) stat[tid] = 0;
     for (int s = tid; s < N; s += NT) nb[s] = 0;
     if (!GS)
@@ -263,6 +333,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     int err = 0;
     long long err_val = 0;
     uint16_t stamp = 0;
+    uint64_t tr0 = 0, tr1 = 0, tr2 = 0;  // SBZ_SRC_STAMP builds only: resample start / loop end / end
 
     // ---- zone-move helpers (as the SAMPLE_SOURCE = false kernel, sbz_mh.hip).  The scans over
     // the sites run in every wave (identical results); the stamps are written by all threads.
@@ -414,6 +485,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     // redraw every source from the current sample's posterior into srcb; returns log q (sum log
     // posterior[new source]) and the new log-likelihood
     auto pass_resample = [&](double &log_q_s, double &ll_new) {
+        if (SBZ_SRC_STAMP) tr0 = __builtin_amdgcn_s_memtime();
         ensure_staged();
         LaneRng lr;
         lr.initw(rng, tid);
@@ -439,9 +511,11 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         } else {
             rng.ctr++;
         }
+        if (SBZ_SRC_STAMP) tr1 = __builtin_amdgcn_s_memtime();
         log_q_s = bsum(acc_q.value());
         const double v = bsum(acc_l.value());
         ll_new = bor(zero_w) ? -INFINITY : v;
+        if (SBZ_SRC_STAMP) tr2 = __builtin_amdgcn_s_memtime();
     };
     auto commit_sources = [&]() {
         for (int c = tid; c < NF; c += NT) wsrc(src, c, rsrc(srcb, c));
@@ -478,7 +552,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     // if al != null.
     // (the generator's fields come in as values and go out through pos / ctr / bad: the lambda
     // does not touch `rng`, which keeps it in registers)
-    auto redraw_rows = [&](double *base, double *lbase, const double *gc, double gc_default, const double *al,
+    auto redraw_rows = [&](double *base, double *lbase, int comp, int row,
                            const double *tape, int64_t len, uint32_t key0, uint32_t key1,
                            uint64_t chain, int64_t &pos, uint64_t &ctr, int &bad) -> double {
         // every (feature, state) draw at once: thread t <-> (f, j) = (t / S, t % S).  Feature f's
@@ -490,7 +564,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             for (int f0 = 0; f0 < F; f0 += WAVE) {
                 const int f = f0 + lane;
                 const int in = f < F && sub[f];
-                int v = in ? a.app_cnt[f] : 0;
+                int v = in ? app_cnt(f) : 0;
 #pragma unroll
                 for (int o = 1; o < WAVE; o <<= 1) {
                     const int t = __shfl_up(v, o, WAVE);
@@ -498,7 +572,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                 }
                 const uint64_t m = __ballot(in);
                 if (f < F) {
-                    fpre[f] = cn + v - (in ? a.app_cnt[f] : 0);
+                    fpre[f] = cn + v - (in ? app_cnt(f) : 0);
                     frank[f] = cr + lane_prefix(m);
                 }
                 cn += uni(__shfl(v, WAVE - 1, WAVE));
@@ -514,19 +588,18 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         const int64_t pos0 = pos;
         const uint64_t ctr0 = ctr;
         const bool have = !tape || pos0 + tot_n <= len;
-        const int FS = F * S;
         for (int t = tid; t < FS; t += NT) {
             const int f = t / S, j = t - f * S;
-            const bool act = sub[f] && j < a.app_cnt[f];
+            const bool act = sub[f] && j < app_cnt(f);
             double g = 0.0;
             if (act) {
                 if (tape) {
                     g = have ? tape[pos0 + fpre[f] + j] : 0.0;
                 } else {
-                    const int x = a.app_list[(size_t)f * S + j];
+                    const int x = app_list(f, j);
                     LaneRng lr;
                     lr.initk(key0, key1, chain, ctr0 + (uint64_t)frank[f], j);
-                    const double alpha = (gc ? ldp(gc + (size_t)f * S + x) : gc_default) + (double)cnt[f * S + x];
+                    const double alpha = gcv(comp, row, f * S + x) + (double)cnt[f * S + x];
                     g = lr.gamma(alpha);
                 }
             }
@@ -534,9 +607,10 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         }
         sync();
         double dp = 0.0;
+        const bool al = has_al(comp);
         for (int t = tid; t < FS; t += NT) {
             const int f = t / S, j = t - f * S;
-            const int n = a.app_cnt[f];
+            const int n = app_cnt(f);
             if (!(sub[f] && j < n)) continue;
             double g = gbuf[t];
             if (!tape) {
@@ -544,27 +618,45 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                 for (int i = 0; i < n; i++) tot += gbuf[f * S + i];
                 g = g / tot;
             }
-            const int x = a.app_list[(size_t)f * S + j];
-            double *row = base + (size_t)f * S;
-            const double old = ldp(row + x);
-            stp(row + x, g);
-            if (lbase) lbase[(size_t)f * S + x] = g;  // the staged copy follows
+            const int x = app_list(f, j);
+            double *prow = base + (size_t)f * S;
+            // the current value: the staged copy once staged (an exact copy), else the global row
+            const double old = stg_ok ? lbase[(size_t)f * S + x] : ldp(prow + x);
+            stp(prow + x, g);
+            if (stg) lbase[(size_t)f * S + x] = g;  // the staged copy follows
             if (al) {
-                const double am1 = ldp(al + (size_t)f * S + x) - 1.0;
+                const double am1 = alv(comp, row, f * S + x) - 1.0;
                 dp += xlogy(am1, g) - xlogy(am1, old);
             }
         }
         bad = have ? 0 : 1;
         pos = uni64(pos0 + (tape ? tot_n : 0));
         ctr = (uint64_t)uni64((int64_t)(ctr0 + (tape ? 0 : (uint64_t)tot_r)));
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // once the parameters are staged every later read of them is the LDS copy (passes, `old`
+        // above), so the global stores need not have landed before the next barrier; the alias copy
+        // and the end of the kernel wait for them
+        if (!(stg && stg_ok)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         return bsum(dp);
     };
 
     bool broken = false;
     for (int step = 0; step < a.n_steps; step++) {
+        uint64_t tph[12] = {};  // SBZ_SRC_STAMP builds only
+        tr0 = tr1 = tr2 = 0;
+        SRC_TS(0);
         if (rng.bad || broken) break;
-        const int op = rng.op(a.op_cdf, a.nops);
+        // rng.op with the CDF in LDS: numpy choice(p), the number of cdf entries <= u
+        int op;
+        if (rng.tape) {
+            op = uni((int)rng.tape_item());
+        } else {
+            const double u = rng.uniform53();
+            int i = 0;
+#pragma unroll
+            for (int k = 0; k < SBZ_N_OPS - 1; k++) i += (k < a.nops - 1 && !(u < cdf3[k])) ? 1 : 0;
+            op = uni(i);
+        }
+        SRC_TS(1);
         const bool zone_op = op <= SWAP;
         if (!(zone_op || (op >= G_SOURCES && op <= G_P_FAMILIES)) || (zone_op && Z == 0) ||
             (op == G_P_ZONES && Z == 0) || (op == G_P_FAMILIES && (C == 2 || Fam == 0))) {
@@ -580,6 +672,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         if (zone_op) {
             // ---- zone move with source resampling
             const double log_q_back_s = pass_logq();
+            SRC_TS(6);
             log_q = 0.0;
             log_q_back = -INFINITY;
             const int n_free = N - occupied;
@@ -650,6 +743,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                     if (sb >= 0) zos[sb] = NONE;
                 }
                 sync();
+                SRC_TS(7);
                 if (a.geo_cost && (zna == Z - 1 || zoa == Z - 1)) {  // the last zone changed
                     geo_new = geo_prior();
                     dprior = uni(dprior + (geo_new - geo_cur));
@@ -672,10 +766,13 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                 break;
             }
             clear_cnt();
-            for (int c = tid; c < NF; c += NT) {
-                const int s = c / F, f = c - s * F;
-                const bool in = (C == 2 || fixed == 0) ? zos[s] < Z : a.fam_site[s] > 0;
-                if (in) atomicAdd(&cnt[f * C + rsrc(src, c)], 1);
+            {
+                CellWalk cw{tid / F, tid - (tid / F) * F, cdS, cdF, F};
+                for (int c = tid; c < NF; c += NT, cw.next()) {
+                    const int s = cw.s, f = cw.f;
+                    const bool in = (C == 2 || fixed == 0) ? zos[s] < Z : (stg ? lfam[s] : a.fam_site[s]) > 0;
+                    if (in) atomicAdd(&cnt[f * C + rsrc(src, c)], 1);
+                }
             }
             sync();
             LaneRng lr;
@@ -683,6 +780,17 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             const int64_t pos0 = rng.pos;
             const int64_t need = 2LL * F;  // C == 2: F pairs; C == 3: F beta draws + F uniforms
             const bool have = !rng.tape || pos0 + need <= rng.len;
+            if (!rng.tape) {
+                // Philox: the 2F gammas in parallel, thread t -> feature t / 2, gamma t % 2 (C == 2:
+                // g0 / g1 of Dirichlet(1 + counts); C == 3: ga / gb of the Beta ratio), into gbuf
+                for (int t = tid; t < 2 * F; t += NT) {
+                    const int f = t >> 1, k = t & 1;
+                    const int cc = C == 2 ? cnt[f * C + k]
+                                          : (k == 0 ? cnt[f * C + (fixed == 0 ? 1 : 2)] : cnt[f * C]);
+                    gbuf[t] = lr.gamma(1.0 + cc);
+                }
+                sync();
+            }
             for (int f = tid; f < F; f += NT) {
                 double *wf = w + (size_t)f * C;
                 if (C == 2) {
@@ -691,7 +799,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                         d0 = have ? rng.tape[pos0 + 2 * f] : 0.5;
                         d1 = have ? rng.tape[pos0 + 2 * f + 1] : 0.5;
                     } else {
-                        const double g0 = lr.gamma(1.0 + cnt[f * C]), g1 = lr.gamma(1.0 + cnt[f * C + 1]);
+                        const double g0 = gbuf[2 * f], g1 = gbuf[2 * f + 1];
                         d0 = g0 / (g0 + g1);
                         d1 = g1 / (g0 + g1);
                     }
@@ -699,12 +807,11 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                     stp(wf + 1, d1);
                     if (stg) stage_nw(f, d0, d1, 0.0);
                 } else {
-                    const int cu = cnt[f * C], cx = cnt[f * C + (fixed == 0 ? 1 : 2)];
                     double r;
                     if (rng.tape) {
                         r = have ? rng.tape[pos0 + f] : 0.5;
                     } else {
-                        const double ga = lr.gamma(1.0 + cx), gb = lr.gamma(1.0 + cu);
+                        const double ga = gbuf[2 * f], gb = gbuf[2 * f + 1];
                         r = ga / (ga + gb);
                     }
                     double w0 = ldp(wf), w1 = ldp(wf + 1), w2 = ldp(wf + 2);
@@ -742,32 +849,39 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             }
             const int comp = op == G_P_GLOBAL ? 0 : (op == G_P_ZONES ? 1 : 2);
             clear_cnt();
-            for (int c = tid; c < NF; c += NT) {
-                const int s = c / F, f = c - s * F;
-                const int x = stg ? lobs[c] : a.obs_sm[c];
-                bool in = sub[f] && rsrc(src, c) == comp && x < S;
-                if (comp == 1) in = in && zos[s] == row;
-                if (comp == 2) in = in && a.fam_site[s] == row + 1;
-                if (in) atomicAdd(&cnt[f * S + x], 1);
+            {
+                CellWalk cw{tid / F, tid - (tid / F) * F, cdS, cdF, F};
+                for (int c = tid; c < NF; c += NT, cw.next()) {
+                    const int s = cw.s, f = cw.f;
+                    const int x = stg ? lobs[c] : a.obs_sm[c];
+                    bool in = sub[f] && rsrc(src, c) == comp && x < S;
+                    if (comp == 1) in = in && zos[s] == row;
+                    if (comp == 2) in = in && (stg ? lfam[s] : a.fam_site[s]) == row + 1;
+                    if (in) atomicAdd(&cnt[f * S + x], 1);
+                }
             }
             sync();
+            SRC_TS(8);
             double *base = comp == 0 ? pg : (comp == 1 ? pz + (size_t)row * F * S : pf + (size_t)row * F * S);
-            const double *gc = comp == 0 ? a.gc_g : (comp == 2 && a.gc_f ? a.gc_f + (size_t)row * F * S : nullptr);
-            const double *al = comp == 0 ? a.alpha_g : (comp == 2 && a.alpha_f ? a.alpha_f + (size_t)row * F * S : nullptr);
             int64_t rpos = rng.pos;
             uint64_t rctr = rng.ctr;
             int rbad = 0;
-            double *lbase = !stg ? nullptr : (comp == 0 ? lpg : (comp == 1 ? lpz + (size_t)row * F * S
-                                                                         : lpf + (size_t)row * F * S));
-            dprior = redraw_rows(base, lbase, gc, 1.0, al, rng.tape, rng.len, rng.key0, rng.key1, rng.chain,
+            // (an LDS address, used only when the parameters are staged)
+            double *lbase = comp == 0 ? lpg : (comp == 1 ? lpz + (size_t)row * F * S : lpf + (size_t)row * F * S);
+            dprior = redraw_rows(base, lbase, comp, row, rng.tape, rng.len, rng.key0, rng.key1, rng.chain,
                                  rpos, rctr, rbad);
             rng.pos = rpos;
             rng.ctr = rctr;
             if (rbad) rng.bad = 1;
-            gsync();  // the new rows are visible to every thread (and their staged copies)
+            // the new rows are visible to every thread (the staged copies; the global rows too
+            // before the parameters are staged)
+            if (stg && stg_ok) sync();
+            else gsync();
+            SRC_TS(9);
             ll_new = pass_ll(src);
         }
 
+        SRC_TS(2);
         // ---- metropolis_hastings_ratio (mcmc_generative.py:307-318)
         bool accept;
         if (log_q_back == -INFINITY) accept = false;
@@ -797,8 +911,10 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             }
             sync();
         }
+        SRC_TS(10);
         if (alias && accept && op != G_SOURCES && op != G_P_GLOBAL && op != G_P_ZONES &&
             op != G_P_FAMILIES) {
+            gsync();  // every thread's parameter stores have landed
             // this accept replaces the reference's Sample object: the arrays of the logged
             // sample stop changing here (sbz.h, alias_pending)
             const size_t fs = (size_t)F * S;
@@ -810,12 +926,27 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                     ch.alias_p_fam[b * Fam * fs + k] = ldp(pf + k);
             alias = 0;
         }
+        if (SBZ_SRC_STAMP) {
+            sync();
+            SRC_TS(3);
+        }
         if (ch.trace_op && tid == 0) {
             const size_t t = (size_t)b * a.n_steps + step;
             ch.trace_op[t] = (int8_t)op;
             ch.trace_accept[t] = accept ? 1 : 0;
             ch.trace_ll[t] = ll;
+            if (SBZ_SRC_STAMP) {
+                tph[11] = tr0;
+                tph[4] = tr1;
+                tph[5] = tr2;
+                // phase k: [end, start] time points
+                constexpr int PE[14] = {0, 1, 2, 3, 3, 4, 5, 6, 7, 8, 9, 2, 10, 3};
+                constexpr int PS[14] = {0, 0, 1, 2, 0, 11, 4, 1, 6, 1, 8, 9, 2, 10};
+                constexpr int k = SBZ_SRC_STAMP;
+                ch.trace_ll[t] = tph[PE[k]] >= tph[PS[k]] && tph[PS[k]] != 0 ? (double)(tph[PE[k]] - tph[PS[k]]) : 0.0;
+            }
         }
+
         if (ch.trace_zos) {
             uint8_t *tz = ch.trace_zos + ((size_t)b * a.n_steps + step) * N;
             for (int s = tid; s < N; s += NT) tz[s] = zos[s];
@@ -857,7 +988,12 @@ int launch_mh_source(sbz_ctx *ctx, int B, const MhArgs &a0) {
     const bool gs = ctx->src_hbm || mh_src_lds_bytes(ctx->d, ctx->C, false, geo, false) > LDS_MAX;  // do not fit: HBM
     // parameters staged in LDS when they fit too (SBZ_SRC_STAGE=0: off)
     a.stage = ctx->src_stage && mh_src_lds_bytes(ctx->d, ctx->C, gs, geo, true) <= LDS_MAX ? 1 : 0;
-    const size_t lds = mh_src_lds_bytes(ctx->d, ctx->C, gs, geo, a.stage != 0);
+    size_t lds = mh_src_lds_bytes(ctx->d, ctx->C, gs, geo, a.stage != 0);
+    // the constant tables too, when they fit beside the staged parameters
+    const size_t cst = mh_src_const_bytes(ctx->d, ctx->C, a.alpha_g != nullptr, a.alpha_f != nullptr,
+                                          a.gc_g != nullptr, a.gc_f != nullptr);
+    a.cstage = a.stage && ctx->d.n_states <= 255 && lds + cst <= LDS_MAX ? 1 : 0;
+    if (a.cstage) lds += cst;
     if (lds > LDS_MAX)
         return fail(ctx, SBZ_EINVAL, "SAMPLE_SOURCE sampler needs " + std::to_string(lds) +
                                          " B of LDS per chain even with the sources in HBM (> 160 KiB)");
