@@ -102,6 +102,7 @@ SIGNATURES = {
                         ctypes.POINTER(sbz_tape), ctypes.POINTER(sbz_state), ctypes.POINTER(sbz_trace)]),
     "sbz_mh_lds_bytes": (ctypes.c_uint64, [ctypes.POINTER(sbz_dims)]),
     "sbz_last_kernels": (ctypes.c_char_p, [_P]),
+    "sbz_draw_gamma": (_I, [_P, ctypes.c_int32, _P, ctypes.c_uint64, _P]),
 }
 
 _lib = None

@@ -574,6 +574,26 @@ int sbz_mh_run(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg, uint6
     return e == hipSuccess ? SBZ_OK : hip_fail(ctx, e, "sbz_mh_run: D2H");
 }
 
+int sbz_draw_gamma(sbz_ctx *ctx, int32_t n, const double *alpha, uint64_t seed, double *out) {
+    if (!ctx) return SBZ_EINVAL;
+    if (n < 0 || (n > 0 && (!alpha || !out))) return fail(ctx, SBZ_EINVAL, "sbz_draw_gamma: bad arguments");
+    for (int i = 0; i < n; i++)
+        if (!(alpha[i] > 0.0) || !std::isfinite(alpha[i])) return fail(ctx, SBZ_EINVAL, "sbz_draw_gamma: alpha must be finite and > 0");
+    if (n == 0) return SBZ_OK;
+    (void)hipSetDevice(ctx->device);
+    const size_t bytes = (size_t)n * sizeof(double);
+    int rc = ensure(ctx, ctx->mh_stage, 2 * bytes);
+    if (rc) return rc;
+    double *d_alpha = static_cast<double *>(ctx->mh_stage.ptr), *d_out = d_alpha + n;
+    hipError_t e = hipMemcpyAsync(d_alpha, alpha, bytes, hipMemcpyHostToDevice, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "sbz_draw_gamma: H2D");
+    rc = launch_draw_gamma(ctx, n, d_alpha, seed, d_out);
+    if (rc) return rc;
+    e = hipMemcpyAsync(out, d_out, bytes, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    return e == hipSuccess ? SBZ_OK : hip_fail(ctx, e, "sbz_draw_gamma: D2H");
+}
+
 uint64_t sbz_mh_lds_bytes(const sbz_dims *dims) {
     if (!dims) return 0;
     const size_t b = mh_lds_bytes(*dims, (dims->flags & SBZ_INHERITANCE) ? 3 : 2);

@@ -103,6 +103,8 @@ inline int np_of(int n_sites) {
 // Sampler (sbz_mh.hip)
 size_t mh_lds_bytes(const sbz_dims &d, int C, bool geo = false);
 int launch_mh(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg, const sbz_chains *chains);
+// sbz_draw_gamma: n gamma draws of the samplers' generator (device arrays)
+int launch_draw_gamma(sbz_ctx *ctx, int n, const double *alpha, uint64_t seed, double *out);
 
 // Launch the likelihood kernels for B chains (all pointers device); out_ll device [B].
 int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, const double *pg,

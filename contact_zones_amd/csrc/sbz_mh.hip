@@ -1209,6 +1209,23 @@ size_t mh_lds_bytes(const sbz_dims &d, int C, bool geo) {
                     MH_WAVES * WAVE, geo).total;
 }
 
+namespace {
+// sbz_draw_gamma: draw i from LaneRng stream (key = seed, chain = i / 64, lane i % 64, counter 0)
+__global__ __launch_bounds__(256) void draw_gamma_kernel(int n, const double *alpha, uint64_t seed, double *out) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    LaneRng lr;
+    lr.initk((uint32_t)seed, (uint32_t)(seed >> 32), (uint64_t)(i / 64), 0, i % 64);
+    out[i] = lr.gamma(alpha[i]);
+}
+}  // namespace
+
+int launch_draw_gamma(sbz_ctx *ctx, int n, const double *alpha, uint64_t seed, double *out) {
+    draw_gamma_kernel<<<(n + 255) / 256, 256, 0, ctx->stream>>>(n, alpha, seed, out);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? SBZ_OK : hip_fail(ctx, e, "draw_gamma_kernel launch");
+}
+
 int launch_mh(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg, const sbz_chains *chains) {
     const sbz_dims &d = ctx->d;
     if (!ctx->d_adj_ptr) return fail(ctx, SBZ_ESTATE, "sbz_set_network must be called before sbz_mh_run_device");

@@ -128,6 +128,12 @@ uint64_t sbz_lik_lds_bytes(const sbz_dims *dims, int source_mode);
  * "repack_source_kernel lik_source_rc_kernel"), "" before the first. */
 const char *sbz_last_kernels(const sbz_ctx *ctx);
 
+/* Diagnostics: n draws of the samplers' gamma generator (LaneRng::gamma, Marsaglia-Tsang on
+ * Philox4x32-10 uniforms; the Dirichlet draws of alter_* / gibbs_sample_* in Philox mode), draw i
+ * with shape alpha[i] from its own stream (key = seed, chain = i / 64, lane i % 64).  Host
+ * arrays [n]; for distribution tests.  Returns 0 or a negative code. */
+int sbz_draw_gamma(sbz_ctx *ctx, int32_t n, const double *alpha, uint64_t seed, double *out);
+
 /* ------------------------------------------------------------------------------------------
  * Metropolis-Hastings sampler  (MCMCGenerative.step, sbayes/sampling/mcmc_generative.py:282-351,
  * operators of ZoneMCMC / ZoneMCMCWarmup, sbayes/sampling/zone_sampling.py:408-933, 1272-1577;

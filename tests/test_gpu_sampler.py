@@ -292,3 +292,31 @@ def test_planned_batches_cut_by_lds(gpu_available, monkeypatch):
         np.testing.assert_array_equal(runs[0][0][k], runs[1][0][k], err_msg=k)
     for k in runs[0][1]:
         np.testing.assert_array_equal(runs[0][1][k], runs[1][1][k], err_msg=k)
+
+
+@pytest.mark.parametrize("alpha", [0.3, 1.0, 1.7, 4.0, 31.0, 250.0])
+def test_gamma_generator_distribution(gpu_available, alpha):
+    """The samplers' gamma generator (LaneRng::gamma: Marsaglia-Tsang, two Box-Muller candidates
+    per round; the Dirichlet draws of the Philox-mode operators) against Gamma(alpha, 1):
+    Kolmogorov-Smirnov on 2^17 draws, and the first two moments."""
+    import ctypes
+    from scipy import stats
+    from contact_zones_amd.likelihood import LikelihoodEngine
+    eng = LikelihoodEngine(np.zeros((4, 3), np.int8), np.full(4, 255, np.uint8), 2, 1, 0, False)
+    n = 1 << 17
+    a = np.full(n, alpha)
+    out = np.empty(n)
+    rc = eng._lib.sbz_draw_gamma(eng.ctx, n, a.ctypes.data_as(ctypes.c_void_p), 12345 + int(alpha * 10),
+                                 out.ctypes.data_as(ctypes.c_void_p))
+    assert rc == 0
+    assert np.all(np.isfinite(out)) and np.all(out > 0)
+    ks = stats.kstest(out, stats.gamma(alpha).cdf)
+    assert ks.pvalue > 1e-4, ks
+    se = np.sqrt(alpha / n)  # standard error of the mean
+    assert abs(out.mean() - alpha) < 6 * se
+    assert abs(out.var() / alpha - 1.0) < 0.05
+    # reproducible: same seed, same draws
+    out2 = np.empty(n)
+    eng._lib.sbz_draw_gamma(eng.ctx, n, a.ctypes.data_as(ctypes.c_void_p), 12345 + int(alpha * 10),
+                            out2.ctypes.data_as(ctypes.c_void_p))
+    np.testing.assert_array_equal(out, out2)
