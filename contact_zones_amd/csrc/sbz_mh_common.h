@@ -244,9 +244,6 @@ __device__ __forceinline__ double philox_uniform(uint32_t key0, uint32_t key1, u
 // j counts the lane's draws in the phase.  The counter's high word goes into c3 (bits 0..19; a
 // counter stays far below 2^52), so a chain's lane streams never repeat when its counter passes
 // 2^32; the host keeps global chain ids below 2^32 (c2).
-#ifndef SBZ_GAMMA1
-#define SBZ_GAMMA1 0
-#endif
 struct LaneRng {
     uint32_t k0, k1, base, c2, c3, j;
     // one Philox block gives two uniforms (words 0-1 and 2-3): the second is kept for the next call
@@ -294,17 +291,16 @@ struct LaneRng {
         // cos(2 pi u2) as cospi(2 u2): no large-argument reduction (u2 in [0, 1))
         return sqrt(-2.0 * log(u1)) * cospi(2.0 * u2);
     }
-    // Marsaglia-Tsang (alpha >= 1; boosted by u^(1/alpha) below 1).  Each round takes both
-    // normals of one Box-Muller pair as two candidates in turn (each with its own acceptance
-    // uniform), so a lane accepts in its first round with probability > 0.997 and a wave, which
-    // loops until its last lane accepts, mostly runs one round instead of two or three.  At most
-    // 32 rounds (64 candidates, each accepted with probability > 0.95).
+    // Marsaglia-Tsang (alpha >= 1; boosted by u^(1/alpha) below 1), at most 64 rounds (each
+    // accepts with probability > 0.95; reaching 64 has probability < 1e-80).  A two-candidate
+    // form (both normals of one Box-Muller pair per round, so a wave mostly runs one round) was
+    // measured slower on the cfg5 sampler (5.03 vs 4.82 us per step) and equal on the source
+    // sampler (profiles/r03_ab_gamma.txt).
     __device__ __forceinline__ double gamma(double alpha) {
         const double boost = alpha < 1.0 ? pow(u(), 1.0 / alpha) : 1.0;
         const double a = alpha < 1.0 ? alpha + 1.0 : alpha;
         const double d = a - 1.0 / 3.0, c = 1.0 / sqrt(9.0 * d);
         double r = d;
-#if SBZ_GAMMA1  // A/B builds: one candidate per round (the round-1 form)
         for (int it = 0; it < 64; it++) {
             const double x = normal();
             double v = 1.0 + c * x;
@@ -315,32 +311,6 @@ struct LaneRng {
                 r = d * v;
                 break;
             }
-        }
-        return r * boost;
-#endif
-        for (int it = 0; it < 32; it++) {
-            const double u1 = 1.0 - u();
-            const double u2 = u();
-            const double rad = sqrt(-2.0 * log(u1));
-            double sn, cs;
-            sincospi(2.0 * u2, &sn, &cs);
-            const double w1 = u();
-            const double w2 = u();
-            bool done = false;
-#pragma unroll
-            for (int k = 0; k < 2; k++) {
-                const double x = rad * (k ? sn : cs);
-                double v = 1.0 + c * x;
-                if (!done && v > 0.0) {
-                    v = v * v * v;
-                    const double w = k ? w2 : w1;
-                    if (w < 1.0 - 0.0331 * (x * x) * (x * x) || log(w) < 0.5 * x * x + d * (1.0 - v + log(v))) {
-                        r = d * v;
-                        done = true;
-                    }
-                }
-            }
-            if (done) break;
         }
         return r * boost;
     }
