@@ -60,6 +60,8 @@ def parse():
                    help="real-data sampler legs (the reference's Balkan / South America configs, "
                         "SAMPLE_SOURCE = true): timed MH steps (0 = skip)")
     p.add_argument("--src-burnin", type=int, default=2000, help="real-data legs: untimed MH steps")
+    p.add_argument("--other-steps", type=int, default=100,
+                   help="launches timed per other-config likelihood leg (0: skip)")
     p.add_argument("--src-chains", type=int, default=128,
                    help="real-data legs: chains per GPU (South America; Balkan runs twice as many)")
     return p.parse_args()
@@ -583,6 +585,77 @@ def source_lik_leg(args, eng, gen, dev, stream, rank, world):
             "kernels": eng.last_kernels()}
 
 
+OTHER_CONFIGS = [
+    # name, sites, features, states, zones, families, zone size, chains per GPU (BASELINE configs)
+    ("cfg2_200x100x5_Z2", 200, 100, 5, 2, 0, 25, 64),
+    ("cfg3_shape_28x47x3_Z3_Fam5", 28, 47, 3, 3, 5, 5, 256),
+    ("cfg4_shape_100x36x5_Z6_Fam6", 100, 36, 5, 6, 6, 8, 128),
+    ("cfg5_Fam0_2000x500x10_Z8", 2000, 500, 10, 8, 0, 50, 256),
+]
+
+
+def other_configs_leg(args, dev, stream, rank, world, local_rank):
+    """Full-evaluation likelihood launches at the other BASELINE.json config shapes (synthetic data
+    of those shapes; cfg5 also without families, C = 2, as SURVEY.md §8d asks).  The small shapes
+    are a few microseconds of work per launch, so they measure launch latency, not HBM: those
+    configs are carried by the sampler kernels, which update the log-likelihood incrementally
+    inside one persistent launch (see sampler / sampler_real_data)."""
+    import copy
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from contact_zones_amd.likelihood import LikelihoodEngine
+    K = args.other_steps
+    res = {}
+    for name, N, F, S, Z, Fam, zs, B in OTHER_CONFIGS:
+        a = copy.copy(args)
+        a.sites, a.features, a.states, a.zones, a.families, a.zone_size = N, F, S, Z, Fam, zs
+        a.mode = "mixture"
+        rng = np.random.default_rng(args.seed + 17)
+        obs, fam = make_shared(a, rng)
+        a._fam = fam
+        eng = LikelihoodEngine(obs, fam, S, Z, Fam, Fam > 0, device=local_rank)
+        eng.set_stream(stream.cuda_stream)
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(args.seed * 7919 + rank)
+        pool = [make_chains_torch(a, B, gen, dev) for _ in range(2)]
+        out = torch.empty(2, B, dtype=torch.float64, device=dev)
+
+        def step(i):
+            c = pool[i % 2]
+            eng.loglik_device(B, c["zos"].data_ptr(), c["w"].data_ptr(), c["pg"].data_ptr(),
+                              c["pz"].data_ptr(), c["pf"].data_ptr() if c["pf"] is not None else 0,
+                              0, out[i % 2].data_ptr(), validate=False)
+        for i in range(5):
+            step(i)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record(stream)
+        for i in range(K):
+            step(i)
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        if not torch.isfinite(out).all():
+            raise SystemExit(f"non-finite log-likelihood in the {name} leg")
+        t = torch.tensor([ev0.elapsed_time(ev1) / 1e3], dtype=torch.float64, device=dev)
+        if world > 1:
+            _all_reduce(t, dist.ReduceOp.MAX)
+        secs = float(t[0])
+        P, D, per_launch = algorithmic_bytes(a, B)
+        launch_s = secs / K
+        res[name] = {"chains_per_gpu": B, "evals_per_sec": B * K * world / secs,
+                     "launch_us": launch_s * 1e6, "bytes_per_eval": P + D / B,
+                     "frac": per_launch / launch_s / 1e9 / HBM_PEAK_GBS, "kernels": eng.last_kernels()}
+        eng.close()
+        del pool
+    res["note"] = ("full-evaluation launches at these shapes are launch-latency bound (a few us of "
+                   "work each); the configs themselves run on the sampler kernels (incremental ll)")
+    return res
+
+
 def _free_port():
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
@@ -706,6 +779,9 @@ def main():
     sampler = None
     if args.mh_steps > 0 and args.mode == "mixture" and args.families > 0:
         sampler = sampler_leg(args, eng, obs, fam, dev, rank, world, stream)
+    other = None
+    if args.other_steps > 0 and not src_mode:
+        other = other_configs_leg(args, dev, stream, rank, world, local_rank)
     real = None
     if args.src_steps > 0:
         # configs[2] (Balkan, 3 zones, 256 chains) and configs[3] (South America, K = 1..6 zone
@@ -757,6 +833,8 @@ def main():
         }
         if src_leg is not None:
             line["likelihood_source_branch"] = src_leg
+        if other is not None:
+            line["likelihood_other_configs"] = other
         if sampler is not None:
             line["sampler"] = sampler
         if real is not None:
