@@ -180,3 +180,33 @@ def test_source_sampler_large_sources_in_hbm(gpu_available):
     fresh = st.refresh_ll().cpu().numpy()
     assert np.all(np.isfinite(fresh))
     assert np.max(np.abs(s["ll"] - fresh) / np.abs(fresh)) <= REL_TOL
+
+
+def test_source_sampler_lds_limit_fails_loudly(gpu_available):
+    """A shape whose per-chain Gibbs scratch (F x S doubles of redraws, beside the counts) exceeds
+    the 160 KiB of LDS even with the sources in HBM: the launch is refused with an error that names
+    the LDS budget (include/sbz.h), nothing runs and no chain state changes."""
+    from scipy.spatial import Delaunay
+
+    from contact_zones_amd.likelihood import LikelihoodEngine
+    from contact_zones_amd.sampler import ChainState, Sampler
+    fx = load_golden("mh_src_small")
+    rng = np.random.default_rng(9)
+    N, F, S, Z, Fam, B = 40, 2100, 10, 1, 1, 2
+    obs = rng.integers(0, S, size=(N, F)).astype(np.int8)
+    fam = np.zeros(N, np.uint8)
+    indptr, indices = Delaunay(rng.random((N, 2))).vertex_neighbor_vertices
+    eng = LikelihoodEngine(obs, fam, S, Z, Fam, True)
+    smp = Sampler(eng, np.ones((F, S), bool), indptr, indices, fx["op_probs"], fx["precision"], 3,
+                  sample_source=True)
+    zos = np.full((B, N), 255, np.uint8)
+    zos[:, :5] = 0
+    st = ChainState(eng, zos, rng.dirichlet(np.ones(3), size=(B, F)), rng.dirichlet(np.ones(S), size=(B, F)),
+                    rng.dirichlet(np.ones(S), size=(B, Z, F)), rng.dirichlet(np.ones(S), size=(B, Fam, F)),
+                    source=np.zeros((B, N, F), np.uint8))
+    before = st.to_numpy()
+    with pytest.raises(Exception, match="LDS"):
+        smp.run(st, 10, np.full(B, 20), np.full(B, 0.85), seed=5)
+    after = st.to_numpy()
+    np.testing.assert_array_equal(after["zone_of_site"], before["zone_of_site"])
+    np.testing.assert_array_equal(after["p_global"], before["p_global"])
