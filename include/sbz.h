@@ -235,7 +235,11 @@ int sbz_set_geo_prior(sbz_ctx *ctx, const double *cost, double scale);
  * [Fam][F][S]; NULL = 1 everywhere (the 'uniform' priors' counts). */
 int sbz_set_gibbs_counts(sbz_ctx *ctx, const double *counts_global, const double *counts_fam);
 
-/* Run n_steps MH steps on B device-resident chains; asynchronous on ctx's stream. */
+/* Run n_steps MH steps on B device-resident chains; asynchronous on ctx's stream.
+ * With sample_source the chain's Gibbs scratch (F x max(S, 2) doubles of redraws, 8F bytes of
+ * scans, the count tables) lives in the 160 KiB of LDS, the sources too when N*F fits (else HBM):
+ * a shape beyond that (e.g. F*S above ~18k) is refused with SBZ_EINVAL and a message naming the
+ * LDS budget before anything runs. */
 int sbz_mh_run_device(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg,
                       const sbz_chains *chains);
 
