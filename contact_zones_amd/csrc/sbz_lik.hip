@@ -91,8 +91,8 @@ __device__ __forceinline__ void wave_lds_sync() {
 // handed-off bytes is a global sc1 load (relaxed agent-scope atomic load, L1 bypassed), (2) the
 // producer stores every byte sc1 (relaxed agent-scope atomic store), (3) the storing lane (the
 // only lane that stores) runs s_waitcnt vmcnt(0) before its agent-scope atomic add to the
-// chain's one unsharded counter, (4) the consumer is the task whose add returned W-1, and it loads
-// only after that add has returned; buffers come from hipMalloc, one single-wave task per
+// chain's one unsharded counter, (4) the consumer is the task whose add returned W-1, and its lanes
+// load (one partial each, in parallel) only after that add has returned; buffers come from hipMalloc, one single-wave task per
 // workgroup.  The release/acquire form (a release on every ticket add, an acquire on the winner)
 // writes back the XCD's L2 once per task: ~1.7 us per fence, measured ~2x the kernel here.
 // tests/test_gpu_likelihood.py::test_partials_handoff_stress re-checks the hand-off under uneven
@@ -103,22 +103,34 @@ __device__ __forceinline__ void wave_lds_sync() {
 // flag travels beside the partials (zflag[b], same sc1 hand-off) and overrides the sum.
 __device__ __forceinline__ void finish_chain(const LikArgs &a, int b, double tot,
                                              bool leader = threadIdx.x == 0, bool zw = false) {
-    if (!leader) return;
+    // every lane of the wave calls this (wave-uniform control flow); lane 0 is the leader
     if (a.W == 1) {
-        a.out[b] = zw ? -INFINITY : tot;
+        if (leader) a.out[b] = zw ? -INFINITY : tot;
         return;
     }
     double *pb = a.partial + (size_t)b * a.W;
-    __hip_atomic_store(&pb[blockIdx.x], tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (zw) __hip_atomic_store(&a.zflag[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned prev =
-        __hip_atomic_fetch_add(&a.ticket[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned prev = 0;
+    if (leader) {
+        __hip_atomic_store(&pb[blockIdx.x], tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (zw) __hip_atomic_store(&a.zflag[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        prev = __hip_atomic_fetch_add(&a.ticket[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    prev = __shfl(prev, 0, WAVE);
     if (prev != (unsigned)a.W - 1) return;
     asm volatile("" ::: "memory");
+    // the W partials loaded by the wave's lanes at once (one round trip, not W), then added in
+    // task order as before: s = ((0 + p0) + p1) + ..., bit-identical for any W
+    const int lane = threadIdx.x % WAVE;
     double s = 0.0;
-    for (int t = 0; t < a.W; t++)
-        s += __hip_atomic_load(&pb[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int t0 = 0; t0 < a.W; t0 += WAVE) {
+        const double v = t0 + lane < a.W
+                             ? __hip_atomic_load(&pb[t0 + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                             : 0.0;
+        const int n = min(WAVE, a.W - t0);
+        for (int i = 0; i < n; i++) s += __shfl(v, i, WAVE);
+    }
+    if (!leader) return;
     if (a.zflag != nullptr && __hip_atomic_load(&a.zflag[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
         s = -INFINITY;
         __hip_atomic_store(&a.zflag[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
