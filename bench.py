@@ -5,7 +5,8 @@ Workload (BASELINE.json configs[4], the roofline run, per GPU): synthetic 2000 s
 500 features x 10 states, 8 zones, 4 families (inheritance, C = 3), 256 chains per GPU
 (2048 over 8 GPUs), mixture likelihood = Likelihood.__call__(sample, caching=False)
 (sbayes/model.py:145-171) per chain.  One step = one batched evaluation of all 256
-resident chains (one likelihood launch + its 256-thread reduce launch).  Chains are
+resident chains: one lik_mixture_kernel launch (the chain's last task adds the task
+partials in-kernel; there is no second launch).  Chains are
 sharded by rank (weak scaling, no collective in the timed loop); the timed region is
 bracketed by a barrier + device synchronize, and the max over ranks is reported.
 
@@ -64,7 +65,15 @@ def parse():
                    help="launches timed per other-config likelihood leg (0: skip)")
     p.add_argument("--src-chains", type=int, default=128,
                    help="real-data legs: chains per GPU (South America; Balkan runs twice as many)")
-    return p.parse_args()
+    p.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
+                   help="context option (include/sbz.h sbz_option, e.g. lik_tasks_per_cu=4) for every "
+                        "engine of the run; A/B runs only, the defaults are the production choices")
+    a = p.parse_args()
+    OPTIONS.update({k: int(v) for k, v in (o.split("=", 1) for o in a.option)})
+    return a
+
+
+OPTIONS = {}  # --option NAME=VALUE
 
 
 def make_shared(args, rng):
@@ -79,8 +88,10 @@ def make_shared(args, rng):
     return obs, fam
 
 
-def make_chains_torch(args, n_chains, gen, dev):
-    """Chain states on the device: disjoint zones of --zone-size sites, Dirichlet(1) parameters."""
+def make_chains_torch(args, n_chains, gen, dev, eng=None):
+    """Chain states on the device: disjoint zones of --zone-size sites, Dirichlet(1) parameters;
+    in source mode the sources by position ([B][F][Np], `src_pm`, the layout the sampler keeps and
+    the likelihood reads in place), generated by site and transposed once by the engine."""
     import torch
     N, F, S, Z, Fam = args.sites, args.features, args.states, args.zones, args.families
     C = 3 if Fam > 0 else 2
@@ -109,8 +120,15 @@ def make_chains_torch(args, n_chains, gen, dev):
         fam_t = torch.as_tensor(args._fam, device=dev)
         if C == 3:
             src[(fam_t[None, :, None] != 255) & (r < 0.25)] = 2
+        del r
+    src_pm = None
+    if src is not None:
+        src_pm = torch.zeros(n_chains, F, eng.n_positions, dtype=torch.uint8, device=dev)
+        eng.source_layout_device(n_chains, src.data_ptr(), src_pm.data_ptr(), True)
+        torch.cuda.synchronize()
+        del src
     return dict(zos=zos.contiguous(), w=w.contiguous(), pg=pg.contiguous(), pz=pz.contiguous(),
-                pf=pf.contiguous() if pf is not None else None, src=src)
+                pf=pf.contiguous() if pf is not None else None, src_pm=src_pm)
 
 
 def algorithmic_bytes(args, B, source=False):
@@ -141,6 +159,34 @@ def pmc_traffic(args, B):
         if d.get("_meta", {}).get("workload_key") == workload_key(args, B) and "_hbm" in d:
             return d["_hbm"]["traffic_bytes"], os.path.relpath(fn, here)
     return None, None
+
+
+def pmc_secondary(args, B):
+    """The binding on-chip resources of the dominant kernel, from the same committed PMC summary
+    as `traffic` (its average counters per launch): the LDS array's busy share of the CU cycles
+    (SQ_LDS_IDX_ACTIVE counts LDS-array cycles, MI355X_MICROARCH.md) and the VALU issue share of
+    the SIMD cycles (SQ_ACTIVE_INST_VALU counts quad-cycles).  The kernel's elapsed cycles per XCD
+    are GRBM_GUI_ACTIVE / 8 (rocprofv3 sums the 8 XCDs); 256 CUs, 1024 SIMDs."""
+    import glob
+    here = os.path.dirname(os.path.abspath(__file__))
+    for fn in sorted(glob.glob(os.path.join(here, "profiles", "r*_pmc.json")), reverse=True):
+        try:
+            d = json.load(open(fn))
+        except (OSError, ValueError):
+            continue
+        if d.get("_meta", {}).get("workload_key") != workload_key(args, B) or "_hbm" not in d:
+            continue
+        s = d.get(d["_hbm"]["kernel"], {})
+        cyc = s.get("GRBM_GUI_ACTIVE", 0.0) / 8.0
+        if not cyc or "SQ_LDS_IDX_ACTIVE" not in s or "SQ_ACTIVE_INST_VALU" not in s:
+            return None
+        return {"lds_array_busy": s["SQ_LDS_IDX_ACTIVE"] / (256 * cyc),
+                "lds_bank_conflict_share": s.get("SQ_LDS_BANK_CONFLICT", 0.0) / s["SQ_LDS_IDX_ACTIVE"],
+                "valu_issue": 4.0 * s["SQ_ACTIVE_INST_VALU"] / (1024 * cyc),
+                "source": os.path.relpath(fn, here),
+                "formula": "lds_array_busy = SQ_LDS_IDX_ACTIVE / (256 CUs x GRBM_GUI_ACTIVE/8); "
+                           "valu_issue = 4 x SQ_ACTIVE_INST_VALU / (1024 SIMDs x GRBM_GUI_ACTIVE/8)"}
+    return None
 
 
 def _cpu_worker(shape, seconds, seed, q):
@@ -176,6 +222,15 @@ def _cpu_worker(shape, seconds, seed, q):
     q.put((n, el))
 
 
+def _cgroup_cpus():
+    """CPUs of this process's cgroup v2 quota (cpu.max 'quota period'), or None without one."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(args, seconds):
     """SURVEY.md §8d CPU timing: one process per host core (spawned, single-threaded BLAS/OpenMP),
     each evaluating one chain of the bench workload for `seconds`; per-core and all-core evals/s
@@ -187,7 +242,12 @@ def cpu_baseline(args, seconds):
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = os.cpu_count() or 1
-    procs = args.cpu_procs if args.cpu_procs > 0 else max(1, min(16, avail))
+    quota = _cgroup_cpus()
+    # one process per core this process may use: the affinity mask, bounded by the cgroup's CPU
+    # quota (more processes than the quota only time-slice) and by the GPU box's CPU share of 16
+    # (the pool's rule for one-GPU jobs: the host's other cores serve the other GPUs' jobs)
+    usable = min(avail, int(quota)) if quota else avail
+    procs = args.cpu_procs if args.cpu_procs > 0 else max(1, min(16, usable))
     shape = {k: getattr(args, k) for k in ("sites", "features", "states", "zones", "families", "zone_size")}
     keep = {k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS")}
     for k in keep:
@@ -224,7 +284,11 @@ def cpu_baseline(args, seconds):
     return {"value": float(sum(rates)), "unit": "likelihood-evals/s", "cores": procs, "kind": "port",
             **extra,
             "per_core": float(sum(rates) / procs), "per_core_min": float(min(rates)),
-            "host_cpu_count": os.cpu_count(), "cores_available": avail,
+            "host_cpu_count": os.cpu_count(), "cores_available": avail, "cgroup_cpu_quota": quota,
+            "per_gpu_share": {"cores": procs, "value": float(sum(rates))},
+            "all_core_extrapolated": {"cores": usable, "value": float(sum(rates) / procs) * usable,
+                                      "how": "measured per-core rate x the usable cores (affinity "
+                                             "mask, cgroup quota); not run"},
             "sample": f"numpy restatement of Likelihood.__call__(caching=False) (oracle/lik_numpy.py), "
                       f"one chain at {N}x{F}x{S}, Z={Z}, Fam={Fam} per process, {procs} processes x "
                       f"{seconds:.0f} s, 1 thread each ({sum(n for n, _ in res)} evals)"}
@@ -395,7 +459,7 @@ def source_sampler_leg(shape, B, K, burnin, seed, rank=0, world=1, device=0):
         fam[:] = 255
     indptr, indices = Delaunay(rng.random((N, 2))).vertex_neighbor_vertices
     states = np.ones((F, S), bool)
-    eng = LikelihoodEngine(obs, fam, S, Z, Fam, inh, device=device)
+    eng = LikelihoodEngine(obs, fam, S, Z, Fam, inh, device=device, options=OPTIONS)
     init = InitialSamples(packing.obs_to_features(obs, S), states, indptr, indices,
                           packing.index_to_groups(fam, Fam) if inh else np.zeros((0, N), bool), Z,
                           MH_M_INITIAL, inh, None, random.Random(seed * 1000003 + rank))
@@ -480,7 +544,7 @@ def real_data_leg(name, n_zones_list, B, K, burnin, seed, rank=0, world=1, devic
     for Z in n_zones_list:
         cfg, _ = experiment.load_config(path, {"model": {"N_AREAS": int(Z)}})
         spec, gibbs = experiment.build_priors(cfg, data)
-        eng = LikelihoodEngine(t.obs, t.fam_of_site, t.n_states, Z, Fam, inh, device=device)
+        eng = LikelihoodEngine(t.obs, t.fam_of_site, t.n_states, Z, Fam, inh, device=device, options=OPTIONS)
         smp = Sampler(eng, t.applicable, indptr, indices, experiment.operators(cfg),
                       precisions(mc["PROPOSAL_PRECISION"]), int(m["MIN_M"]), priors=spec,
                       sample_source=src_mode, gibbs_counts=gibbs if src_mode else None)
@@ -544,21 +608,22 @@ def _all_reduce(t, op):
 def source_lik_leg(args, eng, gen, dev, stream, rank, world):
     """The source branch of the likelihood (model.py:177-184) on the same
     workload: every cell's component drawn among those the site has, B chains, full evaluation
-    (repack + lik_source_rc_kernel), timed with HIP events on the engine's stream."""
+    with the sources by position as the sampler keeps them (lik_source_rc_kernel reads them in
+    place; sbz_loglik_batch_device_pm), timed with HIP events on the engine's stream."""
     import copy
     import torch
     import torch.distributed as dist
     a = copy.copy(args)
     a.mode = "source"
     B, K = args.chains, args.source_lik_steps
-    pool = [make_chains_torch(a, B, gen, dev) for _ in range(2)]
+    pool = [make_chains_torch(a, B, gen, dev, eng) for _ in range(2)]
     out = torch.empty(2, B, dtype=torch.float64, device=dev)
 
     def step(i):
         c = pool[i % 2]
         eng.loglik_device(B, c["zos"].data_ptr(), c["w"].data_ptr(), c["pg"].data_ptr(),
                           c["pz"].data_ptr(), c["pf"].data_ptr() if c["pf"] is not None else 0,
-                          c["src"].data_ptr(), out[i % 2].data_ptr(), validate=False)
+                          c["src_pm"].data_ptr(), out[i % 2].data_ptr(), validate=False, source_pm=True)
     for i in range(3):
         step(i)
     torch.cuda.synchronize()
@@ -614,7 +679,7 @@ def other_configs_leg(args, dev, stream, rank, world, local_rank):
         rng = np.random.default_rng(args.seed + 17)
         obs, fam = make_shared(a, rng)
         a._fam = fam
-        eng = LikelihoodEngine(obs, fam, S, Z, Fam, Fam > 0, device=local_rank)
+        eng = LikelihoodEngine(obs, fam, S, Z, Fam, Fam > 0, device=local_rank, options=OPTIONS)
         eng.set_stream(stream.cuda_stream)
         gen = torch.Generator(device=dev)
         gen.manual_seed(args.seed * 7919 + rank)
@@ -719,14 +784,14 @@ def main():
     obs, fam = make_shared(args, rng)  # replicated on every rank (1 MB)
     args._fam = fam
     eng = LikelihoodEngine(obs, fam, args.states, args.zones, args.families, args.families > 0,
-                           device=local_rank)
+                           device=local_rank, options=OPTIONS)
     stream = torch.cuda.current_stream()
     eng.set_stream(stream.cuda_stream)
 
     B = args.chains
     gen = torch.Generator(device=dev)
     gen.manual_seed(args.seed * 1000003 + rank)  # chains differ per rank (global chain ids)
-    pool = [make_chains_torch(args, B, gen, dev) for _ in range(args.pool)]
+    pool = [make_chains_torch(args, B, gen, dev, eng) for _ in range(args.pool)]
     out = torch.empty(args.pool, B, dtype=torch.float64, device=dev)
     src_mode = args.mode == "source"
 
@@ -734,8 +799,8 @@ def main():
         c = pool[i % args.pool]
         eng.loglik_device(B, c["zos"].data_ptr(), c["w"].data_ptr(), c["pg"].data_ptr(),
                           c["pz"].data_ptr(), c["pf"].data_ptr() if c["pf"] is not None else 0,
-                          c["src"].data_ptr() if src_mode else 0, out[i % args.pool].data_ptr(),
-                          validate=False)  # generated in range by make_chains_torch
+                          c["src_pm"].data_ptr() if src_mode else 0, out[i % args.pool].data_ptr(),
+                          validate=False, source_pm=True)  # generated in range by make_chains_torch
 
     for i in range(args.warmup):
         step(i)
@@ -767,10 +832,14 @@ def main():
     total_evals = B * args.steps * world
     value = total_evals / wall_max
     P, D, per_launch = algorithmic_bytes(args, B, src_mode)
-    launch_s = ev_ms / 1e3 / args.steps  # this rank's device time per step (lik + reduce launch)
-    achieved = per_launch / launch_s / 1e9
+    # roofline from the timed wall clock per step (max over ranks, = ms_per_step); the HIP-event
+    # device time of the same launches is reported beside it under its own name
+    step_s = wall_max / args.steps
+    launch_s = ev_ms / 1e3 / args.steps  # this rank's device time per launch (HIP events)
+    achieved = per_launch / step_s / 1e9
 
     traffic, traffic_src = pmc_traffic(args, B)
+    secondary = pmc_secondary(args, B)
     src_leg = None
     if args.source_lik_steps > 0 and not src_mode:
         del pool
@@ -823,11 +892,15 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
+                "timing": "achieved = bytes_per_launch / ms_per_step (timed wall clock, max over ranks)",
                 "traffic": traffic,
                 "traffic_source": traffic_src,
                 "bytes_per_eval": P + D / B,
                 "bytes_per_launch": per_launch,
-                "launch_us": launch_s * 1e6,
+                "step_us": step_s * 1e6,
+                "launch_us_event": launch_s * 1e6,
+                "frac_event": per_launch / launch_s / 1e9 / HBM_PEAK_GBS,
+                **({"secondary": secondary} if secondary else {}),
             },
             "device_time_s": ev_max,
         }

@@ -12,6 +12,11 @@ LIB_PATH = os.environ.get("SBZ_LIB_PATH") or os.path.join(_HERE, "libsbz.so")
 
 SBZ_OK = 0
 SBZ_INHERITANCE = 1
+SBZ_SOURCE_BY_SITE = 0
+SBZ_SOURCE_BY_POSITION = 1
+# sbz_option (include/sbz.h): name -> id
+OPTIONS = {"lik_tasks_per_cu": 1, "lik_banked": 2, "src_table": 3, "src_waves": 4, "src_hbm": 5,
+           "src_stage": 6, "mh_lookahead": 7}
 ERRORS = {-1: "SBZ_EINVAL", -2: "SBZ_EHIP", -3: "SBZ_ENOMEM", -4: "SBZ_ESTATE"}
 
 
@@ -51,7 +56,8 @@ class sbz_chains(ctypes.Structure):
                 ("trace_ll", ctypes.c_void_p), ("trace_zos", ctypes.c_void_p),
                 ("prior", ctypes.c_void_p), ("source", ctypes.c_void_p),
                 ("alias_pending", ctypes.c_void_p), ("alias_p_global", ctypes.c_void_p),
-                ("alias_p_zones", ctypes.c_void_p), ("alias_p_fam", ctypes.c_void_p)]
+                ("alias_p_zones", ctypes.c_void_p), ("alias_p_fam", ctypes.c_void_p),
+                ("source_layout", ctypes.c_int32)]
 
 
 class sbz_state(ctypes.Structure):
@@ -85,6 +91,12 @@ SIGNATURES = {
     "sbz_last_error": (ctypes.c_char_p, [_P]),
     "sbz_set_stream": (_I, [_P, _P]),
     "sbz_synchronize": (_I, [_P]),
+    "sbz_set_option": (_I, [_P, ctypes.c_int32, ctypes.c_int64]),
+    "sbz_get_option": (_I, [_P, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)]),
+    "sbz_site_positions": (_I, [_P, _P]),
+    "sbz_loglik_batch_device_pm": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "sbz_source_layout_device": (_I, [_P, _I, _P, _P, ctypes.c_int32]),
+    "sbz_check_indices_device_pm": (_I, [_P, _I, _P, _P]),
     "sbz_loglik_batch": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P]),
     "sbz_loglik_batch_device": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P]),
     "sbz_check_indices_device": (_I, [_P, _I, _P, _P]),

@@ -152,13 +152,8 @@ int sbz_open(int device, const sbz_dims *dims, const int8_t *obs, const uint8_t 
             obs_fm[(size_t)f * Np + p] = (uint8_t)((x < 0 ? S : x) * scale);
         }
     }
-    if (const char *v = getenv("SBZ_LIK_BANKED")) ctx->lik_banked = atoi(v) != 0;
-    if (const char *v = getenv("SBZ_SRC_RC")) ctx->src_rc = atoi(v) != 0;
-    if (const char *v = getenv("SBZ_SRC_STAGE")) ctx->src_stage = atoi(v) != 0;
-    if (const char *v = getenv("SBZ_SRC_HBM")) ctx->src_hbm = atoi(v) != 0;
-    if (const char *v = getenv("SBZ_SRC_WAVES")) ctx->src_waves = atoi(v);
-    if (const char *v = getenv("SBZ_LIK_TASKS")) ctx->tasks_per_cu = std::max(1, atoi(v));
-    if (const char *v = getenv("SBZ_MH_LA")) ctx->mh_la = std::min(24, std::max(1, atoi(v)));
+    ctx->h_perm.assign(perm.begin(), perm.end());
+    for (int p = N; p < Np; p++) ctx->h_perm[p] = -1;
     // site-major observations and family classes for the sampler's per-site deltas
     {
         std::vector<uint8_t> obs_sm((size_t)N * F);
@@ -245,13 +240,83 @@ int sbz_loglik_batch_device(sbz_ctx *ctx, int B, const uint8_t *zone_of_site, co
         (ctx->d.n_zones > 0 && !p_zones))
         return fail(ctx, SBZ_EINVAL, "null argument or negative B");
     (void)hipSetDevice(ctx->device);
-    return launch_loglik(ctx, B, zone_of_site, w, p_global, p_zones, p_fam, source, out_ll);
+    return launch_loglik(ctx, B, zone_of_site, w, p_global, p_zones, p_fam, source, false, out_ll);
+}
+
+int sbz_loglik_batch_device_pm(sbz_ctx *ctx, int B, const uint8_t *zone_of_site, const double *w,
+                               const double *p_global, const double *p_zones, const double *p_fam,
+                               const uint8_t *source_pm, double *out_ll) {
+    if (!ctx) return SBZ_EINVAL;
+    if (B < 0 || !zone_of_site || !w || !p_global || !out_ll || !source_pm ||
+        (ctx->d.n_zones > 0 && !p_zones))
+        return fail(ctx, SBZ_EINVAL, "null argument or negative B");
+    (void)hipSetDevice(ctx->device);
+    return launch_loglik(ctx, B, zone_of_site, w, p_global, p_zones, p_fam, source_pm, true, out_ll);
+}
+
+int sbz_source_layout_device(sbz_ctx *ctx, int B, const uint8_t *src, uint8_t *dst, int32_t to_positions) {
+    if (!ctx) return SBZ_EINVAL;
+    if (B < 0 || (B > 0 && (!src || !dst)) || src == dst)
+        return fail(ctx, SBZ_EINVAL, "sbz_source_layout_device: bad arguments (src and dst must differ)");
+    (void)hipSetDevice(ctx->device);
+    return launch_source_transpose(ctx, B, src, dst, to_positions != 0);
+}
+
+int sbz_site_positions(const sbz_ctx *ctx, int32_t *positions) {
+    if (!ctx) return SBZ_EINVAL;
+    if (positions)
+        for (int p = 0; p < ctx->Np; p++) positions[p] = ctx->h_perm[p];
+    return ctx->Np;
+}
+
+int sbz_set_option(sbz_ctx *ctx, int32_t option, int64_t value) {
+    if (!ctx) return SBZ_EINVAL;
+    auto flag = [&](int &dst) -> int {
+        if (value != 0 && value != 1) return fail(ctx, SBZ_EINVAL, "option value must be 0 or 1");
+        dst = (int)value;
+        return SBZ_OK;
+    };
+    switch (option) {
+        case SBZ_OPT_LIK_TASKS_PER_CU:
+            if (value < 0 || value > 64) return fail(ctx, SBZ_EINVAL, "tasks per CU must be in 0..64");
+            ctx->tasks_per_cu = (int)value;
+            return SBZ_OK;
+        case SBZ_OPT_LIK_BANKED: return flag(ctx->lik_banked);
+        case SBZ_OPT_SRC_TABLE: return flag(ctx->src_rc);
+        case SBZ_OPT_SRC_HBM: return flag(ctx->src_hbm);
+        case SBZ_OPT_SRC_STAGE: return flag(ctx->src_stage);
+        case SBZ_OPT_SRC_WAVES:
+            if (value != 0 && value != 1 && value != 4 && value != 8)
+                return fail(ctx, SBZ_EINVAL, "source-mode sampler waves must be 0, 1, 4 or 8");
+            ctx->src_waves = (int)value;
+            return SBZ_OK;
+        case SBZ_OPT_MH_LOOKAHEAD:
+            if (value < 1 || value > 24) return fail(ctx, SBZ_EINVAL, "sampler lookahead must be in 1..24");
+            ctx->mh_la = (int)value;
+            return SBZ_OK;
+        default: return fail(ctx, SBZ_EINVAL, "unknown option " + std::to_string(option));
+    }
+}
+
+int sbz_get_option(const sbz_ctx *ctx, int32_t option, int64_t *value) {
+    if (!ctx || !value) return SBZ_EINVAL;
+    switch (option) {
+        case SBZ_OPT_LIK_TASKS_PER_CU: *value = ctx->tasks_per_cu; return SBZ_OK;
+        case SBZ_OPT_LIK_BANKED: *value = ctx->lik_banked; return SBZ_OK;
+        case SBZ_OPT_SRC_TABLE: *value = ctx->src_rc; return SBZ_OK;
+        case SBZ_OPT_SRC_HBM: *value = ctx->src_hbm; return SBZ_OK;
+        case SBZ_OPT_SRC_STAGE: *value = ctx->src_stage; return SBZ_OK;
+        case SBZ_OPT_SRC_WAVES: *value = ctx->src_waves; return SBZ_OK;
+        case SBZ_OPT_MH_LOOKAHEAD: *value = ctx->mh_la; return SBZ_OK;
+        default: return SBZ_EINVAL;
+    }
 }
 
 namespace {
 // bit 0: a zone byte >= n_zones (and != SBZ_NONE); bit 1: a source byte >= C
+// (sources by position: rows of Np bytes whose columns >= N are padding, not checked)
 __global__ void check_indices_kernel(size_t nz, const uint8_t *zone, int Z, size_t ns,
-                                     const uint8_t *src, int C, unsigned *flags) {
+                                     const uint8_t *src, int C, int N, int row, unsigned *flags) {
     unsigned bad = 0;
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nz; i += stride) {
@@ -259,7 +324,7 @@ __global__ void check_indices_kernel(size_t nz, const uint8_t *zone, int Z, size
         bad |= (z != SBZ_NONE && z >= (unsigned)Z) ? 1u : 0u;
     }
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += stride)
-        bad |= src[i] >= (unsigned)C ? 2u : 0u;
+        bad |= (src[i] >= (unsigned)C && (int)(i % (size_t)row) < N) ? 2u : 0u;
     if (__any(bad != 0)) {
         const unsigned m = bad;
         atomicOr(flags, m);
@@ -267,8 +332,8 @@ __global__ void check_indices_kernel(size_t nz, const uint8_t *zone, int Z, size
 }
 }  // namespace
 
-int sbz_check_indices_device(sbz_ctx *ctx, int B, const uint8_t *zone_of_site,
-                             const uint8_t *source) {
+static int check_indices(sbz_ctx *ctx, int B, const uint8_t *zone_of_site, const uint8_t *source,
+                         bool pm) {
     if (!ctx) return SBZ_EINVAL;
     if (B < 0 || (B > 0 && !zone_of_site)) return fail(ctx, SBZ_EINVAL, "null argument or negative B");
     if (B == 0) return SBZ_OK;
@@ -279,11 +344,13 @@ int sbz_check_indices_device(sbz_ctx *ctx, int B, const uint8_t *zone_of_site,
     hipError_t e = hipMemsetAsync(flags, 0, sizeof(unsigned), ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "hipMemsetAsync(flags)");
     const size_t nz = (size_t)B * ctx->d.n_sites;
-    const size_t ns = source ? nz * (size_t)ctx->d.n_features : 0;
+    const size_t ns = source ? (size_t)B * ctx->d.n_features * (pm ? ctx->Np : ctx->d.n_sites) : 0;
     const size_t work = std::max(nz, ns);
     const int grid = (int)std::min<size_t>(2048, (work + 255) / 256);
+    // site-major rows hold F components, all checked (row = N = F would do; use N >= any column)
+    const int N = pm ? ctx->d.n_sites : ctx->d.n_features, row = pm ? ctx->Np : ctx->d.n_features;
     check_indices_kernel<<<grid, 256, 0, ctx->stream>>>(nz, zone_of_site, ctx->d.n_zones, ns, source,
-                                                        ctx->C, flags);
+                                                        ctx->C, N, row, flags);
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(ctx, e, "check_indices_kernel launch");
     unsigned h = 0;
@@ -293,6 +360,14 @@ int sbz_check_indices_device(sbz_ctx *ctx, int B, const uint8_t *zone_of_site,
     if (h & 1u) return fail(ctx, SBZ_EINVAL, "zone_of_site holds an index >= n_zones");
     if (h & 2u) return fail(ctx, SBZ_EINVAL, "source holds a component index >= C");
     return SBZ_OK;
+}
+
+int sbz_check_indices_device(sbz_ctx *ctx, int B, const uint8_t *zone_of_site, const uint8_t *source) {
+    return check_indices(ctx, B, zone_of_site, source, false);
+}
+
+int sbz_check_indices_device_pm(sbz_ctx *ctx, int B, const uint8_t *zone_of_site, const uint8_t *source_pm) {
+    return check_indices(ctx, B, zone_of_site, source_pm, true);
 }
 
 int sbz_loglik_batch(sbz_ctx *ctx, int B, const uint8_t *zone_of_site, const double *w,
@@ -339,7 +414,7 @@ int sbz_loglik_batch(sbz_ctx *ctx, int B, const uint8_t *zone_of_site, const dou
                        reinterpret_cast<double *>(base + o_w), reinterpret_cast<double *>(base + o_g),
                        reinterpret_cast<double *>(base + o_z),
                        inh ? reinterpret_cast<double *>(base + o_f) : nullptr,
-                       source ? reinterpret_cast<uint8_t *>(base + o_src) : nullptr,
+                       source ? reinterpret_cast<uint8_t *>(base + o_src) : nullptr, false,
                        static_cast<double *>(ctx->out.ptr));
     if (rc) return rc;
     e = hipMemcpyAsync(out_ll, ctx->out.ptr, (size_t)B * 8, hipMemcpyDeviceToHost, st);
@@ -480,6 +555,12 @@ int sbz_mh_run(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg, uint6
         return fail(ctx, SBZ_EINVAL, "sbz_state: a required array is NULL");
     if (tape && (!tape->values || !tape->len || tape->stride <= 0))
         return fail(ctx, SBZ_EINVAL, "sbz_tape: values, len and stride > 0 are required");
+    if (tape)
+        for (int b = 0; b < B; b++) {
+            const int64_t len = tape->len[b], pos = tape->pos ? tape->pos[b] : 0;
+            if (len < 0 || len > tape->stride || pos < 0 || pos > len)
+                return fail(ctx, SBZ_EINVAL, "sbz_tape: need 0 <= pos[b] <= len[b] <= stride");
+        }
     for (size_t i = 0; i < (size_t)B * N; i++)
         if (st->zone_of_site[i] != SBZ_NONE && st->zone_of_site[i] >= Z)
             return fail(ctx, SBZ_EINVAL, "zone_of_site holds an index >= n_zones");
@@ -529,14 +610,20 @@ int sbz_mh_run(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg, uint6
     for (const Part &p : parts)
         if (e == hipSuccess && p.in && p.host && p.bytes)
             e = hipMemcpyAsync(base + p.off, p.host, p.bytes, hipMemcpyHostToDevice, s);
-    if (e != hipSuccess) return hip_fail(ctx, e, "sbz_mh_run: H2D");
+    // from here on the H2D copies from the caller's (pageable) arrays may be in flight: an error
+    // return first waits for them, so the caller may free its arrays
+    auto bail = [&](int code) {
+        (void)hipStreamSynchronize(s);
+        return code;
+    };
+    if (e != hipSuccess) return bail(hip_fail(ctx, e, "sbz_mh_run: H2D"));
     auto dp = [&](size_t i) -> void * { return parts[i].bytes ? base + parts[i].off : nullptr; };
     // the chains' log-likelihood from the staged state
     rc = launch_loglik(ctx, B, static_cast<uint8_t *>(dp(izos)), static_cast<double *>(dp(iw)),
                        static_cast<double *>(dp(ig)), static_cast<double *>(dp(iz)),
-                       static_cast<double *>(dp(ifm)), src ? static_cast<uint8_t *>(dp(isrc)) : nullptr,
+                       static_cast<double *>(dp(ifm)), src ? static_cast<uint8_t *>(dp(isrc)) : nullptr, false,
                        static_cast<double *>(dp(ill)));
-    if (rc) return rc;
+    if (rc) return bail(rc);
     sbz_chains ch{};
     ch.zone_of_site = static_cast<uint8_t *>(dp(izos));
     ch.w = static_cast<double *>(dp(iw));
@@ -566,7 +653,7 @@ int sbz_mh_run(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg, uint6
         ch.trace_ll = static_cast<double *>(dp(itll));
     }
     rc = launch_mh(ctx, B, n_steps, cfg, &ch);
-    if (rc) return rc;
+    if (rc) return bail(rc);
     for (const Part &p : parts)
         if (e == hipSuccess && p.out && p.bytes)
             e = hipMemcpyAsync(p.out, base + p.off, p.bytes, hipMemcpyDeviceToHost, s);

@@ -5,6 +5,7 @@
 
 #include <cstdint>
 #include <string>
+#include <vector>
 
 #include "../../include/sbz.h"
 
@@ -32,8 +33,8 @@ struct LikArgs {
     const double *pg;       // [B][F][S]
     const double *pz;       // [B][Z][F][S]
     const double *pf;       // [B][Fam][F][S] (C == 3 only)
-    const uint8_t *src_fm;  // [B][F][Np] row code per cell (lik_source_rc_kernel), or nullptr
-    const uint8_t *src_rm;  // [B][N][F]  the caller's sources (lik_source_generic_kernel)
+    const uint8_t *src_pm;  // [B][F][Np] component per cell by position (position-major), or nullptr
+    const uint8_t *src_rm;  // [B][N][F]  the caller's sources by site (lik_source_generic_kernel)
     double *partial;        // [B][W]     task partial sums
     unsigned *ticket;       // [B]        finished tasks per chain (0 between launches)
     unsigned *zflag;        // [B]        source branch: a task saw a zero selected weight (0
@@ -66,16 +67,18 @@ struct sbz_ctx {
     double geo_scale = 0.0;
     double *d_gc_g = nullptr;     // [F][S] Gibbs prior counts of p_global (sbz_set_gibbs_counts)
     double *d_gc_f = nullptr;     // [Fam][F][S] of p_families
-    int lik_banked = 1;    // SBZ_LIK_BANKED=0: dense kernel with the packed [class][x] table
-    int src_rc = 1;        // SBZ_SRC_RC=0: source branch on the generic per-cell kernel
-    int src_stage = 1;     // SBZ_SRC_STAGE=0: source-mode sampler passes read parameters from L2
+    std::vector<int> h_perm;  // [Np] host copy of d_perm, -1 at the padding positions
+    // options (sbz_set_option; defaults are the production choices)
+    int lik_banked = 1;    // SBZ_OPT_LIK_BANKED 0: dense kernel with the packed [class][x] table
+    int src_rc = 1;        // SBZ_OPT_SRC_TABLE 0: source branch on the generic per-cell kernel
+    int src_stage = 1;     // SBZ_OPT_SRC_STAGE 0: source-mode sampler passes read parameters from L2
     const void *mix_occ_fn = nullptr;  // the kernel mix_occ was queried for
-    int tasks_per_cu = 0;  // SBZ_LIK_TASKS: single-wave tasks per CU per launch (0: occupancy)
+    int tasks_per_cu = 0;  // SBZ_OPT_LIK_TASKS_PER_CU: single-wave tasks per CU per launch (0: by shape)
     int mix_occ = 0;       // resident mixture-kernel waves per CU (queried at first launch)
     int n_cu = 256;        // compute units of the device
-    int src_waves = 0;     // SBZ_SRC_WAVES: waves per chain of the source-mode sampler (0: by N x F)
-    int mh_la = 24;        // SBZ_MH_LA: sampler proposals planned ahead per batch (1..24; 1 = none)
-    int src_hbm = 0;       // SBZ_SRC_HBM=1: source-mode sampler keeps sources in HBM even when they fit LDS
+    int src_waves = 0;     // SBZ_OPT_SRC_WAVES: waves per chain of the source-mode sampler (0: 8)
+    int mh_la = 24;        // SBZ_OPT_MH_LOOKAHEAD: sampler proposals planned ahead per batch (1..24)
+    int src_hbm = 0;       // SBZ_OPT_SRC_HBM 1: source-mode sampler keeps sources in HBM even when they fit LDS
     std::string last_kernels;  // sbz_last_kernels
     sbz::DevBuf mh_stage;      // host-form sampler staging (sbz_mh_run)
     sbz::DevBuf partial, ticket, zflag, src_t, stage, out, src_cand, flags;
@@ -107,8 +110,11 @@ int launch_mh(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg, const 
 int launch_draw_gamma(sbz_ctx *ctx, int n, const double *alpha, uint64_t seed, double *out);
 
 // Launch the likelihood kernels for B chains (all pointers device); out_ll device [B].
+// source_pm: `source` is [B][F][Np] by position (else [B][N][F] by site).
 int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, const double *pg,
-                  const double *pz, const double *pf, const uint8_t *source_rowmajor,
+                  const double *pz, const double *pf, const uint8_t *source, bool source_pm,
                   double *out_ll);
+// [B][N][F] by site <-> [B][F][Np] by position (to_pm), device arrays, on ctx's stream.
+int launch_source_transpose(sbz_ctx *ctx, int B, const uint8_t *src, uint8_t *dst, bool to_pm);
 
 }  // namespace sbz

@@ -51,6 +51,9 @@ constexpr int ZR = 2;        // zone classes per lane held in registers
 constexpr int MIX_WAVES = SBZ_MIX_WAVES; // launch bound of the dense kernel: waves per SIMD
 constexpr int RN = 4;        // product chains checked and renormalised once per RN features
 constexpr int GIF = 16;      // table reads in flight per wave (scheduling barrier every GIF)
+#ifndef SBZ_LIK_FMA
+#define SBZ_LIK_FMA 1  // (A/B only) 0: the table entries in the reference's unfused operation order
+#endif
 
 __device__ __forceinline__ void renorm(double &m, int &e) {
     const int ex = __builtin_amdgcn_frexp_exp(m);
@@ -375,19 +378,34 @@ struct MixTable {
             const double l1 = r.z[i] + naone;
             double *row = valid ? tab + (BK ? bk_row(zc, 0, FamC, S1) : (uint32_t)(zc * FamC * S1)) + lx : junk;
             const int rs = valid ? (BK ? 32 : S1) : 0;
+            // fused multiply-adds: each entry within an ulp of the reference's per-cell value
+            // (north_star's tolerance is 1e-9 relative on the log-likelihood)
+#if SBZ_LIK_FMA
+            double v = __builtin_fma(n01, l1, n00 * l0);
+            if (C == 3 && wide) v = __builtin_fma(i == 0 ? p[0][2] : u[0][2], naone, v);
+#else
             double v = n00 * l0 + n01 * l1;
             if (C == 3 && wide) v = v + (i == 0 ? p[0][2] : u[0][2]) * naone;
+#endif
             row[0] = v;
             if (C == 3) {
                 const double n10 = i == 0 ? p[1][0] : u[1][0], n11 = i == 0 ? p[1][1] : u[1][1];
                 const double n12 = i == 0 ? p[1][2] : u[1][2];
+#if SBZ_LIK_FMA
+                const double a1 = __builtin_fma(n11, l1, n10 * l0);
+#pragma unroll
+                for (int fm = 0; fm < FR; fm++) {
+                    double *dst = fm < Fam ? row + (fm + 1) * rs : junk;  // families past Fam: junk
+                    *dst = __builtin_fma(n12, r.fm[fm] + naone, a1);
+                }
+#else
                 const double a1 = n10 * l0 + n11 * l1;
 #pragma unroll
                 for (int fm = 0; fm < FR; fm++) {
-                    const double lf = r.fm[fm] + naone;
-                    double *dst = fm < Fam ? row + (fm + 1) * rs : junk;  // families past Fam: junk
-                    *dst = a1 + n12 * lf;
+                    double *dst = fm < Fam ? row + (fm + 1) * rs : junk;
+                    *dst = a1 + n12 * (r.fm[fm] + naone);
                 }
+#endif
             }
         }
         wave_lds_sync();
@@ -585,7 +603,7 @@ __global__ __launch_bounds__(WAVE) void lik_mixture_generic_kernel(LikArgs a) {
 // Source kernel, generic path (any S, Z, Fam within the ABI limits, and the SBZ_SRC_RC=0
 // check): one lane per site, the cell w_norm[src] * l_src computed directly from the
 // parameters in the reference's operation order (model.py:436-452, 241-247) and the caller's
-// source bytes [B][N][F] read in place (no repack), one log per cell.  A selected weight of
+// source bytes ([B][N][F] or [B][F][Np]) read in place, one log per cell.  A selected weight of
 // exactly 0 sets the chain's -inf flag (model.py:181-182).
 // ---------------------------------------------------------------------------------------
 template <int C>
@@ -602,7 +620,8 @@ __global__ __launch_bounds__(WAVE) void lik_source_generic_kernel(LikArgs a) {
     const double *pfb = (C == 3) ? a.pf + (size_t)b * Fam * zfs : nullptr;
     const double *wb = a.w + (size_t)b * a.F * C;
     const uint8_t *zb = a.zone + (size_t)b * a.N;
-    const uint8_t *sb = a.src_rm + (size_t)b * a.N * a.F;
+    // the caller's sources: [B][N][F] by site, or [B][F][Np] by position
+    const uint8_t *sb = a.src_pm ? a.src_pm + (size_t)b * a.F * a.Np : a.src_rm + (size_t)b * a.N * a.F;
     const int div = a.xs8 ? 8 : 1;
     double lsum = 0.0;
     uint32_t zw = 0;
@@ -615,7 +634,7 @@ __global__ __launch_bounds__(WAVE) void lik_source_generic_kernel(LikArgs a) {
         for (int f = fa; f < fb; f++) {
             const int x = a.obs_fm[(size_t)f * a.Np + s] / div;
             const bool na = x == S;
-            const int c = sb[(size_t)site * a.F + f];
+            const int c = a.src_pm ? sb[(size_t)f * a.Np + s] : sb[(size_t)site * a.F + f];
             const double w0 = wb[(size_t)f * C] * 1.0;
             const double w1 = wb[(size_t)f * C + 1] * (hz ? 1.0 : 0.0);
             double sum = w0 + w1, w2 = 0.0;
@@ -646,16 +665,23 @@ __global__ __launch_bounds__(WAVE) void lik_source_generic_kernel(LikArgs a) {
 // Source kernel, table form (lik_source_rc_kernel; the default where it applies).  Rows (each S1
 // doubles): T0[h] (h = hz | hf << 1, w_norm[h][0] * l0) 0..3, T1[z][hf] (w_norm[1|hf<<1][1] * l1)
 // from 4, T2[fam][hz] (w_norm[2|hz][2] * l2) from 4 + 2Z, the zero rows Z0[h] of a selected
-// component the site lacks (weight w_c * 0 / sum_h, lh 0), the neutral row rn (padding).  The
-// repack writes each cell's ROW INDEX (its source byte mapped through the chain's zone and the
-// site's family, repack_source_kernel), so a cell costs one multiply-add for its address, one
-// ds_read_b64 and one v_mul_f64.  Per feature each lane loads
-// (buffer loads, scalar per-feature offsets, one feature ahead) p_global[x], the p_zones rows
-// lg, lg + G and the p_families rows lg, lg + G of its state x = lane % S1 (NA lanes read
-// out of range: 0, plus `naone` = 1), and writes T0[h] and Z0[h] (h = lg, lg + G, .. < 4), the two T1 rows of each zone
-// and the two T2 rows of each family.  Normalised weights come from per-batch LDS (prep).  Inputs
-// are checked as in the dense kernel (one unsigned max; products checked when renormalised, the
-// task re-run per factor when one left the normal range, e.g. a zero weight's -inf cell).
+// component the site lacks (weight w_c * 0 / sum_h, lh 0), the neutral row rn (padding).
+//
+// The sources come POSITION-MAJOR, [B][F][Np] component bytes in the context's family-sorted
+// site order (sbz_loglik_batch_device_pm; the sampler keeps them so), read in place with the
+// observations' layout: one dword = 4 positions of one feature.  A cell's table row depends on
+// its component c and its site's class only, so per chunk each lane holds, for each of its
+// 4-position groups, three ROW-MAP words M_c (byte j = the row of component c at position j of
+// the group); per feature the group's row word is two v_perm_b32 byte selects of its source word:
+// bit 0 of each c picks M0 / M1, bit 1 then picks M2 (c <= 2).  A cell then costs one
+// multiply-add for its address (row * row_bytes + x * 8), one ds_read_b64 and one v_mul_f64.
+// Per feature each lane loads (buffer loads, scalar per-feature offsets, one feature ahead)
+// p_global[x], the p_zones rows lg, lg + G and the p_families rows lg, lg + G of its state
+// x = lane % S1 (NA lanes read out of range: 0, plus `naone` = 1), and writes T0[h] and Z0[h]
+// (h = lg, lg + G, .. < 4), the two T1 rows of each zone and the two T2 rows of each family.
+// Normalised weights come from per-batch LDS (prep).  Inputs are checked as in the dense kernel
+// (one unsigned max; products checked when renormalised, the task re-run per factor when one
+// left the normal range, e.g. a zero weight's -inf cell).
 // ---------------------------------------------------------------------------------------
 constexpr int SRC_NWC = 32;  // features per normalised-weight batch
 #ifndef SBZ_SRC_RC_WAVES
@@ -676,7 +702,7 @@ __global__ __launch_bounds__(WAVE, SBZ_SRC_RC_WAVES) void lik_source_rc_kernel(L
     const int S = a.S, S1 = a.S + 1, Z = a.Z;
     const int Fam = (C == 3) ? a.Fam : 0;
     const int off1 = 4, off2 = 4 + 2 * Z, rz = off2 + 2 * Fam, rn = rz + 4;
-    const int row_bytes = S1 * 8;
+    const uint32_t row_bytes = (uint32_t)S1 * 8u;
     double *tab = reinterpret_cast<double *>(lds);
     double *nwt = tab + ((((rn + 1) * S1) + 1) & ~1);  // [SRC_NWC][8], 16-B aligned
     double *junk = nwt + SRC_NWC * 8 + lane;
@@ -702,7 +728,7 @@ __global__ __launch_bounds__(WAVE, SBZ_SRC_RC_WAVES) void lik_source_rc_kernel(L
     const __amdgpu_buffer_rsrc_t robs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(a.obs_fm), (short)0,
                                                                           a.F * a.Np, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t *>(a.src_fm + (size_t)b * a.F * a.Np), (short)0, a.F * a.Np, 0x00020000);
+        const_cast<uint8_t *>(a.src_pm + (size_t)b * a.F * a.Np), (short)0, a.F * a.Np, 0x00020000);
     // lane offsets (bytes) of its parameter rows; rows past Z / Fam read a valid row (unused)
     const uint32_t vg = na ? OOB : lxc * 8u;
     uint32_t vz[2], vf[2];
@@ -819,6 +845,7 @@ __global__ __launch_bounds__(WAVE, SBZ_SRC_RC_WAVES) void lik_source_rc_kernel(L
     uint64_t under;
     SrcParams P[2];
     uint32_t O[2][NO], R[2][NO];
+    uint32_t M0[NO], M1[NO], M2[NO];  // row maps of the lane's position groups (see above)
     // a product that left the normal range (0, tiny, or NaN: fmin would drop a NaN) re-runs the
     // task per factor, where every cell's row is checked for a zero weight
     auto flush = [&]() {
@@ -828,8 +855,14 @@ __global__ __launch_bounds__(WAVE, SBZ_SRC_RC_WAVES) void lik_source_rc_kernel(L
         for (int q = 0; q < 4; q++)
             if (q < NO) renorm(m[q], e);
     };
+    // the 4 table rows of position group k from its 4 component bytes
+    auto rows_of = [&](int k, uint32_t cw) -> uint32_t {
+        const uint32_t r01 = __builtin_amdgcn_perm(M1[k], M0[k], ((cw & 0x01010101u) << 2) + 0x03020100u);
+        if (C == 2) return r01;
+        return __builtin_amdgcn_perm(M2[k], r01, ((cw & 0x02020202u) << 1) + 0x03020100u);
+    };
     auto feature = [&](int f, int c0, bool live, const SrcParams &cur, const uint32_t (&ob)[NO],
-                       const uint32_t (&rb)[NO], SrcParams &fill, uint32_t (&ofill)[NO], uint32_t (&rfill)[NO]) {
+                       const uint32_t (&sb)[NO], SrcParams &fill, uint32_t (&ofill)[NO], uint32_t (&sfill)[NO]) {
         const int fk = min(f, fb - 1);
         if (fk < nwf0 || fk >= nwf0 + SRC_NWC) prep(fk);
         const bool wide = build(cur, fk) || force;
@@ -837,12 +870,15 @@ __global__ __launch_bounds__(WAVE, SBZ_SRC_RC_WAVES) void lik_source_rc_kernel(L
         const int fn = min(f + 1, fb - 1);
         load(fn, fill);
         load_words(robs, fn, c0, ofill);
-        load_words(rsrc, fn, c0, rfill);
+        load_words(rsrc, fn, c0, sfill);
         if (!live) return;
+        uint32_t rw[NO];
+#pragma unroll
+        for (int k = 0; k < NO; k++) rw[k] = rows_of(k, sb[k]);
         auto addr = [&](int k, int j) {
             const uint32_t xb = (ob[k] >> (8 * j)) & 0xffu;
-            const uint32_t rr = (rb[k] >> (8 * j)) & 0xffu;
-            return rr * (uint32_t)row_bytes + (XS8 ? xb : (xb << 3));
+            const uint32_t rr = (rw[k] >> (8 * j)) & 0xffu;
+            return rr * row_bytes + (XS8 ? xb : (xb << 3));
         };
         if (!wide) {
 #pragma unroll
@@ -860,7 +896,7 @@ __global__ __launch_bounds__(WAVE, SBZ_SRC_RC_WAVES) void lik_source_rc_kernel(L
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     mul_exact(m[0], e, *reinterpret_cast<const double *>(lds + addr(k, j)));
-                    zw |= zrow[(rb[k] >> (8 * j)) & 0xffu];
+                    zw |= zrow[(rw[k] >> (8 * j)) & 0xffu];
                 }
         }
     };
@@ -870,9 +906,52 @@ __global__ __launch_bounds__(WAVE, SBZ_SRC_RC_WAVES) void lik_source_rc_kernel(L
         e = 0;
         under = 0;
         for (int c0 = 0; c0 < a.Np; c0 += SPL * WAVE) {
+            // row maps of this chunk's positions: the chain's zone of each site and its family
+            // class.  Component c -> T0[h] (c = 0), T1[z][hf] (c = 1, zoned sites), T2[fam][hz]
+            // (c = 2, sites with a family), else the zero row of h; padding -> the neutral row.
+            const uint8_t *zb = a.zone + (size_t)b * a.N;
+            int4 pv[NO];
+            uint32_t fw[NO];
+#pragma unroll
+            for (int k = 0; k < NO; k++) {
+                const uint32_t p0 = (uint32_t)(c0 + 4 * lane + 256 * k);  // < Np (arrays padded)
+                pv[k] = *reinterpret_cast<const int4 *>(a.perm + p0);
+                fw[k] = *reinterpret_cast<const uint32_t *>(a.famc + p0);
+            }
+            uint32_t zs[NO][4];
+#pragma unroll
+            for (int k = 0; k < NO; k++) {
+                zs[k][0] = zb[(uint32_t)pv[k].x];
+                zs[k][1] = zb[(uint32_t)pv[k].y];
+                zs[k][2] = zb[(uint32_t)pv[k].z];
+                zs[k][3] = zb[(uint32_t)pv[k].w];
+            }
             load(fa, P[0]);
             load_words(robs, fa, c0, O[0]);
             load_words(rsrc, fa, c0, R[0]);
+#pragma unroll
+            for (int k = 0; k < NO; k++) {
+                uint32_t m0 = 0, m1 = 0, m2 = 0;
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int pos = c0 + 4 * lane + 256 * k + j;
+                    const int z = (int)zs[k][j];
+                    const int fc = C == 3 ? (int)((fw[k] >> (8 * j)) & 0xffu) : 0;
+                    const bool hz = z < Z, hf = fc > 0;
+                    const uint32_t h = (hz ? 1u : 0u) | (hf ? 2u : 0u);
+                    const uint32_t rl = (uint32_t)rz + h;  // a component the site lacks
+                    uint32_t r0 = h;
+                    uint32_t r1 = hz ? (uint32_t)(off1 + 2 * z) + (hf ? 1u : 0u) : rl;
+                    uint32_t r2 = hf ? (uint32_t)(off2 + 2 * (fc - 1)) + (hz ? 1u : 0u) : rl;
+                    if (pos >= a.N) r0 = r1 = r2 = (uint32_t)rn;
+                    m0 |= r0 << (8 * j);
+                    m1 |= r1 << (8 * j);
+                    m2 |= r2 << (8 * j);
+                }
+                M0[k] = m0;
+                M1[k] = m1;
+                M2[k] = m2;
+            }
             for (int f = fa; f < fb; f += 2) {
                 feature(f, c0, true, P[0], O[0], R[0], P[1], O[1], R[1]);
                 feature(f + 1, c0, f + 1 < fb, P[1], O[1], R[1], P[0], O[0], R[0]);
@@ -887,118 +966,118 @@ __global__ __launch_bounds__(WAVE, SBZ_SRC_RC_WAVES) void lik_source_rc_kernel(L
     finish_chain(a, b, tot, lane == 0, __ballot(zw != 0) != 0);
 }
 
-// Row-major source [B][N][F] -> feature-major row codes [B][F][Np] in the family-sorted site
-// order: each byte is the cell's table row in lik_source_rc_kernel, the source component c mapped
-// through the chain's zone of the site and its family class (a component the site lacks, or
-// c >= C -> the zero row of the site's class h; padding -> the neutral row).  One workgroup
-// transposes a tile of RP_T positions x RP_F features through LDS.  Read side: RP_F / 16 lanes
-// per site row, each loading 16 feature bytes as 4-byte words (F a multiple of 4); every pass's
-// loads are issued before the first is used.  Write side: 4 lanes per feature, each storing 16
-// position bytes per 64-position subtile.  (Tile shapes and non-temporal loads / stores measured
-// in round 2: DESIGN.md §3.3.)
+// Source layout transposes between the reference layout [B][N][F] (site-major, row s = site s)
+// and the position-major layout [B][F][Np] (row f = feature f, column p = site perm[p] of the
+// context's family-sorted order; padding columns p >= N hold 0).  One workgroup moves a tile of
+// RP_T positions x RP_F features through LDS: on the site-major side RP_F / 16 lanes per site row
+// (16 feature bytes each, as 4-byte words when F is a multiple of 4), on the position-major side
+// 4 lanes per feature row (16 position bytes each per 64-position subtile, one 16-B access).
+// (Tile shapes measured in round 2)
 constexpr int RP_T = 256;  // positions per workgroup (a multiple of 64)
 constexpr int RP_F = 64;   // features per workgroup (a multiple of 16, RP_F / 16 divides 256)
-__global__ __launch_bounds__(256) void repack_source_kernel(int N, int F, int Np, const int *perm,
-                                                            const uint8_t *src, uint8_t *dst,
-                                                            const uint8_t *zone, const uint8_t *famc,
-                                                            int Z, int Fam, int C) {
-    constexpr int RW = RP_F / 4 + 1;  // words per LDS row (odd: the write side's 4 position
-                                      // groups fall in distinct banks)
+template <bool TO_PM>
+__global__ __launch_bounds__(256) void source_transpose_kernel(int N, int F, int Np, const int *perm,
+                                                               const uint8_t *src, uint8_t *dst) {
+    constexpr int RW = RP_F / 4 + 1;  // words per LDS row (odd: the position-major side's 4
+                                      // position groups fall in distinct banks)
     constexpr int LR = RP_F / 16;     // lanes per site row
     constexpr int RPP = 256 / LR;     // rows per pass
     constexpr int NP = RP_T / RPP;    // passes
     __shared__ uint32_t tile[RP_T][RW];  // [position][feature word]
+    uint8_t *tb = reinterpret_cast<uint8_t *>(&tile[0][0]);
     const int tid = threadIdx.x;
     const int p0 = blockIdx.x * RP_T, f0 = blockIdx.y * RP_F;
     const size_t b = blockIdx.z;
     const int l = tid % LR, rg = tid / LR;  // lane l of row group rg: features f0 + 16 l ..
     const int fq = f0 + 16 * l;
     const bool words = (F & 3) == 0 && fq + 16 <= F;
-    uint32_t w[NP][4];
-    int row[NP];
+    const int q = tid & 3;  // position-major side: positions p0 + 64 t + 16 q .. of feature f0 + fr
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    if (TO_PM) {
+        uint32_t w[NP][4];
+        int row[NP];
 #pragma unroll
-    for (int t = 0; t < NP; t++) {
-        const int p = p0 + RPP * t + rg;
-        row[t] = p < N ? perm[p] : -1;
-    }
+        for (int t = 0; t < NP; t++) {
+            const int p = p0 + RPP * t + rg;
+            row[t] = p < N ? perm[p] : -1;
+        }
 #pragma unroll
-    for (int t = 0; t < NP; t++) {
-        if (row[t] >= 0 && fq < F) {
-            const uint8_t *rp = src + (b * N + row[t]) * F;
-            if (words) {
-                const uint32_t *wp = reinterpret_cast<const uint32_t *>(rp + fq);
+        for (int t = 0; t < NP; t++) {
+            if (row[t] >= 0 && fq < F) {
+                const uint8_t *rp = src + (b * N + row[t]) * F;
+                if (words) {
+                    const uint32_t *wp = reinterpret_cast<const uint32_t *>(rp + fq);
 #pragma unroll
-                for (int k = 0; k < 4; k++) w[t][k] = wp[k];
+                    for (int k = 0; k < 4; k++) w[t][k] = wp[k];
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        uint32_t x = 0;
+#pragma unroll
+                        for (int j = 0; j < 4; j++) x |= (fq + 4 * k + j < F ? (uint32_t)rp[fq + 4 * k + j] : 0u) << (8 * j);
+                        w[t][k] = x;
+                    }
+                }
             } else {
+#pragma unroll
+                for (int k = 0; k < 4; k++) w[t][k] = 0;
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < NP; t++)
+#pragma unroll
+            for (int k = 0; k < 4; k++) tile[RPP * t + rg][4 * l + k] = w[t][k];
+        __syncthreads();
+        for (int fr = tid >> 2; fr < RP_F; fr += 64) {
+            const int f = f0 + fr;
+            if (f >= F) break;
+            uint8_t *drow = dst + (b * F + f) * Np + p0 + 16 * q;
+#pragma unroll
+            for (int t = 0; t < RP_T / 64; t++) {
+                if (p0 + 64 * t >= Np) break;
+                uint32_t o[4];
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
                     uint32_t x = 0;
 #pragma unroll
-                    for (int j = 0; j < 4; j++) x |= (fq + 4 * k + j < F ? (uint32_t)rp[fq + 4 * k + j] : 0u) << (8 * j);
-                    w[t][k] = x;
+                    for (int j = 0; j < 4; j++) x |= (uint32_t)tb[(64 * t + 16 * q + 4 * k + j) * (RW * 4) + fr] << (8 * j);
+                    o[k] = x;
                 }
+                // Np is a multiple of 64, so the 16 bytes are 16-byte aligned and inside the row
+                const u32x4 ov = {o[0], o[1], o[2], o[3]};
+                *reinterpret_cast<u32x4 *>(drow + 64 * t) = ov;
             }
-        } else {
-#pragma unroll
-            for (int k = 0; k < 4; k++) w[t][k] = 0;
         }
-    }
-    const int off2 = 4 + 2 * Z, rz = off2 + 2 * Fam, rn = rz + 4;
+    } else {
+        for (int fr = tid >> 2; fr < RP_F; fr += 64) {
+            const int f = f0 + fr;
+            if (f >= F) break;
+            const uint8_t *srow = src + (b * F + f) * Np + p0 + 16 * q;
 #pragma unroll
-    for (int t = 0; t < NP; t++) {
-        {
-            // row map of this position: byte c = table row of component c (c = 3: c >= C)
-            uint32_t map;
-            if (row[t] >= 0) {
-                const int z = zone[b * N + row[t]];
-                const bool hz = z < Z;
-                const int fc = (C == 3) ? famc[p0 + RPP * t + rg] : 0;
-                const bool hf = fc > 0;
-                const uint32_t r0 = (hz ? 1u : 0u) | (hf ? 2u : 0u);
-                const uint32_t rl = (uint32_t)rz + r0;  // a component the site lacks: zero row of h
-                const uint32_t r1 = hz ? (uint32_t)(4 + 2 * z + (hf ? 1 : 0)) : rl;
-                const uint32_t r2 = (C == 3 && hf) ? (uint32_t)(off2 + 2 * (fc - 1) + (hz ? 1 : 0)) : rl;
-                map = r0 | (r1 << 8) | (r2 << 16) | (rl << 24);
+            for (int t = 0; t < RP_T / 64; t++) {
+                if (p0 + 64 * t >= Np) break;
+                const u32x4 iv = *reinterpret_cast<const u32x4 *>(srow + 64 * t);
+                const uint32_t o[4] = {iv.x, iv.y, iv.z, iv.w};
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+#pragma unroll
+                    for (int j = 0; j < 4; j++) tb[(64 * t + 16 * q + 4 * k + j) * (RW * 4) + fr] = (uint8_t)(o[k] >> (8 * j));
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < NP; t++) {
+            const int p = p0 + RPP * t + rg;
+            const int s = p < N ? perm[p] : -1;
+            if (s < 0 || fq >= F) continue;
+            uint8_t *rp = dst + (b * N + s) * F;
+            if (words) {
+                uint32_t *wp = reinterpret_cast<uint32_t *>(rp + fq);
+#pragma unroll
+                for (int k = 0; k < 4; k++) wp[k] = tile[RPP * t + rg][4 * l + k];
             } else {
-                map = (uint32_t)rn * 0x01010101u;
+                for (int i = 0; i < 16 && fq + i < F; i++) rp[fq + i] = tb[(RPP * t + rg) * (RW * 4) + 16 * l + i];
             }
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                uint32_t x = 0;
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const uint32_t c = min((w[t][k] >> (8 * j)) & 0xffu, 3u);
-                    x |= ((map >> (8 * c)) & 0xffu) << (8 * j);
-                }
-                w[t][k] = x;
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < 4; k++) tile[RPP * t + rg][4 * l + k] = w[t][k];
-    }
-    __syncthreads();
-    const uint8_t *tb = reinterpret_cast<const uint8_t *>(&tile[0][0]);
-    const int q = tid & 3;  // positions p0 + 64 t + 16 q .. of feature f0 + fr
-    for (int fr = tid >> 2; fr < RP_F; fr += 64) {
-        const int f = f0 + fr;
-        if (f >= F) break;
-        uint8_t *drow = dst + (b * F + f) * Np + p0 + 16 * q;
-#pragma unroll
-        for (int t = 0; t < RP_T / 64; t++) {
-            if (p0 + 64 * t >= Np) break;
-            uint32_t o[4];
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                uint32_t x = 0;
-#pragma unroll
-                for (int j = 0; j < 4; j++) x |= (uint32_t)tb[(64 * t + 16 * q + 4 * k + j) * (RW * 4) + fr] << (8 * j);
-                o[k] = x;
-            }
-            // Np is a multiple of 64, so the 16 bytes are 16-byte aligned and inside the row
-            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-            u32x4 *dp = reinterpret_cast<u32x4 *>(drow + 64 * t);
-            const u32x4 ov = {o[0], o[1], o[2], o[3]};
-            *dp = ov;
         }
     }
 }
@@ -1124,7 +1203,12 @@ int tasks_per_chain(sbz_ctx *ctx, const void *fn, size_t lds, int B) {
         ctx->mix_occ = (e == hipSuccess && occ > 0) ? occ : 8;
         ctx->mix_occ_fn = fn;
     }
-    const int per_cu = ctx->tasks_per_cu > 0 ? ctx->tasks_per_cu : ctx->mix_occ;
+    // a chain's tasks all resident at once (occupancy x CUs), except for few sites per lane
+    // (N <= 256): there the per-task set-up and the finish outweigh the per-feature work of more,
+    // shorter tasks, and 4 tasks per CU measured fastest (cfg2 / cfg3 / cfg4 shapes: 28 / 22 / 16 us
+    // at the occupancy, 12 / 15 / 12 at 4; profiles/r03_lik_tasks_per_cu.txt)
+    const int per_cu = ctx->tasks_per_cu > 0 ? ctx->tasks_per_cu
+                                             : (ctx->spl <= 4 ? std::min(4, ctx->mix_occ) : ctx->mix_occ);
     const int F = ctx->d.n_features;
     return std::max(1, std::min((F + 1) / 2, (ctx->n_cu * per_cu + B - 1) / B));
 }
@@ -1162,8 +1246,22 @@ int lik_configure(sbz_ctx *ctx) {
     return SBZ_OK;
 }
 
+int launch_source_transpose(sbz_ctx *ctx, int B, const uint8_t *src, uint8_t *dst, bool to_pm) {
+    if (B <= 0) return SBZ_OK;
+    const dim3 grid((ctx->Np + RP_T - 1) / RP_T, (ctx->d.n_features + RP_F - 1) / RP_F, B);
+    if (to_pm)
+        source_transpose_kernel<true><<<grid, 256, 0, ctx->stream>>>(ctx->d.n_sites, ctx->d.n_features, ctx->Np,
+                                                                     ctx->d_perm, src, dst);
+    else
+        source_transpose_kernel<false><<<grid, 256, 0, ctx->stream>>>(ctx->d.n_sites, ctx->d.n_features, ctx->Np,
+                                                                      ctx->d_perm, src, dst);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? SBZ_OK : hip_fail(ctx, e, "source_transpose_kernel launch");
+}
+
 int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, const double *pg,
-                  const double *pz, const double *pf, const uint8_t *source, double *out_ll) {
+                  const double *pz, const double *pf, const uint8_t *source, bool source_pm,
+                  double *out_ll) {
     const sbz_dims &d = ctx->d;
     const bool src_mode = source != nullptr;
     if (ctx->C == 3 && d.n_families > 0 && pf == nullptr)
@@ -1219,11 +1317,12 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
             lds = source_rc_lds_bytes(d, ctx->C);
             const int W = tasks_per_chain(ctx, fn, lds, B);
             a.fpw = (F + W - 1) / W;
-            names = "repack_source_kernel lik_source_rc_kernel";
+            names = source_pm ? "lik_source_rc_kernel" : "source_transpose_kernel lik_source_rc_kernel";
         } else {
             fn = ctx->C == 3 ? reinterpret_cast<const void *>(&lik_source_generic_kernel<3>)
                              : reinterpret_cast<const void *>(&lik_source_generic_kernel<2>);
-            a.src_rm = source;
+            if (source_pm) a.src_pm = source;
+            else a.src_rm = source;
             names = "lik_source_generic_kernel";
         }
     }
@@ -1257,15 +1356,16 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
         (void)hipMemsetAsync(ctx->zflag.ptr, 0, ctx->zflag.bytes, st);
         return hip_fail(ctx, e, what);
     };
-    if (src_rc) {  // row codes for lik_source_rc_kernel
-        rc = ensure(ctx, ctx->src_t, (size_t)B * F * ctx->Np);
-        if (rc) return rc;
-        const dim3 rgrid((ctx->Np + RP_T - 1) / RP_T, (F + RP_F - 1) / RP_F, B);
-        repack_source_kernel<<<rgrid, 256, 0, st>>>(d.n_sites, F, ctx->Np, ctx->d_perm, source,
-                                                    static_cast<uint8_t *>(ctx->src_t.ptr), zone,
-                                                    ctx->d_famc, d.n_zones,
-                                                    ctx->C == 3 ? d.n_families : 0, ctx->C);
-        a.src_fm = static_cast<const uint8_t *>(ctx->src_t.ptr);
+    if (src_rc) {
+        if (source_pm) {
+            a.src_pm = source;
+        } else {  // the reference layout: transposed to the position-major one first
+            rc = ensure(ctx, ctx->src_t, (size_t)B * F * ctx->Np);
+            if (rc) return rc;
+            rc = launch_source_transpose(ctx, B, source, static_cast<uint8_t *>(ctx->src_t.ptr), true);
+            if (rc) return rc;
+            a.src_pm = static_cast<const uint8_t *>(ctx->src_t.ptr);
+        }
     }
     ctx->last_kernels = names;
     void *args[] = {&a};

@@ -449,7 +449,8 @@ struct Chain {
 struct MhArgs {
     int N, F, S, Z, Fam, C, FamC, Np, xs8;
     int n_steps, nops, min_size, warmup;
-    int la;     // mh_kernel, Philox draws: proposals planned ahead per batch (1 = none; <= 6)
+    int la;     // mh_kernel, Philox draws: proposals planned ahead per batch (1 = none; <= LA = 24;
+                // the host lowers it until the plan columns fit the 160 KiB of LDS)
     int stage;  // mh_src_kernel: parameters and normalised weights staged in LDS for the N*F passes
     int cstage; // mh_src_kernel (with stage): the constant tables (applicable states, Gibbs prior
                 //   counts, 'counts' prior) staged in LDS too
@@ -469,7 +470,8 @@ struct MhArgs {
     int size_prior;             // 0 none, 1 uniform, 2 quadratic
     const double *gc_g;         // [F][S] Gibbs prior counts of p_global (sbz_set_gibbs_counts) or null = 1
     const double *gc_f;         // [Fam][F][S] of p_families, or null = 1
-    uint8_t *src_scratch;       // [B][N][F] candidate sources when they live in HBM (source mode)
+    uint8_t *src_scratch;       // [B][F][Np] candidate sources when they live in HBM (source mode)
+    int src_pm;                 // ch.source is [B][F][Np] by position (SBZ_SOURCE_BY_POSITION)
     const double *geo_cost;     // [N][N] 'cost_based' geo prior costs (sbz_set_geo_prior), or null
     double geo_scale;
     sbz_chains ch;

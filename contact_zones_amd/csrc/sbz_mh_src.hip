@@ -51,10 +51,9 @@ namespace {
 // likelihoods model.py:230-249 with NA -> 1 for every component; normalize_weights :436-452).
 template <int C>
 __device__ __forceinline__ void obs_terms(const MhArgs &a, const double *w, const double *pg,
-                                          const double *pz, const double *pf, int s, int f, int zc,
+                                          const double *pz, const double *pf, int f, int x, int zc,
                                           int fc, double (&l)[3], double (&wn)[3]) {
     const int S = a.S, F = a.F, Z = a.Z;
-    const int x = a.obs_sm[(size_t)s * F + f];
     const bool na = x >= S;
     const int xc = na ? 0 : x;
     const bool hz = zc < Z;
@@ -115,6 +114,19 @@ size_t mh_src_const_bytes(const sbz_dims &d, int C, bool alg, bool alf, bool gcg
 
 namespace {
 
+// (p, f) of position-major cell i = f * Np + p, advanced by NT cells per step
+struct PosWalk {
+    int p, f, dP, dF, Np;
+    __device__ __forceinline__ void next() {
+        p += dP;
+        f += dF;
+        if (p >= Np) {
+            p -= Np;
+            f++;
+        }
+    }
+};
+
 // (s, f) of cell c = s * F + f, advanced by NT cells per step
 struct CellWalk {
     int s, f, dS, dF, F;
@@ -134,9 +146,13 @@ struct CellWalk {
 // and the per-feature Gibbs draws.  Shared LDS state (zone assignment, counters) is written by
 // thread 0 and published by a barrier.
 // GS: the current sources are the chain's own array in HBM (updated in place) and the candidate
-// sources a per-chain scratch row, for N * F too large for LDS.  Only this chain's threads touch
-// them; they exchange cells through agent-scope (sc1, L1-bypassing) byte accesses and a
-// vmcnt(0) wait at every barrier.
+// sources a per-chain scratch row, for N * F too large for LDS, both POSITION-MAJOR ([F][Np], the
+// context's family-sorted site order; launch_mh_source transposes a caller's site-major array):
+// the N * F passes then walk the cells feature by feature, consecutive threads on consecutive
+// positions, so every source and observation access is coalesced.  Only this chain's threads
+// touch them; they exchange cells through agent-scope (sc1, L1-bypassing) byte accesses and a
+// vmcnt(0) wait at every barrier.  Without GS the sources live in LDS as [N][F]; a.src_pm says
+// which layout the chain's array in HBM has (copied in and out at the launch's ends).
 template <int C, bool GS, int NW>
 __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     constexpr int NT = NW * WAVE;
@@ -223,10 +239,12 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     };
 
     uint8_t *gzos = ch.zone_of_site + (size_t)b * N;
-    uint8_t *gsrc = ch.source + (size_t)b * NF;
+    const int Np = a.Np;
+    const size_t NFP = (size_t)F * Np;  // position-major cells per chain
+    uint8_t *gsrc = ch.source + (size_t)b * (a.src_pm ? NFP : (size_t)NF);
     if (GS) {
         src = gsrc;
-        srcb = a.src_scratch + (size_t)b * NF;
+        srcb = a.src_scratch + (size_t)b * NFP;
     }
     // source cell access
     auto rsrc = [&](const uint8_t *p, int c) -> int {
@@ -296,8 +314,16 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     }
     if (tid < MH_STAT_INTS) stat[tid] = 0;
     for (int s = tid; s < N; s += NT) nb[s] = 0;
-    if (!GS)
-        for (int c = tid; c < NF; c += NT) src[c] = gsrc[c];
+    if (!GS) {
+        if (a.src_pm) {  // [F][Np] by position -> [N][F] by site
+            for (int i = tid; i < (int)NFP; i += NT) {
+                const int f = i / Np, p = i - f * Np;
+                if (p < N) src[a.perm[p] * F + f] = gsrc[i];
+            }
+        } else {
+            for (int c = tid; c < NF; c += NT) src[c] = gsrc[c];
+        }
+    }
     sync();
     int occ = 0;
     for (int s = tid; s < N; s += NT) {
@@ -410,15 +436,16 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         sync();
         stg_ok = true;
     };
-    // obs_terms from the staged copies (the same values, the same operations)
-    auto terms = [&](int s, int f, double (&l)[3], double (&wn)[3]) {
+    // obs_terms from the staged copies (the same values, the same operations); x = the observed
+    // state of (s, f) (S = NA)
+    auto terms = [&](int s, int f, int x, double (&l)[3], double (&wn)[3]) {
         const int zc = zos[s];
         if (!stg) {
             const int fc = C == 3 ? a.fam_site[s] : 0;
-            obs_terms<C>(a, w, pg, pz, pf, s, f, zc, fc, l, wn);
+            obs_terms<C>(a, w, pg, pz, pf, f, x, zc, fc, l, wn);
             return;
         }
-        const int x = lobs[s * F + f], fc = lfam[s];
+        const int fc = lfam[s];
         const bool na = x >= S;
         const int xc = na ? 0 : x;
         const bool hz = zc < Z, hf = (C == 3) && fc > 0;
@@ -430,9 +457,33 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         l[1] = na ? 1.0 : (hz ? lpz[(zc * F + f) * S + xc] : 0.0);
         l[2] = (C == 3) ? (na ? 1.0 : (hf ? lpf[((fc - 1) * F + f) * S + xc] : 0.0)) : 0.0;
     };
-    // ---- passes over the N*F observations (cell c = s*F + f, C order); (s, f) stepped with the
-    // cell index (CellWalk) instead of a division per cell
+    // ---- passes over the N*F observations; (s, f) stepped with the cell index instead of a
+    // division per cell.  body(s, f, x, g, c): x the observed state, g the cell's index in the
+    // source arrays, c = s * F + f its index in C order (the reference's order of the tape's
+    // per-observation uniforms).  Without GS the cells go in C order (g = c, LDS [N][F]); with GS
+    // position-major (g = f * Np + p, s = perm[p]), so consecutive threads read consecutive bytes.
     const int cdS = NT / F, cdF = NT - cdS * F;
+    const int pdF = NT / Np, pdP = NT - pdF * Np;
+    const int xdiv = a.xs8 ? 8 : 1;
+    auto for_cells = [&](auto &&body) {
+        if constexpr (!GS) {
+            CellWalk cw{tid / F, tid - (tid / F) * F, cdS, cdF, F};
+            for (int c = tid; c < NF; c += NT, cw.next()) {
+                const int x = stg ? lobs[c] : a.obs_sm[c];
+                body(cw.s, cw.f, x, c, c);
+            }
+        } else {
+            PosWalk pw{tid - (tid / Np) * Np, tid / Np, pdP, pdF, Np};
+            for (int i = tid; i < (int)NFP; i += NT, pw.next()) {
+                const int p = pw.p, f = pw.f;
+                if (p >= N) continue;
+                const int s = a.perm[p];
+                const int c = s * F + f;
+                const int x = stg ? lobs[c] : a.obs_fm[i] / xdiv;
+                body(s, f, x, i, c);
+            }
+        }
+    };
     // Sums of logs as one log per thread: each factor's mantissa multiplies a product and its
     // exponent adds to an integer (exact for any factor, denormals included), the product is
     // renormalised every 8 cells, and log(m) + e ln 2 is taken once (~1e-16 relative).
@@ -454,14 +505,12 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     auto pass_logq = [&]() -> double {
         ensure_staged();
         LogAcc acc;
-        CellWalk cw{tid / F, tid - (tid / F) * F, cdS, cdF, F};
-        for (int c = tid; c < NF; c += NT, cw.next()) {
-            const int s = cw.s, f = cw.f;
+        for_cells([&](int s, int f, int x, int g, int) {
             double l[3], wn[3], p[3];
-            terms(s, f, l, wn);
+            terms(s, f, x, l, wn);
             posterior_draw<C>(l, wn, 2.0, p);
-            acc.add(p[rsrc(src, c)]);
-        }
+            acc.add(p[rsrc(src, g)]);
+        });
         return bsum(acc.value());
     };
     // log-likelihood of the current sample with sources `sv` (combine_lh source branch,
@@ -470,15 +519,13 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         ensure_staged();
         LogAcc acc;
         int zero_w = 0;
-        CellWalk cw{tid / F, tid - (tid / F) * F, cdS, cdF, F};
-        for (int c = tid; c < NF; c += NT, cw.next()) {
-            const int s = cw.s, f = cw.f;
+        for_cells([&](int s, int f, int x, int g, int) {
             double l[3], wn[3];
-            terms(s, f, l, wn);
-            const int k = rsrc(sv, c);
+            terms(s, f, x, l, wn);
+            const int k = rsrc(sv, g);
             zero_w |= wn[k] == 0.0;
             acc.add(wn[k] * l[k]);
-        }
+        });
         const double v = bsum(acc.value());
         return bor(zero_w) ? -INFINITY : v;
     };
@@ -493,18 +540,16 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         int zero_w = 0;
         const int64_t pos0 = rng.pos;
         const bool have = !rng.tape || pos0 + NF <= rng.len;
-        CellWalk cw{tid / F, tid - (tid / F) * F, cdS, cdF, F};
-        for (int c = tid; c < NF; c += NT, cw.next()) {
-            const int s = cw.s, f = cw.f;
+        for_cells([&](int s, int f, int x, int g, int c) {
             double l[3], wn[3], p[3];
-            terms(s, f, l, wn);
+            terms(s, f, x, l, wn);
             const double u = rng.tape ? (have ? rng.tape[pos0 + c] : 0.0) : lr.u();
             const int k = posterior_draw<C>(l, wn, u, p);
-            wsrc(srcb, c, k);
+            wsrc(srcb, g, k);
             acc_q.add(p[k]);
             zero_w |= wn[k] == 0.0;
             acc_l.add(wn[k] * l[k]);
-        }
+        });
         if (rng.tape) {
             if (!have) rng.bad = 1;
             rng.pos = uni64(pos0 + NF);
@@ -518,7 +563,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         if (SBZ_SRC_STAMP) tr2 = __builtin_amdgcn_s_memtime();
     };
     auto commit_sources = [&]() {
-        for (int c = tid; c < NF; c += NT) wsrc(src, c, rsrc(srcb, c));
+        for (int c = tid; c < (GS ? (int)NFP : NF); c += NT) wsrc(src, c, rsrc(srcb, c));
         sync();
     };
     // per-feature counts of sources / states into cnt
@@ -766,14 +811,10 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                 break;
             }
             clear_cnt();
-            {
-                CellWalk cw{tid / F, tid - (tid / F) * F, cdS, cdF, F};
-                for (int c = tid; c < NF; c += NT, cw.next()) {
-                    const int s = cw.s, f = cw.f;
-                    const bool in = (C == 2 || fixed == 0) ? zos[s] < Z : (stg ? lfam[s] : a.fam_site[s]) > 0;
-                    if (in) atomicAdd(&cnt[f * C + rsrc(src, c)], 1);
-                }
-            }
+            for_cells([&](int s, int f, int, int g, int) {
+                const bool in = (C == 2 || fixed == 0) ? zos[s] < Z : (stg ? lfam[s] : a.fam_site[s]) > 0;
+                if (in) atomicAdd(&cnt[f * C + rsrc(src, g)], 1);
+            });
             sync();
             LaneRng lr;
             lr.initw(rng, tid);
@@ -849,17 +890,12 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             }
             const int comp = op == G_P_GLOBAL ? 0 : (op == G_P_ZONES ? 1 : 2);
             clear_cnt();
-            {
-                CellWalk cw{tid / F, tid - (tid / F) * F, cdS, cdF, F};
-                for (int c = tid; c < NF; c += NT, cw.next()) {
-                    const int s = cw.s, f = cw.f;
-                    const int x = stg ? lobs[c] : a.obs_sm[c];
-                    bool in = sub[f] && rsrc(src, c) == comp && x < S;
-                    if (comp == 1) in = in && zos[s] == row;
-                    if (comp == 2) in = in && (stg ? lfam[s] : a.fam_site[s]) == row + 1;
-                    if (in) atomicAdd(&cnt[f * S + x], 1);
-                }
-            }
+            for_cells([&](int s, int f, int x, int g, int) {
+                bool in = sub[f] && rsrc(src, g) == comp && x < S;
+                if (comp == 1) in = in && zos[s] == row;
+                if (comp == 2) in = in && (stg ? lfam[s] : a.fam_site[s]) == row + 1;
+                if (in) atomicAdd(&cnt[f * S + x], 1);
+            });
             sync();
             SRC_TS(8);
             double *base = comp == 0 ? pg : (comp == 1 ? pz + (size_t)row * F * S : pf + (size_t)row * F * S);
@@ -956,8 +992,16 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
 
     sync();
     for (int s = tid; s < N; s += NT) gzos[s] = zos[s];
-    if (!GS)
-        for (int c = tid; c < NF; c += NT) gsrc[c] = src[c];
+    if (!GS) {
+        if (a.src_pm) {  // back to [F][Np] by position (padding positions untouched)
+            for (int i = tid; i < (int)NFP; i += NT) {
+                const int f = i / Np, p = i - f * Np;
+                if (p < N) gsrc[i] = src[a.perm[p] * F + f];
+            }
+        } else {
+            for (int c = tid; c < NF; c += NT) gsrc[c] = src[c];
+        }
+    }
     if (tid == 0) {
         ch.ll[b] = ll;
         if (ch.prior) ch.prior[b] = prior;
@@ -997,11 +1041,24 @@ int launch_mh_source(sbz_ctx *ctx, int B, const MhArgs &a0) {
     if (lds > LDS_MAX)
         return fail(ctx, SBZ_EINVAL, "SAMPLE_SOURCE sampler needs " + std::to_string(lds) +
                                          " B of LDS per chain even with the sources in HBM (> 160 KiB)");
-    const size_t nf = (size_t)ctx->d.n_sites * ctx->d.n_features;
+    const size_t nfp = (size_t)ctx->d.n_features * ctx->Np;
+    // the chain's sources: position-major as given, or (site-major) copied in / out by the kernel
+    // (LDS) or transposed around the launch (HBM, whose passes walk them position-major)
+    a.src_pm = a.ch.source_layout == SBZ_SOURCE_BY_POSITION ? 1 : 0;
+    uint8_t *src_sm = nullptr;  // the caller's site-major array, transposed around an HBM launch
     if (gs) {
-        int rc = ensure(ctx, ctx->src_cand, (size_t)B * nf);
+        int rc = ensure(ctx, ctx->src_cand, (size_t)B * nfp);
         if (rc) return rc;
         a.src_scratch = static_cast<uint8_t *>(ctx->src_cand.ptr);
+        if (!a.src_pm) {
+            rc = ensure(ctx, ctx->src_t, (size_t)B * nfp);
+            if (rc) return rc;
+            src_sm = a.ch.source;
+            a.ch.source = static_cast<uint8_t *>(ctx->src_t.ptr);
+            rc = launch_source_transpose(ctx, B, src_sm, a.ch.source, true);
+            if (rc) return rc;
+            a.src_pm = 1;
+        }
     }
     // waves per chain: 8 (SBZ_SRC_WAVES overrides: 1, 4 or 8).  8 waves = 2 per SIMD, so up to
     // 256 VGPRs: no spills.  Measured against 4 on the real-data shapes (tools/src_optime.py):
@@ -1041,6 +1098,7 @@ int launch_mh_source(sbz_ctx *ctx, int B, const MhArgs &a0) {
     else by_gs(std::integral_constant<int, 2>());
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(ctx, e, "source-mode sampler launch");
+    if (src_sm) return launch_source_transpose(ctx, B, a.ch.source, src_sm, false);
     return SBZ_OK;
 }
 

@@ -18,7 +18,7 @@ import ctypes
 import numpy as np
 
 from . import packing
-from ._lib import SBZ_INHERITANCE, check, lib, sbz_dims
+from ._lib import OPTIONS, SBZ_INHERITANCE, check, lib, sbz_dims
 
 
 def _ptr(a):
@@ -28,7 +28,8 @@ def _ptr(a):
 class LikelihoodEngine:
     """Batched full log-likelihood on one MI355X (sbz C-ABI context)."""
 
-    def __init__(self, obs, fam_of_site, n_states, n_zones, n_families, inheritance, device=0):
+    def __init__(self, obs, fam_of_site, n_states, n_zones, n_families, inheritance, device=0,
+                 options=None):
         obs = np.ascontiguousarray(obs, dtype=np.int8)
         n_sites, n_features = obs.shape
         if fam_of_site is None:
@@ -48,6 +49,45 @@ class LikelihoodEngine:
                                  _ptr(self.fam_of_site), ctypes.byref(ctx)))
         self.ctx = ctx
         self.device = device
+        for name, value in (options or {}).items():
+            self.set_option(name, value)
+        # the context's site order (sbz_site_positions): positions[p] = site at position p, -1 for
+        # padding; the position-major source layout [B][F][Np] follows it
+        self.n_positions = int(self._lib.sbz_site_positions(self.ctx, None))
+        self.positions = np.empty(self.n_positions, np.int32)
+        self._lib.sbz_site_positions(self.ctx, self.positions.ctypes.data_as(ctypes.c_void_p))
+        self.position_of_site = np.empty(n_sites, np.int64)
+        self.position_of_site[self.positions[:n_sites]] = np.arange(n_sites)
+
+    def set_option(self, name, value):
+        """sbz_set_option by name (include/sbz.h sbz_option: lik_tasks_per_cu, lik_banked, src_table,
+        src_waves, src_hbm, src_stage, mh_lookahead)."""
+        if name not in OPTIONS:
+            raise ValueError(f"unknown option {name!r} (one of {sorted(OPTIONS)})")
+        check(self._lib.sbz_set_option(self.ctx, OPTIONS[name], int(value)), self.ctx)
+
+    def get_option(self, name):
+        v = ctypes.c_int64()
+        check(self._lib.sbz_get_option(self.ctx, OPTIONS[name], ctypes.byref(v)), self.ctx)
+        return int(v.value)
+
+    def sources_to_positions(self, source):
+        """Host sources [B][N][F] (by site) -> [B][F][Np] (by position, padding 0)."""
+        src = np.asarray(source, np.uint8)
+        out = np.zeros((src.shape[0], self.n_features, self.n_positions), np.uint8)
+        out[:, :, :self.n_sites] = src[:, self.positions[:self.n_sites], :].transpose(0, 2, 1)
+        return out
+
+    def sources_from_positions(self, source_pm):
+        """Host sources [B][F][Np] (by position) -> [B][N][F] (by site)."""
+        pm = np.asarray(source_pm, np.uint8)
+        return np.ascontiguousarray(pm[:, :, self.position_of_site].transpose(0, 2, 1))
+
+    def source_layout_device(self, B, src, dst, to_positions):
+        """sbz_source_layout_device on device pointers (async on the engine's stream)."""
+        v = ctypes.c_void_p
+        check(self._lib.sbz_source_layout_device(self.ctx, int(B), v(src), v(dst), int(bool(to_positions))),
+              self.ctx)
 
     def close(self):
         if getattr(self, "ctx", None):
@@ -106,22 +146,29 @@ class LikelihoodEngine:
               self.ctx)
         return out
 
-    def check_indices_device(self, B, zone_of_site, source=0):
-        """Range-check device index arrays (zone bytes < n_zones or 255, source bytes < C);
-        raises SbzError (SBZ_EINVAL) otherwise.  Synchronises the engine's stream."""
+    def check_indices_device(self, B, zone_of_site, source=0, source_pm=False):
+        """Range-check device index arrays (zone bytes < n_zones or 255, source bytes < C; sources
+        by site [B][N][F], or by position [B][F][Np] with source_pm); raises SbzError (SBZ_EINVAL)
+        otherwise.  Synchronises the engine's stream."""
         v = ctypes.c_void_p
-        check(self._lib.sbz_check_indices_device(self.ctx, int(B), v(zone_of_site), v(source or 0)),
-              self.ctx)
+        fn = self._lib.sbz_check_indices_device_pm if source_pm else self._lib.sbz_check_indices_device
+        check(fn(self.ctx, int(B), v(zone_of_site), v(source or 0)), self.ctx)
 
     def loglik_device(self, B, zone_of_site, w, p_global, p_zones, p_fam, source, out_ll,
-                      validate=True):
+                      validate=True, source_pm=False):
         """Device-pointer variant (ints = device addresses, 0 for None); async on the stream.
-        The kernels trust the index bytes (include/sbz.h), so by default they are range-checked
-        first (one extra pass and a stream sync); callers whose arrays the sampler itself
-        maintains pass validate=False."""
+        source_pm: the sources are [B][F][Np] by position (sbz_loglik_batch_device_pm, read in
+        place), else [B][N][F] by site.  The kernels trust the index bytes (include/sbz.h), so by
+        default they are range-checked first (one extra pass and a stream sync); callers whose
+        arrays the sampler itself maintains pass validate=False."""
         if validate:
-            self.check_indices_device(B, zone_of_site, source)
+            self.check_indices_device(B, zone_of_site, source, source_pm)
         v = ctypes.c_void_p
+        if source_pm and source:
+            check(self._lib.sbz_loglik_batch_device_pm(self.ctx, int(B), v(zone_of_site), v(w),
+                                                       v(p_global), v(p_zones), v(p_fam or 0), v(source),
+                                                       v(out_ll)), self.ctx)
+            return
         check(self._lib.sbz_loglik_batch_device(self.ctx, int(B), v(zone_of_site), v(w), v(p_global),
                                                 v(p_zones), v(p_fam or 0), v(source or 0),
                                                 v(out_ll)), self.ctx)

@@ -425,8 +425,8 @@ class BatchedZoneMCMC:
                       p_global=st.p_global[i].cpu().numpy()[None],
                       p_zones=st.p_zones[i].cpu().numpy(),
                       p_families=st.p_fam[i].cpu().numpy() if st.p_fam is not None else None,
-                      source=(packing.index_to_source(st.source[i].cpu().numpy(), self.n_sources)
-                              if st.source is not None else None),
+                      source=(packing.index_to_source(st.source_of(i).cpu().numpy(), self.n_sources)
+                              if st.source_pm is not None else None),
                       chain=c)
 
     def _max_size_for(self, lo, hi):

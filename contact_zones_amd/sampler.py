@@ -16,7 +16,7 @@ import ctypes
 
 import numpy as np
 
-from ._lib import check, sbz_chains, sbz_mh_config, sbz_state, sbz_tape, sbz_trace
+from ._lib import SBZ_SOURCE_BY_POSITION, check, sbz_chains, sbz_mh_config, sbz_state, sbz_tape, sbz_trace
 
 OPS = ["shrink_zone", "grow_zone", "swap_zone", "alter_weights", "alter_p_global",
        "alter_p_zones", "alter_p_families", "gibbsish_sample_zones",
@@ -78,21 +78,37 @@ class ChainState:
                                       device=dev))
         self.accepted = torch.zeros((self.B, N_OPS_MAX), dtype=torch.int64, device=dev)
         self.proposed = torch.zeros((self.B, N_OPS_MAX), dtype=torch.int64, device=dev)
-        # SAMPLE_SOURCE = true: component of every observation, uint8 [B][N][F] (Sample.source)
-        self.source = None
+        # SAMPLE_SOURCE = true: component of every observation (Sample.source), kept on the device
+        # by POSITION, uint8 [B][F][Np] (include/sbz.h source_pm): the layout the likelihood's
+        # source branch reads in place and the sampler updates; `source` gives it by site
+        self.source_pm = None
         if source is not None:
             src = np.ascontiguousarray(source, np.uint8)
             if src.shape != (self.B, engine.n_sites, engine.n_features):
                 raise ValueError(f"source: expected {(self.B, engine.n_sites, engine.n_features)}, "
                                  f"got {src.shape}")
-            self.source = torch.as_tensor(src, device=dev)
+            self.source_pm = torch.as_tensor(engine.sources_to_positions(src), device=dev)
         self.counter = torch.zeros(self.B, dtype=torch.int64, device=dev)
         # the kernels trust the index bytes (include/sbz.h): range-check them once here, on the
         # stream that produced the tensors
         engine.set_stream(torch.cuda.current_stream(dev).cuda_stream)
         engine.check_indices_device(self.B, self.zone_of_site.data_ptr(),
-                                    self.source.data_ptr() if self.source is not None else 0)
+                                    self.source_pm.data_ptr() if self.source_pm is not None else 0,
+                                    source_pm=True)
         self.refresh_ll()
+
+    @property
+    def source(self):
+        """The sources by site, uint8 [B][N][F] (a device tensor computed from source_pm)."""
+        if self.source_pm is None:
+            return None
+        pos = _torch().as_tensor(self.engine.position_of_site, device=self.source_pm.device)
+        return self.source_pm[:, :, pos].transpose(1, 2).contiguous()
+
+    def source_of(self, i):
+        """Chain i's sources by site, uint8 [N][F] (device tensor)."""
+        pos = _torch().as_tensor(self.engine.position_of_site, device=self.source_pm.device)
+        return self.source_pm[i][:, pos].t().contiguous()
 
     def refresh_ll(self):
         """Recompute every chain's log-likelihood from scratch (the likelihood kernel; the source
@@ -103,15 +119,16 @@ class ChainState:
         eng.loglik_device(self.B, self.zone_of_site.data_ptr(), self.w.data_ptr(),
                           self.p_global.data_ptr(), self.p_zones.data_ptr(),
                           self.p_fam.data_ptr() if self.p_fam is not None else 0,
-                          self.source.data_ptr() if self.source is not None else 0,
-                          self.ll.data_ptr(), validate=False)  # checked at construction
+                          self.source_pm.data_ptr() if self.source_pm is not None else 0,
+                          self.ll.data_ptr(), validate=False,  # checked at construction
+                          source_pm=True)
         return self.ll
 
     def to_numpy(self):
         out = {"zone_of_site": self.zone_of_site.cpu().numpy(), "w": self.w.cpu().numpy(),
                "p_global": self.p_global.cpu().numpy(), "p_zones": self.p_zones.cpu().numpy(),
                "ll": self.ll.cpu().numpy(), "prior": self.prior.cpu().numpy()}
-        if self.source is not None:
+        if self.source_pm is not None:
             out["source"] = self.source.cpu().numpy()
         if self.p_fam is not None:
             out["p_fam"] = self.p_fam.cpu().numpy()
@@ -220,9 +237,10 @@ class Sampler:
         ch.ll = state.ll.data_ptr()
         ch.prior = state.prior.data_ptr()
         if self.sample_source:
-            if state.source is None:
+            if state.source_pm is None:
                 raise ValueError("SAMPLE_SOURCE sampler needs chains with sources (ChainState(source=...))")
-            ch.source = state.source.data_ptr()
+            ch.source = state.source_pm.data_ptr()
+            ch.source_layout = SBZ_SOURCE_BY_POSITION
         if alias is not None:  # (pending [B] int32, p_global, p_zones, p_fam) device tensors
             pend, apg, apz, apf = alias
             ch.alias_pending = pend.data_ptr()

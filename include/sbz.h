@@ -32,6 +32,10 @@
  *   p_zones      double [B][Z][F][S]                                       (Sample.p_zones)
  *   p_fam        double [B][Fam][F][S] or NULL without inheritance         (Sample.p_families)
  *   source       uint8  [B][N][F]     component index per cell, or NULL   (Sample.source one-hot -> index)
+ *   source_pm    uint8  [B][F][Np]    the same by POSITION: row f = feature f, column p = site
+ *                                     positions[p] of the context's site order (sbz_site_positions;
+ *                                     Np >= N, columns p >= N are padding and never read).  The
+ *                                     layout the kernels read in place; the sampler keeps it.
  */
 #ifndef SBZ_H
 #define SBZ_H
@@ -54,6 +58,11 @@ enum sbz_status {
 
 enum sbz_flags {
     SBZ_INHERITANCE = 1, /* model families: C = 3 components (Model.inheritance, model.py:45) */
+};
+
+enum sbz_source_layout {
+    SBZ_SOURCE_BY_SITE = 0,     /* [B][N][F], the reference's Sample.source order */
+    SBZ_SOURCE_BY_POSITION = 1, /* [B][F][Np] in the context's site order (source_pm above) */
 };
 
 typedef struct sbz_dims {
@@ -89,6 +98,39 @@ const char *sbz_last_error(const sbz_ctx *ctx);
 int sbz_set_stream(sbz_ctx *ctx, void *hip_stream);
 int sbz_synchronize(sbz_ctx *ctx);
 
+/* Tuning options of a context.  Every default is the production choice; nothing is read from the
+ * environment.  No reference counterpart (the reference has no device code).
+ *   SBZ_OPT_LIK_TASKS_PER_CU  likelihood single-wave tasks per CU and launch; 0 (default) = by
+ *                             shape: 4 when N <= 256, else the kernel's occupancy
+ *   SBZ_OPT_LIK_BANKED        1 (default): the banked table layout of the dense mixture kernel where
+ *                             it applies (S + 1 <= 16); 0: the packed [class][x] layout
+ *   SBZ_OPT_SRC_TABLE         1 (default): source branch on the table kernel where it applies;
+ *                             0: the per-cell kernel
+ *   SBZ_OPT_SRC_WAVES         source-mode sampler waves per chain: 0 (default) = 8, or 1, 4, 8
+ *   SBZ_OPT_SRC_HBM           1: the source-mode sampler keeps the sources in HBM even when they
+ *                             fit LDS (default 0: LDS when they fit)
+ *   SBZ_OPT_SRC_STAGE         1 (default): the source-mode sampler stages parameters in LDS where
+ *                             they fit; 0: its passes read them from L2
+ *   SBZ_OPT_MH_LOOKAHEAD      sampler with Philox draws: parameter proposals planned ahead per
+ *                             batch, 1..24 (default 24; 1 = none; trajectories do not depend on it)
+ * SBZ_EINVAL for an unknown option or a value out of range. */
+enum sbz_option {
+    SBZ_OPT_LIK_TASKS_PER_CU = 1,
+    SBZ_OPT_LIK_BANKED = 2,
+    SBZ_OPT_SRC_TABLE = 3,
+    SBZ_OPT_SRC_WAVES = 4,
+    SBZ_OPT_SRC_HBM = 5,
+    SBZ_OPT_SRC_STAGE = 6,
+    SBZ_OPT_MH_LOOKAHEAD = 7,
+};
+int sbz_set_option(sbz_ctx *ctx, int32_t option, int64_t value);
+int sbz_get_option(const sbz_ctx *ctx, int32_t option, int64_t *value);
+
+/* The context's site order: positions[p] = site at position p for p < N, -1 for the padding
+ * positions N <= p < Np (sites sorted stably by family, so that neighbouring lanes read the same
+ * table rows).  Returns Np (> 0), or a negative code; `positions` (int32[Np]) may be NULL. */
+int sbz_site_positions(const sbz_ctx *ctx, int32_t *positions);
+
 /*
  * Full log-likelihood of B chains, host buffers (PCIe copies included; blocks until done).
  * source == NULL: mixture branch  sum_{s,f} log sum_c w_norm*lh      (model.py:174-176)
@@ -108,12 +150,27 @@ int sbz_loglik_batch_device(sbz_ctx *ctx, int B, const uint8_t *zone_of_site, co
                             const double *p_global, const double *p_zones, const double *p_fam,
                             const uint8_t *source, double *out_ll);
 
+/* Same, with the sources by position (source_pm [B][F][Np], see Layouts): read in place, as the
+ * source-mode sampler keeps them (sbz_chains.source_layout = SBZ_SOURCE_BY_POSITION).  The
+ * reference's combine_lh source branch (model.py:177-184) on the sampler's own state. */
+int sbz_loglik_batch_device_pm(sbz_ctx *ctx, int B, const uint8_t *zone_of_site, const double *w,
+                               const double *p_global, const double *p_zones, const double *p_fam,
+                               const uint8_t *source_pm, double *out_ll);
+
+/* Convert B chains' sources between the layouts (device arrays, asynchronous on ctx's stream):
+ * to_positions = 1: src [B][N][F] -> dst [B][F][Np] (padding columns 0); 0: the reverse. */
+int sbz_source_layout_device(sbz_ctx *ctx, int B, const uint8_t *src, uint8_t *dst,
+                             int32_t to_positions);
+
 /* Validate device index arrays (zone_of_site [B][N]: < n_zones or SBZ_NONE; source
  * [B][N][F] or NULL: < C) with one kernel pass; synchronises ctx's stream.  SBZ_EINVAL with
  * a message naming the first offending array, SBZ_OK otherwise.  No reference counterpart:
  * the reference's arrays are host numpy arrays whose shapes/values it builds itself. */
 int sbz_check_indices_device(sbz_ctx *ctx, int B, const uint8_t *zone_of_site,
                              const uint8_t *source);
+/* Same for sources by position (source_pm [B][F][Np]; padding columns are not checked). */
+int sbz_check_indices_device_pm(sbz_ctx *ctx, int B, const uint8_t *zone_of_site,
+                                const uint8_t *source_pm);
 
 /* Device memory helpers (so a host without torch can stage device buffers). */
 int sbz_device_alloc(sbz_ctx *ctx, uint64_t bytes, void **out);
@@ -187,8 +244,9 @@ typedef struct sbz_chains {
     uint8_t *trace_zos;               /* [B][n_steps][N] or NULL (tests) */
     double *prior;                    /* [B] in/out: the chain's log prior (sbz_set_priors), or NULL
                                          when every prior term is 0 */
-    uint8_t *source;                  /* [B][N][F] in/out (sample_source): component of each
-                                         observation, 0 global, 1 zone, 2 family (Sample.source) */
+    uint8_t *source;                  /* in/out (sample_source): component of each observation,
+                                         0 global, 1 zone, 2 family (Sample.source), in the layout
+                                         source_layout names */
     /* sample_source only: the reference's Gibbs operators on p_global / p_zones / p_families
      * change the chain's Sample in place (zone_sampling.py:333-400), so the parameter arrays of a
      * logged sample (mcmc_generative.py:353-367 keeps references) go on changing until an
@@ -197,6 +255,9 @@ typedef struct sbz_chains {
      * p_* into alias_* and clears the flag. */
     int32_t *alias_pending;           /* [B] in/out, or NULL */
     double *alias_p_global, *alias_p_zones, *alias_p_fam;  /* [B][...] as p_global / p_zones / p_fam */
+    int32_t source_layout;            /* sbz_source_layout of `source`: SBZ_SOURCE_BY_SITE [B][N][F]
+                                         (0) or SBZ_SOURCE_BY_POSITION [B][F][Np] (the layout the
+                                         likelihood reads in place, sbz_loglik_batch_device_pm) */
 } sbz_chains;
 
 /* Sampler-only data: applicable states (uint8 [F][S], data.states) and the site network as CSR

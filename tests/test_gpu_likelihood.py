@@ -16,12 +16,31 @@ REL_TOL = 1e-9
 CASES = golden_cases()
 
 
-def _engine(d, device=0):
+def _engine(d, device=0, options=None):
     from contact_zones_amd.likelihood import LikelihoodEngine
     inh = bool(d["inheritance"])
     Fam = d["p_fam"].shape[1] if inh else 0
     return LikelihoodEngine(d["obs"], d["fam_of_site"], d["p_global"].shape[2],
-                            d["p_zones"].shape[1], Fam, inh, device)
+                            d["p_zones"].shape[1], Fam, inh, device, options=options)
+
+
+def _loglik(eng, kernel, zos, w, pg, pz, pf, src):
+    """Host entry (sbz_loglik_batch, sources by site), or for kernel 'pm' the device entry with the
+    sources by position (sbz_loglik_batch_device_pm: the layout the sampler keeps, read in place)."""
+    if kernel != "pm" or src is None:
+        return eng.loglik(zos, w, pg, pz, pf, src)
+    import torch
+    dev = torch.device("cuda:0")
+    B = zos.shape[0]
+    t = [torch.from_numpy(np.ascontiguousarray(v)).to(dev) if v is not None else None
+         for v in (zos, w, pg, pz, pf, eng.sources_to_positions(src))]
+    out = torch.empty(B, dtype=torch.float64, device=dev)
+    eng.set_stream(torch.cuda.current_stream().cuda_stream)
+    eng.loglik_device(B, *[x.data_ptr() if x is not None else 0 for x in t], out.data_ptr(),
+                      source_pm=True)
+    torch.cuda.synchronize()
+    assert eng.last_kernels() in ("lik_source_rc_kernel", "lik_source_generic_kernel")
+    return out.cpu().numpy()
 
 
 def _assert_close(got, ref, tol=REL_TOL):
@@ -35,18 +54,20 @@ def _assert_close(got, ref, tol=REL_TOL):
 
 
 # Kernel paths: the dense mixture kernel with its banked table layout (the default where
-# S + 1 <= 16) and with the packed [class][x] layout (SBZ_LIK_BANKED=0, the layout of every
-# larger S); the source branch on the row-code table kernel (default) and on the generic per-cell
-# kernel (SBZ_SRC_RC=0, the path of shapes the table kernel does not take).  Both variables are
-# read when a context opens.
-MODES = [("mixture", "dense"), ("mixture", "packed"), ("source", "rc"), ("source", "generic")]
+# S + 1 <= 16) and with the packed [class][x] layout (option lik_banked = 0, the layout of every
+# larger S); the source branch on the table kernel (default) with the sources by site (transposed
+# to positions first) and by position (read in place, 'pm'), and on the generic per-cell kernel
+# (option src_table = 0, the path of shapes the table kernel does not take).
+MODES = [("mixture", "dense"), ("mixture", "packed"), ("source", "rc"), ("source", "pm"),
+         ("source", "generic")]
+
+
+def _options(kernel):
+    return {"lik_banked": 0 if kernel == "packed" else 1, "src_table": 0 if kernel == "generic" else 1}
 
 
 @pytest.fixture
-def lik_kernel(request, monkeypatch):
-    kernel = request.param
-    monkeypatch.setenv("SBZ_LIK_BANKED", "0" if kernel == "packed" else "1")
-    monkeypatch.setenv("SBZ_SRC_RC", "0" if kernel == "generic" else "1")
+def lik_kernel(request):
     return request.param
 
 
@@ -54,9 +75,9 @@ def lik_kernel(request, monkeypatch):
 @pytest.mark.parametrize("mode,lik_kernel", MODES, indirect=["lik_kernel"])
 def test_golden(gpu_available, case, mode, lik_kernel):
     d = load_golden(case)
-    eng = _engine(d)
+    eng = _engine(d, options=_options(lik_kernel))
     src = d["source"] if mode == "source" else None
-    got = eng.loglik(d["zone_of_site"], d["w"], d["p_global"], d["p_zones"], d.get("p_fam"), src)
+    got = _loglik(eng, lik_kernel, d["zone_of_site"], d["w"], d["p_global"], d["p_zones"], d.get("p_fam"), src)
     _assert_close(got, d["ll_" + mode])
 
 
@@ -111,9 +132,9 @@ def test_random_vs_c_oracle(gpu_available, shape, mode, lik_kernel):
     N, F, S, Z, Fam, B, inh, zs = shape
     rng = np.random.default_rng(hash(shape) % 2**32)
     obs, fam, zos, w, pg, pz, pf, src = _random_batch(rng, N, F, S, Z, Fam, B, inh, zs)
-    eng = LikelihoodEngine(obs, fam, S, Z, Fam, inh)
+    eng = LikelihoodEngine(obs, fam, S, Z, Fam, inh, options=_options(lik_kernel))
     s = src if mode == "source" else None
-    got = eng.loglik(zos, w, pg, pz, pf, s)
+    got = _loglik(eng, lik_kernel, zos, w, pg, pz, pf, s)
     ref = oracle_c.loglik_batch(obs, fam, zos, w, pg, pz, pf, source=s, inheritance=inh)
     _assert_close(got, ref, tol=1e-12)
 
@@ -182,14 +203,13 @@ def test_drop_in_likelihood_interface(gpu_available):
 
 @pytest.mark.parametrize("banked", ["1", "0"])
 @pytest.mark.parametrize("shape", [(1500, 40, 6, 4, 3, 9), (2000, 64, 10, 8, 4, 9), (300, 21, 15, 3, 2, 9)])
-def test_dense_edge_paths(gpu_available, monkeypatch, banked, shape):
+def test_dense_edge_paths(gpu_available, banked, shape):
     """Dense kernel (banked and packed table layouts) on inputs that leave the fast path: zero
     cells (finite when another component covers them, -inf otherwise), tiny parameters whose
     products underflow (the task re-runs with per-factor renormalisation), parameters above 1
     and denormal parameters (per-feature renormalisation)."""
     from contact_zones_amd.likelihood import LikelihoodEngine
     from oracle import oracle_c
-    monkeypatch.setenv("SBZ_LIK_BANKED", banked)
     N, F, S, Z, Fam, B = shape
     rng = np.random.default_rng(N + F)
     obs, fam, zos, w, pg, pz, pf, _ = _random_batch(rng, N, F, S, Z, Fam, B, True, N // (3 * Z))
@@ -205,7 +225,7 @@ def test_dense_edge_paths(gpu_available, monkeypatch, banked, shape):
     pz[6, :, :, 2] = 0.0                 # zero zoned cells
     pg[7, 3:9] *= 7.5                    # above 1 -> per-feature renormalisation
     pf[8, :, 5, :] = 4e-320              # denormal family parameters
-    eng = LikelihoodEngine(obs, fam, S, Z, Fam, True)
+    eng = LikelihoodEngine(obs, fam, S, Z, Fam, True, options={"lik_banked": int(banked)})
     got = eng.loglik(zos, w, pg, pz, pf)
     ref = oracle_c.loglik_batch(obs, fam, zos, w, pg, pz, pf, inheritance=True)
     assert np.isfinite(ref[3]) and ref[4] == -np.inf
@@ -213,15 +233,14 @@ def test_dense_edge_paths(gpu_available, monkeypatch, banked, shape):
     assert eng.lds_bytes(False) > 0
 
 
-@pytest.mark.parametrize("rc", ["1", "0"])
+@pytest.mark.parametrize("rc", ["rc", "pm", "generic"])
 @pytest.mark.parametrize("shape", [(2000, 64, 10, 8, 4, 8), (300, 21, 15, 3, 2, 8), (120, 30, 4, 0, 3, 8)])
-def test_source_edge_paths(gpu_available, monkeypatch, rc, shape):
+def test_source_edge_paths(gpu_available, rc, shape):
     """Source branch (row-code table kernel and the generic per-cell kernel): a selected component
     of weight 0 (-inf, model.py:181-182), tiny parameters (products underflow -> task re-run),
     parameters above 1, denormal family parameters, sources past the site's components."""
     from contact_zones_amd.likelihood import LikelihoodEngine
     from oracle import oracle_c
-    monkeypatch.setenv("SBZ_SRC_RC", rc)
     N, F, S, Z, Fam, B = shape
     rng = np.random.default_rng(N * 3 + F)
     obs, fam, zos, w, pg, pz, pf, src = _random_batch(rng, N, F, S, Z, Fam, B, True, max(1, N // (3 * max(Z, 1))))
@@ -239,8 +258,8 @@ def test_source_edge_paths(gpu_available, monkeypatch, rc, shape):
     src[7, :, 0] = 0                    # every site from the global component at feature 0
     s2 = int(np.flatnonzero(fam == 255)[0])
     src[2, s2, 1] = 2                   # a site without family selects the family component
-    eng = LikelihoodEngine(obs, fam, S, Z, Fam, True)
-    got = eng.loglik(zos, w, pg, pz, pf, src)
+    eng = LikelihoodEngine(obs, fam, S, Z, Fam, True, options=_options(rc))
+    got = _loglik(eng, rc, zos, w, pg, pz, pf, src)
     ref = oracle_c.loglik_batch(obs, fam, zos, w, pg, pz, pf, source=src, inheritance=True)
     assert ref[3] == -np.inf and ref[2] == -np.inf
     _assert_close(got, ref, tol=1e-12)
@@ -335,11 +354,11 @@ def test_device_index_validation(gpu_available):
     np.testing.assert_array_equal(out.cpu().numpy(), eng.loglik(zos, w, pg, pz, pf))
 
 
-@pytest.mark.parametrize("rc", ["1", "0"])
+@pytest.mark.parametrize("rc", ["rc", "pm", "generic"])
 @pytest.mark.parametrize("S,Z,Fam,inh", [(15, 3, 3, True), (16, 3, 3, True), (17, 4, 3, True),
                                          (20, 5, 5, True), (31, 2, 0, False), (32, 2, 0, False),
                                          (40, 2, 0, False)])
-def test_source_wide_state_tables(gpu_available, monkeypatch, rc, S, Z, Fam, inh):
+def test_source_wide_state_tables(gpu_available, rc, S, Z, Fam, inh):
     """Source branch with many states: S + 1 > 16 leaves fewer than 4 lane groups of S + 1 lanes
     in a wave, so the row-code kernel writes its 4 T0 rows (and the 4 zero rows) by a strided
     loop over the groups; every (class, state) entry must be written (a missed T0 row would read
@@ -347,27 +366,25 @@ def test_source_wide_state_tables(gpu_available, monkeypatch, rc, S, Z, Fam, inh
     (zoned / unzoned sites with and without a family, every component selected)."""
     from contact_zones_amd.likelihood import LikelihoodEngine
     from oracle import oracle_c
-    monkeypatch.setenv("SBZ_SRC_RC", rc)
     N, F, B = 300, 23, 6
     rng = np.random.default_rng(1000 * S + Z)
     obs, fam, zos, w, pg, pz, pf, src = _random_batch(rng, N, F, S, Z, Fam, B, inh, 20, nofam=0.3)
     if not inh:
         src = np.minimum(src, 1).astype(np.uint8)
-    eng = LikelihoodEngine(obs, fam, S, Z, Fam, inh)
-    got = eng.loglik(zos, w, pg, pz, pf, src)
+    eng = LikelihoodEngine(obs, fam, S, Z, Fam, inh, options=_options(rc))
+    got = _loglik(eng, rc, zos, w, pg, pz, pf, src)
     ref = oracle_c.loglik_batch(obs, fam, zos, w, pg, pz, pf, source=src, inheritance=inh)
     assert np.all(np.isfinite(ref))
     _assert_close(got, ref, tol=1e-12)
 
 
-@pytest.mark.parametrize("rc", ["1", "0"])
-def test_source_zero_weight_beside_nan(gpu_available, monkeypatch, rc):
+@pytest.mark.parametrize("rc", ["rc", "pm", "generic"])
+def test_source_zero_weight_beside_nan(gpu_available, rc):
     """model.py:181-182: a selected weight of exactly 0 gives -inf even when other selected
     weights are NaN (0 / 0); without a zero selected weight the NaN cells give NaN.  The chains
     are split over several tasks, so the zero and the NaN cells land in different tasks."""
     from contact_zones_amd.likelihood import LikelihoodEngine
     from oracle import oracle_c
-    monkeypatch.setenv("SBZ_SRC_RC", rc)
     N, F, S, Z, Fam, B = 700, 90, 5, 3, 2, 4
     rng = np.random.default_rng(99)
     obs, fam, zos, w, pg, pz, pf, src = _random_batch(rng, N, F, S, Z, Fam, B, True, 40)
@@ -380,14 +397,14 @@ def test_source_zero_weight_beside_nan(gpu_available, monkeypatch, rc):
     s2 = int(np.flatnonzero(zos[2] == 255)[0])
     src[2, s2, 80] = 0
     w[3, 3] = [0.2, 0.5, 0.3]            # chain 3: no NaN, no zero weight -> finite
-    eng = LikelihoodEngine(obs, fam, S, Z, Fam, True)
+    eng = LikelihoodEngine(obs, fam, S, Z, Fam, True, options=_options(rc))
     with np.errstate(invalid="ignore", divide="ignore"):
         ref = oracle_c.loglik_batch(obs, fam, zos, w, pg, pz, pf, source=src, inheritance=True)
     assert ref[0] == -np.inf and np.isnan(ref[1]) and ref[2] == -np.inf and np.isfinite(ref[3])
     for _ in range(2):  # the per-chain flag is re-armed between launches
-        got = eng.loglik(zos, w, pg, pz, pf, src)
+        got = _loglik(eng, rc, zos, w, pg, pz, pf, src)
         _assert_close(got, ref, tol=1e-12)
-    one = eng.loglik(zos[1:2], w[1:2], pg[1:2], pz[1:2], pf[1:2], src[1:2])
+    one = _loglik(eng, rc, zos[1:2], w[1:2], pg[1:2], pz[1:2], pf[1:2], src[1:2])
     assert np.isnan(one[0])
 
 
@@ -395,17 +412,16 @@ def test_source_zero_weight_beside_nan(gpu_available, monkeypatch, rc):
 @pytest.mark.parametrize("mode", ["mixture", "source"])
 def test_bench_launch_parity(gpu_available, B, mode):
     """The exact launch bench.py times (BASELINE configs[4]: 2000 sites x 500 features x 10
-    states, 8 zones of 50 sites, 4 families, device pointers, validate=False) at the bench's
-    chains per GPU (256) and at 2048 chains on one GPU: the task split W depends on B, so these
-    are the long-task shapes (12 tasks of ~42 features at B = 256, 2 of 250 at B = 2048) no
-    smaller case reaches.  First, last and 8 sampled chains against the C oracle."""
+    states, 8 zones of 50 sites, 4 families, device pointers, validate=False; the source branch
+    with the sources by position, read in place) at the bench's chains per GPU (256) and at 2048
+    chains on one GPU: the task split W depends on B, so these are the long-task shapes (12 tasks
+    of ~42 features at B = 256, 2 of 250 at B = 2048) no smaller case reaches.  First, last and 8
+    sampled chains against the C oracle."""
     import argparse
     import torch
     import bench
     from contact_zones_amd.likelihood import LikelihoodEngine
     from oracle import oracle_c
-    if mode == "source" and B > 256:
-        pytest.skip("source sweep at the bench's 256 chains (2048 x 1 MB of sources)")
     args = argparse.Namespace(sites=2000, features=500, states=10, zones=8, families=4,
                               zone_size=50, mode=mode, seed=5)
     obs, fam = bench.make_shared(args, np.random.default_rng(args.seed))
@@ -413,20 +429,82 @@ def test_bench_launch_parity(gpu_available, B, mode):
     dev = torch.device("cuda:0")
     gen = torch.Generator(device=dev)
     gen.manual_seed(1234 + B)
-    c = bench.make_chains_torch(args, B, gen, dev)
     eng = LikelihoodEngine(obs, fam, 10, 8, 4, True)
     eng.set_stream(torch.cuda.current_stream().cuda_stream)
+    c = bench.make_chains_torch(args, B, gen, dev, eng)
     out = torch.empty(B, dtype=torch.float64, device=dev)
-    src = c["src"]
+    src = c["src_pm"]
     for _ in range(2):  # twice: the second launch runs on re-armed tickets
         eng.loglik_device(B, c["zos"].data_ptr(), c["w"].data_ptr(), c["pg"].data_ptr(),
                           c["pz"].data_ptr(), c["pf"].data_ptr(),
-                          src.data_ptr() if src is not None else 0, out.data_ptr(), validate=False)
+                          src.data_ptr() if src is not None else 0, out.data_ptr(), validate=False,
+                          source_pm=True)
     torch.cuda.synchronize()
+    if mode == "source":
+        assert eng.last_kernels() == "lik_source_rc_kernel"
     got = out.cpu().numpy()
     assert np.all(np.isfinite(got))
     pick = sorted({0, B - 1, *np.random.default_rng(B).choice(B, 8, replace=False).tolist()})
     h = {k: (v[pick].cpu().numpy() if v is not None else None) for k, v in c.items()}
+    src_rm = eng.sources_from_positions(h["src_pm"]) if h["src_pm"] is not None else None
     ref = oracle_c.loglik_batch(obs, fam, h["zos"], h["w"], h["pg"], h["pz"], h["pf"],
-                                source=h["src"], inheritance=True)
+                                source=src_rm, inheritance=True)
     _assert_close(got[pick], ref, tol=1e-12)
+
+
+def test_source_layouts(gpu_available):
+    """The two source layouts (include/sbz.h): sbz_site_positions is the stable family sort,
+    sbz_source_layout_device transposes [B][N][F] <-> [B][F][Np] exactly as the host restatement
+    (padding columns 0) and back to the identity, and sbz_check_indices_device_pm refuses a
+    component >= C at a site position but not in the padding columns."""
+    import torch
+    from contact_zones_amd._lib import SbzError
+    from contact_zones_amd.likelihood import LikelihoodEngine
+    rng = np.random.default_rng(17)
+    N, F, S, Z, Fam, B = 300, 45, 4, 2, 3, 5   # F not a multiple of 4: the byte path
+    obs, fam, zos, w, pg, pz, pf, src = _random_batch(rng, N, F, S, Z, Fam, B, True, 10)
+    eng = LikelihoodEngine(obs, fam, S, Z, Fam, True)
+    fc = np.where(fam == 255, 0, fam.astype(int) + 1)
+    np.testing.assert_array_equal(eng.positions[:N], np.argsort(fc, kind="stable"))
+    assert np.all(eng.positions[N:] == -1) and eng.n_positions % 256 == 0
+    dev = torch.device("cuda:0")
+    eng.set_stream(torch.cuda.current_stream().cuda_stream)
+    t_src = torch.from_numpy(src).to(dev)
+    pm = torch.full((B, F, eng.n_positions), 7, dtype=torch.uint8, device=dev)
+    eng.source_layout_device(B, t_src.data_ptr(), pm.data_ptr(), True)
+    back = torch.empty_like(t_src)
+    eng.source_layout_device(B, pm.data_ptr(), back.data_ptr(), False)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(pm.cpu().numpy(), eng.sources_to_positions(src))
+    np.testing.assert_array_equal(back.cpu().numpy(), src)
+    np.testing.assert_array_equal(eng.sources_from_positions(pm.cpu().numpy()), src)
+    t_zos = torch.from_numpy(zos).to(dev)
+    pm[:, :, N:] = 9  # padding: never read, never checked
+    eng.check_indices_device(B, t_zos.data_ptr(), pm.data_ptr(), source_pm=True)
+    pm[2, 7, N - 1] = 3
+    with pytest.raises(SbzError, match="source"):
+        eng.check_indices_device(B, t_zos.data_ptr(), pm.data_ptr(), source_pm=True)
+
+
+def test_options(gpu_available):
+    """Context options (sbz_set_option) replace the environment: defaults, round trip, range
+    checks, and the likelihood unchanged by the table layout / tasks-per-CU choices."""
+    from contact_zones_amd._lib import SbzError
+    from contact_zones_amd.likelihood import LikelihoodEngine
+    rng = np.random.default_rng(23)
+    obs, fam, zos, w, pg, pz, pf, _ = _random_batch(rng, 200, 100, 5, 2, 2, 64, True, 25)
+    eng = LikelihoodEngine(obs, fam, 5, 2, 2, True)
+    assert {k: eng.get_option(k) for k in ("lik_tasks_per_cu", "lik_banked", "src_table", "src_waves",
+                                           "src_hbm", "src_stage", "mh_lookahead")} == \
+        {"lik_tasks_per_cu": 0, "lik_banked": 1, "src_table": 1, "src_waves": 0, "src_hbm": 0,
+         "src_stage": 1, "mh_lookahead": 24}
+    ref = eng.loglik(zos, w, pg, pz, pf)
+    for tpc in (1, 2, 4, 12):
+        eng.set_option("lik_tasks_per_cu", tpc)
+        _assert_close(eng.loglik(zos, w, pg, pz, pf), ref, tol=1e-14)
+    for name, bad in (("lik_tasks_per_cu", -1), ("lik_banked", 2), ("src_waves", 3), ("mh_lookahead", 0),
+                      ("mh_lookahead", 25)):
+        with pytest.raises(SbzError):
+            eng.set_option(name, bad)
+    with pytest.raises(ValueError):
+        eng.set_option("no_such_option", 1)

@@ -13,14 +13,14 @@ MH_CASES = mh_cases(source=False)  # source mode: test_gpu_source.py
 REL_TOL = 1e-9
 
 
-def _setup(fx):
+def _setup(fx, options=None):
     from contact_zones_amd.likelihood import LikelihoodEngine
     from contact_zones_amd.sampler import ChainState, Sampler
     inh = bool(fx["inheritance"])
     S = fx["states"].shape[1]
     Z = int(fx["n_zones"])
     Fam = fx["init_p_fam"].shape[1] if inh else 0
-    eng = LikelihoodEngine(fx["obs"], fx["fam_of_site"], S, Z, Fam, inh)
+    eng = LikelihoodEngine(fx["obs"], fx["fam_of_site"], S, Z, Fam, inh, options=options)
     from contact_zones_amd.priors import PriorSpec
     priors = prior_spec(fx)
     smp = Sampler(eng, fx["states"], fx["adj_indptr"], fx["adj_indices"], fx["op_probs"],
@@ -129,7 +129,7 @@ def test_philox_carried_prior_matches_full_prior(gpu_available):
     assert np.any(s["prior"] != fx["init_prior"])  # the prior moved
 
 
-def _synthetic_chains(N, F, S, Z, Fam, inh, B):
+def _synthetic_chains(N, F, S, Z, Fam, inh, B, options=None):
     """A Delaunay network of random sites, random observations, reference-initialised zones
     (InitialSamples) and random parameters: sampler, chain state and likelihood engine."""
     import random
@@ -157,7 +157,7 @@ def _synthetic_chains(N, F, S, Z, Fam, inh, B):
     pg = rng.dirichlet(np.ones(S), size=(B, F))
     pz = rng.dirichlet(np.ones(S), size=(B, Z, F))
     pf = rng.dirichlet(np.ones(S), size=(B, Fam, F)) if inh else None
-    eng = LikelihoodEngine(obs, fam, S, Z, Fam, inh)
+    eng = LikelihoodEngine(obs, fam, S, Z, Fam, inh, options=options)
     ops = {"shrink_zone": 0.1, "grow_zone": 0.1, "swap_zone": 0.05, "alter_weights": 0.3,
            "alter_p_global": 0.15, "alter_p_zones": 0.2, "alter_p_families": 0.1 if inh and Fam else 0.0}
     smp = Sampler(eng, states, indptr, indices, ops, [15, 40, 20, 20], 3)
@@ -246,17 +246,16 @@ def test_host_form_philox_matches_device_form(gpu_available):
 
 
 @pytest.mark.parametrize("case", ["mh_small_priors", "mh_cfg1_sim_inh_z2", "mh_small_bounds"])
-def test_philox_planned_proposals_do_not_change_trajectories(gpu_available, monkeypatch, case):
-    """Philox mode plans the proposals of the next parameter moves in parallel lanes (SBZ_MH_LA
-    steps at a time) and recomputes a plan that an accepted move made stale: the trajectory
-    (operators, accepts, ll, final state, counters) is bit-identical to the one-step-at-a-time
-    path (SBZ_MH_LA = 1), over launches of different lengths."""
+def test_philox_planned_proposals_do_not_change_trajectories(gpu_available, case):
+    """Philox mode plans the proposals of the next parameter moves in parallel lanes (option
+    mh_lookahead steps at a time) and recomputes a plan that an accepted move made stale: the
+    trajectory (operators, accepts, ll, final state, counters) is bit-identical to the
+    one-step-at-a-time path (mh_lookahead = 1), over launches of different lengths."""
     import torch
     fx = load_golden(case)
     runs = []
-    for la in ("1", "24", "6"):
-        monkeypatch.setenv("SBZ_MH_LA", la)
-        eng, smp, st = _setup(fx)
+    for la in (1, 24, 6):
+        eng, smp, st = _setup(fx, {"mh_lookahead": la})
         outs = [smp.run(st, n, fx["max_size"], fx["p_grow_connected"], seed=4242, chain_id0=3, trace=True)
                 for n in (700, 5, 1301)]
         torch.cuda.synchronize()
@@ -274,15 +273,14 @@ def test_philox_planned_proposals_do_not_change_trajectories(gpu_available, monk
         np.testing.assert_array_equal(base[3], other[3])
 
 
-def test_planned_batches_cut_by_lds(gpu_available, monkeypatch):
+def test_planned_batches_cut_by_lds(gpu_available):
     """Wide parameter columns (S = 60, Z = 6, Fam = 4: 663 doubles per planned step) leave room
     in the 160 KiB for fewer than 24 planned steps (about 20 here): the host cuts the batch, and
     the trajectory stays bit-identical to the one-step-at-a-time path."""
     import torch
     runs = []
-    for la in ("1", "24"):
-        monkeypatch.setenv("SBZ_MH_LA", la)
-        smp, st = _synthetic_chains(300, 30, 60, 6, 4, True, 8)
+    for la in (1, 24):
+        smp, st = _synthetic_chains(300, 30, 60, 6, 4, True, 8, {"mh_lookahead": la})
         out = smp.run(st, 600, 40, 0.85, seed=9, trace=True)
         torch.cuda.synchronize()
         runs.append(({k: out[k].cpu().numpy() for k in ("op", "accept", "ll", "status")}, st.to_numpy()))

@@ -15,17 +15,15 @@ REL_TOL = 1e-9
 
 
 @pytest.fixture(params=["lds", "hbm", "lds-w1", "hbm-w4"])
-def src_home(request, monkeypatch):
-    """Where the sampler keeps the sources — LDS (when they fit) or HBM (SBZ_SRC_HBM=1, the path
-    every N x F too large for LDS takes) — and the waves per chain (default 8, or
-    SBZ_SRC_WAVES = 1 / 4); read when the context opens."""
+def src_home(request):
+    """Context options: where the sampler keeps the sources — LDS (when they fit) or HBM (option
+    src_hbm = 1, the path every N x F too large for LDS takes, walking the sources by position) —
+    and the waves per chain (default 8, or src_waves = 1 / 4)."""
     home, _, waves = request.param.partition("-w")
-    monkeypatch.setenv("SBZ_SRC_HBM", "1" if home == "hbm" else "0")
-    monkeypatch.setenv("SBZ_SRC_WAVES", waves or "0")
-    return request.param
+    return {"src_hbm": 1 if home == "hbm" else 0, "src_waves": int(waves or 0)}
 
 
-def _setup(fx):
+def _setup(fx, options=None):
     from contact_zones_amd.likelihood import LikelihoodEngine
     from contact_zones_amd.priors import PriorSpec
     from contact_zones_amd.sampler import ChainState, Sampler
@@ -33,7 +31,7 @@ def _setup(fx):
     S = fx["states"].shape[1]
     Z = int(fx["n_zones"])
     Fam = fx["init_p_fam"].shape[1] if inh else 0
-    eng = LikelihoodEngine(fx["obs"], fx["fam_of_site"], S, Z, Fam, inh)
+    eng = LikelihoodEngine(fx["obs"], fx["fam_of_site"], S, Z, Fam, inh, options=options)
     priors = prior_spec(fx)
     smp = Sampler(eng, fx["states"], fx["adj_indptr"], fx["adj_indices"], fx["op_probs"],
                   fx["precision"], int(fx["min_size"]), warmup=bool(fx["warmup"]), priors=priors,
@@ -60,7 +58,7 @@ def test_source_tape_replay_matches_reference(gpu_available, case, src_home):
     import torch
     fx = load_golden(case)
     inh = bool(fx["inheritance"])
-    eng, smp, st = _setup(fx)
+    eng, smp, st = _setup(fx, src_home)
     n_steps = fx["step_op"].shape[1]
     out = smp.run(st, n_steps, fx["max_size"], fx["p_grow_connected"], tape=fx["tape"],
                   tape_len=fx["tape_len"], trace=True, trace_zones=True)
@@ -110,7 +108,7 @@ def test_source_philox_chains_are_valid(gpu_available, src_home):
     import torch
     from contact_zones_amd.priors import PriorSpec
     fx = load_golden("mh_src_small")
-    eng, smp, st = _setup(fx)
+    eng, smp, st = _setup(fx, src_home)
     out = smp.run(st, 3000, fx["max_size"], fx["p_grow_connected"], seed=77)
     torch.cuda.synchronize()
     assert out["status"].cpu().numpy().tolist() == [0] * st.B
@@ -131,7 +129,7 @@ def test_source_philox_chains_are_valid(gpu_available, src_home):
                           int(fx["n_zones"]), bool(fx["inheritance"]))
     np.testing.assert_allclose(s["prior"], full, rtol=1e-12, atol=1e-12)
     assert st.accepted.sum().item() > 100
-    eng2, smp2, st2 = _setup(fx)
+    eng2, smp2, st2 = _setup(fx, src_home)
     smp2.run(st2, 3000, fx["max_size"], fx["p_grow_connected"], seed=77)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(st2.source.cpu().numpy(), src)
@@ -210,3 +208,33 @@ def test_source_sampler_lds_limit_fails_loudly(gpu_available):
     after = st.to_numpy()
     np.testing.assert_array_equal(after["zone_of_site"], before["zone_of_site"])
     np.testing.assert_array_equal(after["p_global"], before["p_global"])
+
+
+@pytest.mark.parametrize("home", ["lds", "hbm"])
+def test_source_host_form_replays_reference(gpu_available, home):
+    """sbz_mh_run with SAMPLE_SOURCE: the host form takes the sources BY SITE ([B][N][F], the
+    reference's order; the sampler copies them in and out of LDS, or transposes them to positions
+    around an HBM run), the device form (ChainState) keeps them BY POSITION.  Both replay the
+    reference's tape: operators, accepts, final sources and parameters bit for bit."""
+    from contact_zones_amd.sampler import run_host
+    fx = load_golden("mh_src_small")
+    inh = bool(fx["inheritance"])
+    eng, smp, st = _setup(fx, {"src_hbm": 1 if home == "hbm" else 0})
+    n_steps = fx["step_op"].shape[1]
+    host = {"zone_of_site": fx["init_zone_of_site"].copy(), "w": fx["init_w"].copy(),
+            "p_global": fx["init_p_global"].copy(), "p_zones": fx["init_p_zones"].copy(),
+            "p_fam": fx["init_p_fam"].copy() if inh else None, "source": fx["init_source"].copy(),
+            "prior": np.broadcast_to(np.asarray(fx["init_prior"], np.float64), (st.B,)).copy()}
+    tr = run_host(smp, host, n_steps, fx["max_size"], fx["p_grow_connected"], tape=fx["tape"],
+                  tape_len=fx["tape_len"], trace=True)
+    assert host["status"].tolist() == [0] * st.B
+    np.testing.assert_array_equal(tr["op"], fx["step_op"])
+    np.testing.assert_array_equal(tr["accept"].astype(bool), fx["step_accept"])
+    np.testing.assert_array_equal(host["source"], fx["step_source"][:, -1])
+    np.testing.assert_array_equal(host["w"], fx["final_w"])
+    np.testing.assert_array_equal(host["p_zones"], fx["final_p_zones"])
+    assert np.max(np.abs(tr["ll"] - fx["step_ll"]) / np.abs(fx["step_ll"])) <= REL_TOL
+    smp.run(st, n_steps, fx["max_size"], fx["p_grow_connected"], tape=fx["tape"], tape_len=fx["tape_len"])
+    dev = st.to_numpy()
+    for k in ("zone_of_site", "w", "p_global", "p_zones", "source") + (("p_fam",) if inh else ()):
+        np.testing.assert_array_equal(host[k], dev[k], err_msg=k)
