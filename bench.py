@@ -399,6 +399,8 @@ def sampler_leg(args, eng, obs, fam, dev, rank, world, stream):
         "ess_trace": f"Tracer ESS (lag cap 2000 samples) of the log-likelihood samples the reference "
                      f"logs: every {sps}-th step of {K} (N_SAMPLES 1000, mcmc_generative.py:205-218)",
         "ess_capped_chains": int(n_capped),
+        "ess_capped_note": "chains whose autocovariance pair sums stayed positive up to the lag cap "
+                           "(max_lag or the logged trace's length): their ESS is an upper bound",
         "ess_full_trace_per_sec": ess_full_tot / wall_max,
         "ess_full_trace_per_chain_mean": ess_full_tot / (B * world),
         "chains": B * world,

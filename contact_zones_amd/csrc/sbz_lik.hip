@@ -104,9 +104,12 @@ __device__ __forceinline__ void wave_lds_sync() {
 // `zw` (source branch): the task saw a selected normalised weight of exactly 0.  The reference
 // then returns -inf whatever the other cells hold (model.py:181-182, NaN cells included), so the
 // flag travels beside the partials (zflag[b], same sc1 hand-off) and overrides the sum.
-__device__ __forceinline__ void finish_chain(const LikArgs &a, int b, double tot,
-                                             bool leader = threadIdx.x == 0, bool zw = false) {
-    // every lane of the wave calls this (wave-uniform control flow); lane 0 is the leader
+//
+// Contract: the workgroup is exactly one wave (every caller launches blockDim.x == WAVE) and all
+// 64 lanes call this in wave-uniform control flow: the partials are loaded and broadcast with
+// __shfl (ds_bpermute), which reads garbage from lanes that did not arrive.
+__device__ __forceinline__ void finish_chain(const LikArgs &a, int b, double tot, bool zw = false) {
+    const bool leader = threadIdx.x % WAVE == 0;
     if (a.W == 1) {
         if (leader) a.out[b] = zw ? -INFINITY : tot;
         return;
@@ -658,7 +661,7 @@ __global__ __launch_bounds__(WAVE) void lik_source_generic_kernel(LikArgs a) {
         }
     }
     const double tot = wave_sum(lsum);
-    finish_chain(a, b, tot, lane == 0, __ballot(zw != 0) != 0);
+    finish_chain(a, b, tot, __ballot(zw != 0) != 0);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -963,7 +966,7 @@ __global__ __launch_bounds__(WAVE, SBZ_SRC_RC_WAVES) void lik_source_rc_kernel(L
     }
     const double v = (log(m[0]) + log(m[1])) + (log(m[2]) + log(m[3])) + (double)e * LN2;
     const double tot = wave_sum(v);
-    finish_chain(a, b, tot, lane == 0, __ballot(zw != 0) != 0);
+    finish_chain(a, b, tot, __ballot(zw != 0) != 0);
 }
 
 // Source layout transposes between the reference layout [B][N][F] (site-major, row s = site s)

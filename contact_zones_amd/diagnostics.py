@@ -46,7 +46,9 @@ def ess(x, max_lag=2000, return_capped=False):
                 break
             var += 2.0 * pair
             lag += 2
-        capped[i] = lag >= lag_cap and lag_cap < n - 1
+        # the pair sums stayed positive up to the cap, whether the cap was max_lag or the trace
+        # length: the estimate is then limited by the window, an upper bound on the ESS
+        capped[i] = lag >= lag_cap
         out[i] = n * gi[0] / var
     if return_capped:
         return out.reshape(x.shape[:-1]), capped.reshape(x.shape[:-1])

@@ -53,3 +53,16 @@ def test_ess_batched_and_degenerate():
     assert np.isclose(e[1, 2], ess(x[1, 2]))
     assert ess(np.ones(50)) == 0.0
     assert ess(np.array([1.0])) == 0.0
+
+
+def test_ess_capped_flag():
+    """A trace whose pair sums stay positive up to the lag window is flagged (its ESS is then an
+    upper bound), whether the window is max_lag or the trace length; a white-noise trace is not."""
+    rng = np.random.default_rng(3)
+    iid = rng.normal(size=400)
+    walk = np.cumsum(rng.normal(size=400))  # unmixed: positive autocovariance over short lags
+    e, capped = ess(np.stack([iid, walk]), max_lag=50, return_capped=True)
+    assert capped.tolist() == [False, True]
+    # window = the trace length: a short, strongly correlated trace reaches it
+    _, capped = ess(np.array([0.0, 1.0, 2.0, 2.5, 2.0, 1.0]), max_lag=None, return_capped=True)
+    assert not bool(capped)  # the mean-centred pair sums turn negative before the end
