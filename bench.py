@@ -517,12 +517,17 @@ def source_sampler_leg(shape, B, K, burnin, seed, rank=0, world=1, device=0):
 EXPERIMENTS = os.path.join(ROOT, "tests", "golden", "io", "data", "experiments")  # the reference's data
 
 
-def real_data_leg(name, n_zones_list, B, K, burnin, seed, rank=0, world=1, device=0):
+def real_data_leg(name, n_zones_list, B, K, burnin, seed, rank=0, world=1, device=0, concurrent=False):
     """The reference's own experiment configs on their real data (experiments/<name>/config.json:
     features, counts priors, STEPS, PROPOSAL_PRECISION, MIN_M / MAX_M / M_INITIAL, SAMPLE_SOURCE
     default true), B chains per GPU from generate_initial_sample, K Philox MH steps after `burnin`,
     for each number of zones: steps/s and ESS/s of the log-likelihood traces (max wall over
-    ranks, ESS summed over ranks)."""
+    ranks, ESS summed over ranks).
+
+    concurrent: after the per-K runs (one at a time, as the reference's cli.py:71-84 sweeps K),
+    time the whole sweep once more with every K's run launched on a stream of its own, so the
+    K runs' B-chain launches share the GPU's CUs (B = 128 chains leave half of the 256 CUs idle
+    when run alone); reported as `sweep_concurrent` beside the sequential sum."""
     import random
     import numpy as np
     import torch
@@ -540,10 +545,12 @@ def real_data_leg(name, n_zones_list, B, K, burnin, seed, rank=0, world=1, devic
     inh, src_mode = bool(m["INHERITANCE"]), bool(m["SAMPLE_SOURCE"])
     Fam = len(t.family_names) if inh else 0
     indptr, indices = data.network["adj_mat"].indptr, data.network["adj_mat"].indices
+    dev = torch.device("cuda", device)
     out = {"data": f"{name}: {t.n_sites} sites x {t.n_features} features x {t.n_states} states, "
                    f"{Fam} families, SAMPLE_SOURCE = {src_mode}, {B} chains/GPU",
            "runs": {}}
-    for Z in n_zones_list:
+
+    def setup(Z):
         cfg, _ = experiment.load_config(path, {"model": {"N_AREAS": int(Z)}})
         spec, gibbs = experiment.build_priors(cfg, data)
         eng = LikelihoodEngine(t.obs, t.fam_of_site, t.n_states, Z, Fam, inh, device=device, options=OPTIONS)
@@ -563,35 +570,72 @@ def real_data_leg(name, n_zones_list, B, K, burnin, seed, rank=0, world=1, devic
         src = np.stack([packing.source_to_index(x.source) for x in samples]) if src_mode else None
         prior = spec.log_prior(zos, pg, pf, t.applicable, Z, inh)
         st = ChainState(eng, zos, w, pg, pz, pf, prior=prior, source=src)
-        max_m, p_grow = int(m["MAX_M"]), float(mc["P_GROW_CONNECTED"])
-        if burnin:
-            smp.run(st, burnin, max_m, p_grow, seed=seed * 7919 + Z, chain_id0=rank * B)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        t0 = time.perf_counter()
-        res = smp.run(st, K, max_m, p_grow, seed=seed * 7919 + Z, chain_id0=rank * B, trace=True)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        wall = time.perf_counter() - t0
-        status = res["status"].cpu().numpy()
-        if np.any(status != 0):
-            raise SystemExit(f"{name} leg: chain status {np.unique(status)}")
-        e = logged_ess(res["ll"].cpu().numpy())[0]
-        tt = torch.tensor([wall, float(e.sum()), res["accept"].float().mean().item()],
-                          dtype=torch.float64, device=torch.device("cuda", device))
+        return {"Z": Z, "eng": eng, "smp": smp, "st": st, "max_m": int(m["MAX_M"]),
+                "p_grow": float(mc["P_GROW_CONNECTED"])}
+
+    def launch(r, n, trace):
+        return r["smp"].run(r["st"], n, r["max_m"], r["p_grow"], seed=seed * 7919 + r["Z"],
+                            chain_id0=rank * B, trace=trace)
+
+    def reduce(wall, res_list):
+        e = sum(float(logged_ess(res["ll"].cpu().numpy())[0].sum()) for res in res_list)
+        acc = float(np.mean([res["accept"].float().mean().item() for res in res_list]))
+        for res in res_list:
+            status = res["status"].cpu().numpy()
+            if np.any(status != 0):
+                raise SystemExit(f"{name} leg: chain status {np.unique(status)}")
+        tt = torch.tensor([wall, e, acc], dtype=torch.float64, device=dev)
         if world > 1:
             mx, sm = tt.clone(), tt.clone()
             _all_reduce(mx, dist.ReduceOp.MAX)
             _all_reduce(sm, dist.ReduceOp.SUM)
             tt = torch.stack([mx[0], sm[1], sm[2] / world])
-        wall_max, ess_tot, acc = (float(v) for v in tt)
+        return (float(v) for v in tt)
+
+    def sync():
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+
+    runs = []
+    for Z in n_zones_list:
+        r = setup(Z)
+        runs.append(r)
+        if burnin:
+            launch(r, burnin, False)
+        sync()
+        t0 = time.perf_counter()
+        res = launch(r, K, True)
+        sync()
+        wall_max, ess_tot, acc = reduce(time.perf_counter() - t0, [res])
         out["runs"][f"Z={Z}"] = {"chains": B * world, "steps": K, "burnin": burnin,
                                  "mh_steps_per_sec": B * K * world / wall_max,
                                  "ess_per_sec": ess_tot / wall_max, "us_per_step": wall_max / K * 1e6,
-                                 "acceptance": acc}
-        eng.close()
+                                 "acceptance": acc, "wall_s": wall_max}
+        if not concurrent:
+            r["eng"].close()
+    if concurrent and len(runs) > 1:
+        seq_wall = sum(v["wall_s"] for v in out["runs"].values())
+        streams = [torch.cuda.Stream(dev) for _ in runs]
+        sync()
+        t0 = time.perf_counter()
+        res_list = []
+        for r, s in zip(runs, streams):
+            with torch.cuda.stream(s):
+                res_list.append(launch(r, K, True))
+        sync()
+        wall_max, ess_tot, acc = reduce(time.perf_counter() - t0, res_list)
+        n = len(runs)
+        out["sweep_concurrent"] = {
+            "zones": list(n_zones_list), "chains_per_run": B * world, "steps": K,
+            "mh_steps_per_sec": n * B * K * world / wall_max, "ess_per_sec": ess_tot / wall_max,
+            "wall_s": wall_max, "sequential_wall_s": seq_wall,
+            "sequential_mh_steps_per_sec": n * B * K * world / seq_wall,
+            "speedup_vs_sequential": seq_wall / wall_max, "acceptance": acc,
+            "how": f"the {n} K runs (each continuing its chains after the per-K run) launched at once, "
+                   f"one HIP stream each; sequential = the per-K runs' walls added"}
+        for r in runs:
+            r["eng"].close()
     return out
 
 
@@ -861,7 +905,7 @@ def main():
                                              args.src_burnin, args.seed, rank, world, local_rank),
                 "cfg4_south_america": real_data_leg("south_america", [1, 2, 3, 4, 5, 6], args.src_chains,
                                                     args.src_steps, args.src_burnin, args.seed, rank,
-                                                    world, local_rank)}
+                                                    world, local_rank, concurrent=True)}
     if rank == 0:
         line = {
             "metric": METRIC,
