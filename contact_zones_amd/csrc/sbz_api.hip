@@ -684,7 +684,7 @@ int sbz_draw_gamma(sbz_ctx *ctx, int32_t n, const double *alpha, uint64_t seed, 
 uint64_t sbz_mh_lds_bytes(const sbz_dims *dims) {
     if (!dims) return 0;
     const size_t b = mh_lds_bytes(*dims, (dims->flags & SBZ_INHERITANCE) ? 3 : 2);
-    return b > 64 * 1024 ? 0 : b;
+    return b > 160 * 1024 ? 0 : b;
 }
 
 int sbz_device_alloc(sbz_ctx *ctx, uint64_t bytes, void **out) {

@@ -104,7 +104,7 @@ inline int np_of(int n_sites) {
 }
 
 // Sampler (sbz_mh.hip)
-size_t mh_lds_bytes(const sbz_dims &d, int C, bool geo = false);
+size_t mh_lds_bytes(const sbz_dims &d, int C, bool geo = false, bool gib = false);
 int launch_mh(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg, const sbz_chains *chains);
 // sbz_draw_gamma: n gamma draws of the samplers' generator (device arrays)
 int launch_draw_gamma(sbz_ctx *ctx, int n, const double *alpha, uint64_t seed, double *out);

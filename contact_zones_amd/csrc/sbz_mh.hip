@@ -9,6 +9,8 @@
 //   swap_zone :704-786 (:1328-1416)             alter_weights :408-452
 //   alter_p_global :454-493   alter_p_zones :495-535   alter_p_families :571-612
 //   dirichlet_proposal :537-569 (q = exp(scipy dirichlet._logpdf) then log)
+//   gibbsish_sample_zones :619-702 (warm-up :1323-1326; weight 0 in the reference's own table,
+//   mcmc_setup.py:77, so it runs only when a caller gives it a weight)
 // Every decision is uniform: all lanes of all 4 waves draw the same values and take the same
 // branches; the 256 threads share the per-site / per-feature work.
 //
@@ -79,10 +81,10 @@ struct Plans {
 struct MhLayout {
     int KT, CH, nsc, NpS, nent, ncol;
     uint32_t col, zsize, red, nb, zos, selc, lst, tabo, tabn, nw, rowp, ipos, plans, plcol,
-        plnw, geo;
+        plnw, geo, gib;
     size_t total;
     __host__ __device__ MhLayout(int N, int Np, int S, int Z, int Fam, int C, int FamC, int NT,
-                                 bool with_geo = false, int la = 1) {
+                                 bool with_geo = false, int la = 1, bool with_gib = false) {
         KT = Np / NT;
         KT = KT < 4 ? 4 : (KT > 32 ? 32 : KT);
         CH = NT * KT;
@@ -114,6 +116,9 @@ struct MhLayout {
         plcol = take(la > 1 ? (size_t)la * ncol * 8 : 0);
         plnw = take(la > 1 ? (size_t)la * 32 * 8 : 0);
         geo = with_geo ? take(geo_scratch_bytes(N)) : o;
+        // gibbsish_sample_zones: per available site its two log marginals [N] + [N] doubles and
+        // its in / out flags [N] bytes
+        gib = with_gib ? take((size_t)N * 17) : o;
         total = o;
     }
 };
@@ -138,7 +143,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
     const int N = a.N, F = a.F, S = a.S, Z = a.Z, Fam = (C == 3) ? a.Fam : 0;
     const sbz_chains &ch = a.ch;
 
-    const MhLayout L(N, a.Np, S, Z, a.Fam, C, a.FamC, NT, a.geo_cost != nullptr, a.la);
+    const MhLayout L(N, a.Np, S, Z, a.Fam, C, a.FamC, NT, a.geo_cost != nullptr, a.la, a.gib != 0);
     const int KT = L.KT, CH = L.CH, nsc = L.nsc, ncol = L.ncol;
     double *col = reinterpret_cast<double *>(lds + L.col);  // staged parameter column
     int *zsize = reinterpret_cast<int *>(lds + L.zsize);     // [Z]
@@ -264,8 +269,9 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
     uint16_t stamp = 0;
 
     auto is_nb = [&](int s) { return nb[s] == stamp && zos[s] == NONE; };
-    // site selections: SEL_NB (neighbours of the marked zone, free), SEL_FREE, SEL_ZONE (members of z)
-    enum { SEL_NB = 0, SEL_FREE = 1, SEL_ZONE = 2 };
+    // site selections: SEL_NB (neighbours of the marked zone, free), SEL_FREE, SEL_ZONE (members of
+    // z), SEL_AVAIL (free or in z: gibbsish_sample_zones' available sites, zone_sampling.py:627)
+    enum { SEL_NB = 0, SEL_FREE = 1, SEL_ZONE = 2, SEL_AVAIL = 3 };
     // Scan: every thread builds the bit mask of its selected sites (bit j = site base + j, KT <= 32
     // sites read with a few wide LDS reads) of chunk c; per-wave counts go to selc.
     auto scan_mask = [&](int mode, int z, int c) -> uint32_t {
@@ -280,8 +286,10 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             for (int j = 0; j < 4; j++) {
                 const uint32_t zs = (zw >> (8 * j)) & 0xffu;
                 const uint32_t ns = ((j < 2 ? nw2.x : nw2.y) >> (16 * (j & 1))) & 0xffffu;
-                const bool f = mode == SEL_NB ? (ns == stamp && zs == NONE)
-                                              : (mode == SEL_FREE ? zs == NONE : zs == (uint32_t)z);
+                const bool f = mode == SEL_NB     ? (ns == stamp && zs == NONE)
+                               : mode == SEL_FREE ? zs == NONE
+                               : mode == SEL_ZONE ? zs == (uint32_t)z
+                                                  : (zs == NONE || zs == (uint32_t)z);
                 m |= (f ? 1u : 0u) << (4 * g + j);
             }
         }
@@ -344,20 +352,12 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
         }
         return -1;
     };
-    // mark nb[t] = stamp for every site t adjacent to a member of zone z: the members are
-    // compacted into lst, then every thread marks one member's neighbours (the adjacency loads of
-    // all members in flight at once)
-    auto mark = [&](int z) {
-        stamp++;
-        if (stamp == 0) {  // wrapped: clear
-            for (int s = tid; s < L.NpS; s += NT) nb[s] = 0;
-            bsync();
-            stamp = 1;
-        }
-        const int nmem = scan_sel(SEL_ZONE, z);
+    // the selected sites of (mode, z) compacted into lst[0 .. n) in ascending order; returns n
+    auto compact_sel = [&](int mode, int z) -> int {
+        const int nsel = scan_sel(mode, z);
         int base = 0;
         for (int c = 0; c < nsc; c++) {
-            uint32_t m = c < 4 ? msk[c & 3] : scan_mask(SEL_ZONE, z, c);
+            uint32_t m = c < 4 ? msk[c & 3] : scan_mask(mode, z, c);
             int woff = 0, tot = 0;
 #pragma unroll
             for (int i = 0; i < NWV; i++) {
@@ -374,6 +374,19 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             base += uni(tot);
         }
         bsync();
+        return nsel;
+    };
+    // mark nb[t] = stamp for every site t adjacent to a member of zone z: the members are
+    // compacted into lst, then every thread marks one member's neighbours (the adjacency loads of
+    // all members in flight at once)
+    auto mark = [&](int z) {
+        stamp++;
+        if (stamp == 0) {  // wrapped: clear
+            for (int s = tid; s < L.NpS; s += NT) nb[s] = 0;
+            bsync();
+            stamp = 1;
+        }
+        const int nmem = compact_sel(SEL_ZONE, z);
         for (int i = tid; i < nmem; i += NT) {
             const int s = lst[i];
             const int e0 = a.adj_ptr[s], e1 = a.adj_ptr[s + 1];
@@ -418,6 +431,36 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
         }
         return (log(mn) - log(mo)) + (double)(en - eo) * LN2;  // this thread's part (block_sum)
     };
+
+    // gibbsish_sample_zones (zone_sampling.py:644-665): site s's log marginal likelihood with
+    // zone z (lw) and without any zone (lwo), sum_f log feature_lh, over the wave's lanes (one
+    // wave per site; every lane of the wave gets both)
+    auto site_logs = [&](int s, int z, double &lw, double &lwo) {
+        const int fc = (C == 3) ? a.fam_site[MH_IDX(s, N, 3)] : 0;
+        const bool hf = fc > 0;
+        double mw = 1.0, mo = 1.0;
+        int ew = 0, eo = 0;
+        for (int f = lane; f < F; f += WAVE) {
+            const int x = a.obs_sm[MH_IDX((long long)s * F + f, (long long)N * F, 4)];
+            const bool na = x == S;
+            const int xc = na ? 0 : x;
+            const double *wp = w + MH_IDX((long long)f * C, (long long)F * C, 5);
+            const double wf[3] = {ldp(wp), ldp(wp + 1), C == 3 ? ldp(wp + C - 1) : 0.0};
+            const double l0 = ldp(pg + MH_IDX((long long)f * S + xc, nFS, 6));
+            const double l2v = ldp(pf + MH_IDX(((long long)(hf ? fc - 1 : 0) * F + f) * S + xc, C == 3 && Fam > 0 ? nFamFS : nFS, 7));
+            const double lz = ldp(pz + MH_IDX(((long long)z * F + f) * S + xc, Z > 0 ? nZFS : 1, 8));
+            const double l2 = hf ? l2v : 0.0;
+            mw *= cell<C>(wf, true, hf, na, l0, lz, l2);
+            mo *= cell<C>(wf, false, hf, na, l0, 0.0, l2);
+            renorm(mw, ew);
+            renorm(mo, eo);
+        }
+        lw = wave_sum(log(mw) + (double)ew * LN2);
+        lwo = wave_sum(log(mo) + (double)eo * LN2);
+    };
+    double *gib_lw = reinterpret_cast<double *>(lds + L.gib);  // [N] per available site
+    double *gib_lwo = gib_lw + N;                               // [N]
+    uint8_t *gib_fl = reinterpret_cast<uint8_t *>(gib_lwo + N); // [N] bit 0 new, bit 1 old membership
 
     // Feature f's parameter column pg | pz[z] | pf[fam] | w: loaded into registers early
     // (col_load, issued before the proposal math so the loads are in flight meanwhile) and
@@ -880,8 +923,8 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
         const bool planned = philox && LAe > 1 && uni(p_ok) != 0;
         const int op = planned ? uni(p_op) : rng.op(a.op_cdf, a.nops);
         if (SBZ_MH_STAMP) tph[21] = __builtin_amdgcn_s_memtime();
-        if (op < 0 || op > P_FAMILIES || (op == P_FAMILIES && (C == 2 || Fam == 0)) ||
-            (op <= SWAP && Z == 0) || (op == P_ZONES && Z == 0)) {
+        if (op < 0 || op > GIBBSISH || (op == P_FAMILIES && (C == 2 || Fam == 0)) ||
+            ((op <= SWAP || op == GIBBSISH) && Z == 0) || (op == P_ZONES && Z == 0)) {
             broken = true;
             break;
         }
@@ -895,6 +938,11 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
         double prec = 0.0;
         double *base = nullptr;
         const int n_free = N - occupied;
+        // gibbsish_sample_zones: zone gz, its gn available sites in lst, the proposed size, the
+        // change of the occupied count and the move's delta ll; gtent: zos holds the proposal
+        bool gib = false, gtent = false;
+        int gz = 0, gn = 0, gsize = 0, gdocc = 0;
+        double gdelta = 0.0;
 
         // ---- 1. the move
         if (op <= SWAP) {
@@ -965,6 +1013,123 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                 sa = site;
                 zoa = z;
                 zna = NONE;
+            }
+        } else if (op == GIBBSISH) {
+            // zone_sampling.py:619-702: zone z's available sites (free or in z; a random subset of
+            // about 100 when more), each resampled in / out of z with the posterior
+            // exp(lw) / (exp(lw) + exp(lwo)) of its marginal likelihoods; uniforms from the tape
+            // in site order (np.random.random(n)) or the per-site Philox streams of slots 2 / 3
+            const int z = rng.below(Z);
+            if (z < 0 || z >= Z) {
+                broken = true;
+                break;
+            }
+            gib = true;
+            gz = z;
+            const uint64_t slot = ctr0 + (uint64_t)step * WIN;
+            auto site_u = [&](int64_t p0, int k, int sl) {
+                return rng.tape ? rng.tape[p0 + k] : site_uniform(rng.key0, rng.key1, rng.chain, slot + sl, (uint32_t)k);
+            };
+            auto take_tape = [&](int n) -> int64_t {  // the next n tape items (wave-uniform)
+                const int64_t p0 = rng.pos;
+                if (rng.tape) {
+                    if (p0 + n > rng.len) rng.bad = 1;
+                    rng.pos = uni64(min(p0 + n, rng.len));
+                }
+                return p0;
+            };
+            const int size = uni(zsize[z]);
+            int n = compact_sel(SEL_AVAIL, z);
+            if (n > 100) {  // available[available] &= np.random.random(n) < (100 / n)   (:631-633)
+                const double thr = 100.0 / (double)n;
+                const int64_t p0 = take_tape(n);
+                if (rng.bad) break;
+                int kept = 0;
+                for (int r0 = 0; r0 < n; r0 += NT) {  // order-preserving compaction in place
+                    const int i = r0 + tid;
+                    int st = 0;
+                    bool keep = false;
+                    if (i < n) {
+                        st = lst[i];
+                        keep = site_u(p0, i, 2) < thr;
+                    }
+                    const uint64_t bal = __ballot(keep);
+                    if (lane == 0) selc[wv] = (int)__popcll(bal);
+                    bsync();
+                    int woff = 0, tot = 0;
+#pragma unroll
+                    for (int q = 0; q < NWV; q++) {
+                        const int t = selc[q];
+                        woff += q < wv ? t : 0;
+                        tot += t;
+                    }
+                    if (keep) lst[kept + woff + (int)__popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)st;
+                    kept += uni(tot);
+                    bsync();
+                }
+                n = kept;
+            }
+            gn = n;
+            if (n > 0) {
+                for (int k = wv; k < n; k += NWV) {
+                    double lw, lwo;
+                    site_logs(lst[k], z, lw, lwo);
+                    if (lane == 0) {
+                        gib_lw[k] = lw;
+                        gib_lwo[k] = lwo;
+                    }
+                }
+                bsync();
+                const int64_t p1 = take_tape(n);  // new_zone = np.random.random(n) < posterior_zone
+                if (rng.bad) break;
+                double lq = 0.0, lqb = 0.0, d = 0.0;
+                int n_new = 0, n_old = 0, n_zero = 0;
+                for (int k = tid; k < n; k += NT) {
+                    const double lw = gib_lw[k], lwo = gib_lwo[k];
+                    const double mw = exp(lw), mo = exp(lwo);
+                    const double post = mw / (mw + mo);
+                    const bool nz = site_u(p1, k, 3) < post;
+                    const bool oz = zos[lst[k]] == (uint8_t)z;
+                    const double fn = nz ? 1.0 : 0.0, fo = oz ? 1.0 : 0.0;
+                    const double q = post * fn + (1.0 - post) * (1.0 - fn);
+                    const double qb = post * fo + (1.0 - post) * (1.0 - fo);
+                    lq += log(q);
+                    lqb += log(qb);
+                    n_zero += qb == 0.0 ? 1 : 0;
+                    n_new += nz ? 1 : 0;
+                    n_old += oz ? 1 : 0;
+                    if (nz != oz) d += nz ? lw - lwo : lwo - lw;
+                    gib_fl[k] = (uint8_t)((nz ? 1 : 0) | (oz ? 2 : 0));
+                }
+                int nn = 0, no = 0, nzb = 0;
+                const double LQ = block_sum_di(lq, n_new, nn);
+                const double LQB = block_sum_di(lqb, n_old, no);
+                gdelta = block_sum_di(d, n_zero + (err != 0 ? 0x10000 : 0), nzb);
+                if (nzb >= 0x10000) {  // a range check failed
+                    broken = true;
+                    break;
+                }
+                gsize = size - no + nn;
+                gdocc = nn - no;
+                // reject: a size outside [min_size, max_size] (:678-681), or a zero back probability
+                if (a.min_size <= gsize && gsize <= max_size && nzb == 0) {
+                    log_q = LQ;
+                    log_q_back = LQB;
+                    if (a.size_prior == 1) {  // -log C(N, size) per zone: one site at a time
+                        double dp = 0.0;
+                        for (int sz = size; sz != gsize; sz += gsize > sz ? 1 : -1)
+                            dp += size_prior_delta(1, N, sz, sz + (gsize > sz ? 1 : -1));
+                        dprior = uni(dp);
+                    } else {
+                        dprior = uni(size_prior_delta(a.size_prior, N, size, gsize));
+                    }
+                    if (a.geo_cost && z == Z - 1) {  // the last zone's MST on the proposed zone
+                        for (int k = tid; k < n; k += NT)
+                            zos[lst[k]] = (gib_fl[k] & 1) ? (uint8_t)z : (uint8_t)NONE;
+                        bsync();
+                        gtent = true;
+                    }
+                }
             }
         } else if (planned) {
             // checked when planned (make_plans stage A; an invalid move is never planned)
@@ -1079,8 +1244,13 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             }
         }
 
+        if (gib) delta = gdelta;
         // the geo prior of the last zone, when the move changes it
         double geo_new = geo_cur;
+        if (gtent) {
+            geo_new = geo_prior(-1, -1, -1);
+            dprior = uni(dprior + (geo_new - geo_cur));
+        }
         if (a.geo_cost && sa >= 0 && (zna == Z - 1 || zoa == Z - 1)) {
             geo_new = geo_prior(zna == Z - 1 ? sa : -1, zoa == Z - 1 ? sa : -1,
                                 (sb >= 0 && zna == Z - 1) ? sb : -1);
@@ -1109,7 +1279,18 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             ll = ll + delta;
             prior = prior + dprior;
             geo_cur = geo_new;
-            if (sa >= 0) {
+            if (gib) {
+                for (int k = tid; k < gn; k += NT) {
+                    const int st = lst[k];
+                    const bool nz = gib_fl[k] & 1;
+                    const int fcs = C == 3 ? (int)a.fam_site[st] : 0;
+                    zos[st] = nz ? (uint8_t)gz : (uint8_t)NONE;
+                    rowp[ipos[st]] = (uint32_t)(((nz ? gz + 1 : 0) * FamC + fcs) * row_bytes);
+                }
+                if (tid == 0) zsize[gz] = gsize;
+                occupied += gdocc;
+                bsync();
+            } else if (sa >= 0) {
                 if (tid == 0) {
                     const int fca = C == 3 ? (int)a.fam_site[sa] : 0;
                     rowp[ipos[sa]] = (uint32_t)(((zna < Z ? zna + 1 : 0) * FamC + fca) * row_bytes);
@@ -1148,6 +1329,11 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                     if (__ballot(in) != 0) bsync();  // the same ballot in every wave
                 }
             }
+        }
+        if (gtent && !accept) {  // restore the assignment the proposal overwrote
+            for (int k = tid; k < gn; k += NT)
+                zos[lst[k]] = (gib_fl[k] & 2) ? (uint8_t)gz : (uint8_t)NONE;
+            bsync();
         }
         if (ch.trace_op && tid == 0) {
             const size_t t = (size_t)b * a.n_steps + step;
@@ -1203,10 +1389,10 @@ constexpr int MH_WAVES = 4;  // waves per chain (one workgroup per chain)
 
 }  // namespace
 
-size_t mh_lds_bytes(const sbz_dims &d, int C, bool geo) {
+size_t mh_lds_bytes(const sbz_dims &d, int C, bool geo, bool gib) {
     const int FamC = C == 3 ? d.n_families + 1 : 1;
     return MhLayout(d.n_sites, np_of(d.n_sites), d.n_states, d.n_zones, d.n_families, C, FamC,
-                    MH_WAVES * WAVE, geo).total;
+                    MH_WAVES * WAVE, geo, 1, gib).total;
 }
 
 namespace {
@@ -1249,7 +1435,7 @@ int launch_mh(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg, const 
     a.warmup = cfg->warmup;
     // operators of the mode: zone moves + alter_* (mixture) or + Gibbs operators (source mode)
     bool allowed[SBZ_N_OPS] = {};
-    allowed[SHRINK] = allowed[GROW] = allowed[SWAP] = true;
+    allowed[SHRINK] = allowed[GROW] = allowed[SWAP] = allowed[GIBBSISH] = true;
     if (src) {
         for (int i = G_SOURCES; i <= G_P_FAMILIES; i++) allowed[i] = true;
     } else {
@@ -1262,14 +1448,13 @@ int launch_mh(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg, const 
         if (p < 0.0 || std::isnan(p)) return fail(ctx, SBZ_EINVAL, "negative operator probability");
         if (p > 0.0 && !allowed[i])
             return fail(ctx, SBZ_EINVAL, std::string("operator ") + std::to_string(i) +
-                                             (i == 7 ? " (gibbsish_sample_zones) is not supported"
-                                                     : " is not available in this mode (sample_source)"));
+                                             " is not available in this mode (sample_source)");
         if (p > 0.0) last = i;
         tot += p;
     }
     if (!(tot > 0.0)) return fail(ctx, SBZ_EINVAL, "operator probabilities sum to 0");
     const double zone_ops = cfg->op_prob[SHRINK] + cfg->op_prob[GROW] + cfg->op_prob[SWAP] +
-                            cfg->op_prob[P_ZONES] + cfg->op_prob[G_P_ZONES];
+                            cfg->op_prob[GIBBSISH] + cfg->op_prob[P_ZONES] + cfg->op_prob[G_P_ZONES];
     if (d.n_zones == 0 && zone_ops > 0) return fail(ctx, SBZ_EINVAL, "zone operators need n_zones > 0");
     if ((ctx->C == 2 || d.n_families == 0) && (cfg->op_prob[P_FAMILIES] + cfg->op_prob[G_P_FAMILIES]) > 0)
         return fail(ctx, SBZ_EINVAL, "family operators need inheritance with families");
@@ -1281,6 +1466,7 @@ int launch_mh(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg, const 
     }
     a.op_cdf[a.nops - 1] = 1.0;
     for (int i = 0; i < 4; i++) a.prec[i] = cfg->precision[i];
+    a.gib = cfg->op_prob[GIBBSISH] > 0.0 ? 1 : 0;
     a.obs_fm = ctx->d_obs_fm;
     a.famc = ctx->d_famc;
     a.perm = ctx->d_perm;
@@ -1312,12 +1498,12 @@ int launch_mh(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg, const 
     if (src) return launch_mh_source(ctx, B, a);
     if (d.n_sites > 65535) return fail(ctx, SBZ_EINVAL, "sampler supports at most 65535 sites");
     const bool geo = a.geo_cost != nullptr;
-    if (mh_lds_bytes(d, ctx->C, geo) > 64 * 1024)
-        return fail(ctx, SBZ_EINVAL, "sampler state exceeds 64 KiB of LDS (too many sites)");
+    if (mh_lds_bytes(d, ctx->C, geo, a.gib != 0) > 160 * 1024)
+        return fail(ctx, SBZ_EINVAL, "sampler state exceeds the 160 KiB of LDS (too many sites)");
     // planned steps per batch (Philox only): as many as SBZ_MH_LA asks whose columns fit the LDS
     auto lds_of = [&](int la) {
         return MhLayout(d.n_sites, np_of(d.n_sites), d.n_states, d.n_zones, d.n_families, ctx->C, ctx->FamC,
-                        MH_WAVES * WAVE, geo, la).total;
+                        MH_WAVES * WAVE, geo, la, a.gib != 0).total;
     };
     constexpr size_t LDS_MAX = 160 * 1024;
     int la = a.ch.tape ? 1 : std::min(ctx->mh_la, LA);

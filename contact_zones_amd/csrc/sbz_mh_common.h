@@ -16,7 +16,7 @@ constexpr int WAVE = 64;
 constexpr int NONE = 255;
 constexpr double LN2 = 0.69314718055994530941723212145818;
 enum Op { SHRINK = 0, GROW = 1, SWAP = 2, WEIGHTS = 3, P_GLOBAL = 4, P_ZONES = 5, P_FAMILIES = 6,
-          G_SOURCES = 8, G_WEIGHTS = 9, G_P_GLOBAL = 10, G_P_ZONES = 11, G_P_FAMILIES = 12 };
+          GIBBSISH = 7, G_SOURCES = 8, G_WEIGHTS = 9, G_P_GLOBAL = 10, G_P_ZONES = 11, G_P_FAMILIES = 12 };
 
 __device__ __forceinline__ void wsync() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -239,6 +239,17 @@ __device__ __forceinline__ double philox_uniform(uint32_t key0, uint32_t key1, u
     return (i & 1) ? u53(c[2], c[3]) : u53(c[0], c[1]);
 }
 
+// gibbsish_sample_zones, Philox mode: uniform i of the per-site stream keyed by counter slot
+// `slot` of the step's window (the subset draw at slot 2, the in / out draw at slot 3): half
+// (i & 1) of block (i >> 1, slot lo, chain, slot hi ^ 0xFE << 24), a stream no LaneRng lane
+// (lane + 1 < 0xFE) shares.  Any thread computes any site's uniform on its own.
+__device__ __forceinline__ double site_uniform(uint32_t key0, uint32_t key1, uint64_t chain, uint64_t slot,
+                                               uint32_t i) {
+    uint32_t c[4] = {i >> 1, (uint32_t)slot, (uint32_t)chain, (uint32_t)(slot >> 32) ^ 0xFE000000u};
+    philox4x32_10(c, key0, key1);
+    return (i & 1) ? u53(c[2], c[3]) : u53(c[0], c[1]);
+}
+
 // Per-lane Philox stream: block (j, base lo, chain, base hi ^ (lane + 1) << 24), key = seed.
 // `base` is the wave's 64-bit counter when the phase started (the wave then advances it by one),
 // j counts the lane's draws in the phase.  The counter's high word goes into c3 (bits 0..19; a
@@ -454,6 +465,8 @@ struct MhArgs {
     int stage;  // mh_src_kernel: parameters and normalised weights staged in LDS for the N*F passes
     int cstage; // mh_src_kernel (with stage): the constant tables (applicable states, Gibbs prior
                 //   counts, 'counts' prior) staged in LDS too
+    int gib;    // gibbsish_sample_zones has a non-zero weight: LDS holds its per-site scratch
+    uint32_t gib_off;  // mh_src_kernel: byte offset of that scratch in LDS
     double op_cdf[SBZ_N_OPS];
     double prec[4];
     const uint8_t *obs_fm;      // [F][Np] by position

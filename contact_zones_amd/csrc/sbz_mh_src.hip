@@ -16,6 +16,10 @@
 //   gibbs_sample_p_global  (:334-357)  40 % of the features, Dirichlet(prior counts + counts)
 //   gibbs_sample_p_zones   (:359-379)  one zone, every feature, Dirichlet(1 + counts)
 //   gibbs_sample_p_families(:381-406)  one family, 40 % of the features
+//   gibbsish_sample_zones  (:619-702)  one zone's available sites resampled in / out from their
+//                                      marginal likelihoods, then their sources redrawn
+//                                      (site_subset = available); weight 0 in the reference's own
+//                                      operator table (mcmc_setup.py:77)
 // The Gibbs operators return Q_GIBBS (log q = -inf): always accepted.
 //
 // One wave runs one chain.  The chain's sources (N x F bytes, current and candidate), zone
@@ -438,8 +442,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     };
     // obs_terms from the staged copies (the same values, the same operations); x = the observed
     // state of (s, f) (S = NA)
-    auto terms = [&](int s, int f, int x, double (&l)[3], double (&wn)[3]) {
-        const int zc = zos[s];
+    auto terms_z = [&](int s, int f, int x, int zc, double (&l)[3], double (&wn)[3]) {
         if (!stg) {
             const int fc = C == 3 ? a.fam_site[s] : 0;
             obs_terms<C>(a, w, pg, pz, pf, f, x, zc, fc, l, wn);
@@ -457,6 +460,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         l[1] = na ? 1.0 : (hz ? lpz[(zc * F + f) * S + xc] : 0.0);
         l[2] = (C == 3) ? (na ? 1.0 : (hf ? lpf[((fc - 1) * F + f) * S + xc] : 0.0)) : 0.0;
     };
+    auto terms = [&](int s, int f, int x, double (&l)[3], double (&wn)[3]) { terms_z(s, f, x, zos[s], l, wn); };
     // ---- passes over the N*F observations; (s, f) stepped with the cell index instead of a
     // division per cell.  body(s, f, x, g, c): x the observed state, g the cell's index in the
     // source arrays, c = s * F + f its index in C order (the reference's order of the tape's
@@ -684,6 +688,37 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         return bsum(dp);
     };
 
+    // ---- gibbsish_sample_zones scratch (a.gib): per available site its two log marginals, the
+    // available list, its in / out flags, and the position of every site (GS: cells by position)
+    double *g_lw = reinterpret_cast<double *>(lds + a.gib_off);  // [N]
+    double *g_lwo = g_lw + N;                                     // [N]
+    uint16_t *g_lst = reinterpret_cast<uint16_t *>(g_lwo + N);    // [N]
+    uint16_t *g_pos = g_lst + N;                                  // [N] (GS only)
+    uint8_t *g_fl = reinterpret_cast<uint8_t *>(g_pos + N);       // [N] bit 0 new, bit 1 old
+    if (a.gib && GS) {
+        for (int p = tid; p < N; p += NT) g_pos[a.perm[p]] = (uint16_t)p;  // positions < N hold sites
+        sync();
+    }
+    // the source-array index of observation (s, f)
+    auto cell_of = [&](int s, int f) -> int { return GS ? f * Np + (int)g_pos[s] : s * F + f; };
+    // the observed state of (s, f) (S = NA)
+    auto obs_of = [&](int s, int f) -> int { return stg ? lobs[s * F + f] : a.obs_sm[(size_t)s * F + f]; };
+    // the n sites of the list, compacted in ascending order by `keep` (wave 0 writes; every wave
+    // gets the count).  Reads of a chunk precede its writes, so the compaction may be in place.
+    auto compact = [&](int n, auto &&site_at, auto &&keep) -> int {
+        int kept = 0;
+        for (int k0 = 0; k0 < n; k0 += WAVE) {
+            const int k = k0 + lane;
+            const int st = k < n ? site_at(k) : 0;
+            const bool in = k < n && keep(k, st);
+            const uint64_t m = __ballot(in);
+            if (wv == 0 && in) g_lst[kept + lane_prefix(m)] = (uint16_t)st;
+            kept += __popcll(m);
+        }
+        sync();
+        return uni(kept);
+    };
+
     bool broken = false;
     for (int step = 0; step < a.n_steps; step++) {
         uint64_t tph[12] = {};  // SBZ_SRC_STAMP builds only
@@ -703,7 +738,8 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         }
         SRC_TS(1);
         const bool zone_op = op <= SWAP;
-        if (!(zone_op || (op >= G_SOURCES && op <= G_P_FAMILIES)) || (zone_op && Z == 0) ||
+        if (!(zone_op || op == GIBBSISH || (op >= G_SOURCES && op <= G_P_FAMILIES)) ||
+            ((zone_op || op == GIBBSISH) && Z == 0) ||
             (op == G_P_ZONES && Z == 0) || (op == G_P_FAMILIES && (C == 2 || Fam == 0))) {
             broken = true;
             break;
@@ -713,6 +749,10 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         int sa = -1, zoa = NONE, zna = NONE, sb = -1;
         bool new_sources = false;
         double geo_new = geo_cur;
+        // gibbsish_sample_zones: zone gz, gn sites in g_lst, proposed size; gtent: zos holds the
+        // proposal (undone on rejection)
+        bool gtent = false;
+        int gz = 0, gn = 0, gsize = 0, gdocc = 0;
 
         if (zone_op) {
             // ---- zone move with source resampling
@@ -798,6 +838,157 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                 new_sources = true;
                 log_q = a.warmup ? -INFINITY : uni(log(q) + log_q_s);
                 log_q_back = uni(log(q_back) + log_q_back_s);
+            }
+        } else if (op == GIBBSISH) {
+            // ---- gibbsish_sample_zones (zone_sampling.py:619-702), as the SAMPLE_SOURCE = false
+            // kernel (sbz_mh.hip) plus the sources of the available sites: log q_back gains their
+            // current posterior terms, their sources are redrawn from the new sample's posterior
+            // (gibbs_sample_sources(site_subset=available)) and log q gains those terms
+            log_q = 0.0;
+            log_q_back = -INFINITY;
+            const int z = rng.below(Z);
+            if (z < 0 || z >= Z) {
+                broken = true;
+                break;
+            }
+            gz = z;
+            auto take = [&](int n) -> int64_t {  // n tape items / one Philox slot (uniform)
+                const int64_t p0 = rng.pos;
+                if (rng.tape) {
+                    if (p0 + n > rng.len) rng.bad = 1;
+                    rng.pos = uni64(min(p0 + n, rng.len));
+                }
+                return p0;
+            };
+            auto site_u = [&](int64_t p0, uint64_t slot, int k) {
+                return rng.tape ? rng.tape[p0 + k] : site_uniform(rng.key0, rng.key1, rng.chain, slot, (uint32_t)k);
+            };
+            const int size = uni(zsize[z]);
+            int n = compact(N, [&](int k) { return k; }, [&](int, int st) { return zos[st] == NONE || zos[st] == z; });
+            if (n > 100) {  // available[available] &= np.random.random(n) < (100 / n)
+                const double thr = 100.0 / (double)n;
+                const int64_t p0 = take(n);
+                const uint64_t slot = rng.ctr;
+                if (!rng.tape) rng.ctr++;
+                if (rng.bad) break;
+                n = compact(n, [&](int k) { return (int)g_lst[k]; }, [&](int k, int) { return site_u(p0, slot, k) < thr; });
+            }
+            gn = n;
+            if (n > 0) {
+                const int nc = n * F;  // the available sites' observations, C order (site, feature)
+                // log q_back_s: the current sources' posterior terms (zone_sampling.py:638-643)
+                double log_q_back_s;
+                {
+                    ensure_staged();
+                    LogAcc acc;
+                    for (int c = tid; c < nc; c += NT) {
+                        const int k = c / F, f = c - k * F, st = g_lst[k];
+                        double l[3], wn[3], p[3];
+                        terms(st, f, obs_of(st, f), l, wn);
+                        posterior_draw<C>(l, wn, 2.0, p);
+                        acc.add(p[rsrc(src, cell_of(st, f))]);
+                    }
+                    log_q_back_s = bsum(acc.value());
+                }
+                // each site's log marginal likelihood with zone z and without (:644-665): one wave
+                // per site, the cells of the mixture (sum_c lh * w)
+                for (int k = wv; k < n; k += NW) {
+                    const int st = g_lst[k];
+                    LogAcc aw, ao;
+                    for (int f = lane; f < F; f += WAVE) {
+                        const int x = obs_of(st, f);
+                        double l[3], wn[3];
+                        terms_z(st, f, x, z, l, wn);
+                        double v = l[0] * wn[0] + l[1] * wn[1];
+                        if (C == 3) v = v + l[2] * wn[2];
+                        aw.add(v);
+                        terms_z(st, f, x, NONE, l, wn);
+                        v = l[0] * wn[0] + l[1] * wn[1];
+                        if (C == 3) v = v + l[2] * wn[2];
+                        ao.add(v);
+                    }
+                    const double lw = wave_sum(aw.value()), lwo = wave_sum(ao.value());
+                    if (lane == 0) {
+                        g_lw[k] = lw;
+                        g_lwo[k] = lwo;
+                    }
+                }
+                sync();
+                const int64_t p1 = take(n);  // new_zone = np.random.random(n) < posterior_zone
+                const uint64_t slot = rng.ctr;
+                if (!rng.tape) rng.ctr++;
+                if (rng.bad) break;
+                double lq = 0.0, lqb = 0.0, n_new = 0.0, n_old = 0.0, n_zero = 0.0;
+                for (int k = tid; k < n; k += NT) {
+                    const double mw = exp(g_lw[k]), mo = exp(g_lwo[k]);
+                    const double post = mw / (mw + mo);
+                    const bool nz = site_u(p1, slot, k) < post;
+                    const bool oz = zos[g_lst[k]] == (uint8_t)z;
+                    const double fn = nz ? 1.0 : 0.0, fo = oz ? 1.0 : 0.0;
+                    const double q = post * fn + (1.0 - post) * (1.0 - fn);
+                    const double qb = post * fo + (1.0 - post) * (1.0 - fo);
+                    lq += log(q);
+                    lqb += log(qb);
+                    n_zero += qb == 0.0 ? 1.0 : 0.0;
+                    n_new += fn;
+                    n_old += fo;
+                    g_fl[k] = (uint8_t)((nz ? 1 : 0) | (oz ? 2 : 0));
+                }
+                const double LQ = bsum(lq), LQB = bsum(lqb);
+                const int nn = (int)bsum(n_new), no = (int)bsum(n_old), nzb = (int)bsum(n_zero);
+                gsize = size - no + nn;
+                gdocc = nn - no;
+                if (a.min_size <= gsize && gsize <= max_size && nzb == 0) {
+                    if (a.size_prior == 1) {  // -log C(N, size) per zone: one site at a time
+                        double dp = 0.0;
+                        for (int sz = size; sz != gsize; sz += gsize > sz ? 1 : -1)
+                            dp += size_prior_delta(1, N, sz, sz + (gsize > sz ? 1 : -1));
+                        dprior = uni(dp);
+                    } else {
+                        dprior = uni(size_prior_delta(a.size_prior, N, size, gsize));
+                    }
+                    // the proposed zone (tentatively), every source into the candidate array
+                    for (int k = tid; k < n; k += NT) zos[g_lst[k]] = (g_fl[k] & 1) ? (uint8_t)z : (uint8_t)NONE;
+                    for (int c = tid; c < (GS ? (int)NFP : NF); c += NT) wsrc(srcb, c, rsrc(src, c));
+                    sync();
+                    gtent = true;
+                    if (a.geo_cost && z == Z - 1) {
+                        geo_new = geo_prior();
+                        dprior = uni(dprior + (geo_new - geo_cur));
+                    }
+                    // gibbs_sample_sources(sample_new, as_gibbs=False, site_subset=available):
+                    // one uniform per available observation in C order
+                    double log_q_s;
+                    {
+                        LaneRng lr;
+                        lr.initw(rng, tid);
+                        LogAcc acc;
+                        const int64_t p2 = rng.pos;
+                        const bool have = !rng.tape || p2 + nc <= rng.len;
+                        for (int c = tid; c < nc; c += NT) {
+                            const int k = c / F, f = c - k * F, st = g_lst[k];
+                            double l[3], wn[3], p[3];
+                            terms(st, f, obs_of(st, f), l, wn);
+                            const double u = rng.tape ? (have ? rng.tape[p2 + c] : 0.0) : lr.u();
+                            const int kk = posterior_draw<C>(l, wn, u, p);
+                            wsrc(srcb, cell_of(st, f), kk);
+                            acc.add(p[kk]);
+                        }
+                        if (rng.tape) {
+                            if (!have) rng.bad = 1;
+                            rng.pos = uni64(p2 + nc);
+                        } else {
+                            rng.ctr++;
+                        }
+                        log_q_s = bsum(acc.value());
+                    }
+                    sync();
+                    ll_new = pass_ll(srcb);
+                    new_sources = true;
+                    // ZoneMCMCWarmup.gibbs_sample_sources returns Q_GIBBS = -inf (:1293-1296)
+                    log_q = a.warmup ? -INFINITY : uni(LQ + log_q_s);
+                    log_q_back = uni(LQB + log_q_back_s);
+                }
             }
         } else if (op == G_SOURCES) {
             double log_q_s;
@@ -939,6 +1130,14 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                 occupied += (zna < Z ? 1 : -1) + (sb >= 0 ? -1 : 0);
                 sync();
             }
+            if (gtent) {
+                if (tid == 0) zsize[gz] = gsize;
+                occupied += gdocc;
+                sync();
+            }
+        } else if (gtent) {  // undo the proposed zone
+            for (int k = tid; k < gn; k += NT) zos[g_lst[k]] = (g_fl[k] & 2) ? (uint8_t)gz : (uint8_t)NONE;
+            sync();
         } else if (sa >= 0) {
             sync();
             if (tid == 0) {  // undo the tentative zone change
@@ -1038,6 +1237,11 @@ int launch_mh_source(sbz_ctx *ctx, int B, const MhArgs &a0) {
                                           a.gc_g != nullptr, a.gc_f != nullptr);
     a.cstage = a.stage && ctx->d.n_states <= 255 && lds + cst <= LDS_MAX ? 1 : 0;
     if (a.cstage) lds += cst;
+    if (a.gib) {  // gibbsish_sample_zones scratch at the end (16-B aligned)
+        lds = (lds + 15) & ~(size_t)15;
+        a.gib_off = (uint32_t)lds;
+        lds += (size_t)ctx->d.n_sites * 21;
+    }
     if (lds > LDS_MAX)
         return fail(ctx, SBZ_EINVAL, "SAMPLE_SOURCE sampler needs " + std::to_string(lds) +
                                          " B of LDS per chain even with the sources in HBM (> 160 KiB)");

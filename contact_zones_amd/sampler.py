@@ -39,8 +39,6 @@ def op_probabilities(operators):
         if name not in OPS:
             raise ValueError(f"unknown operator {name!r} (sampler supports {OPS})")
         p[OPS.index(name)] = float(v)
-    if p[OPS.index("gibbsish_sample_zones")] != 0.0:
-        raise ValueError("gibbsish_sample_zones must have weight 0 (as in the reference, mcmc_setup.py:77)")
     return p
 
 

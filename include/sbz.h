@@ -203,7 +203,7 @@ int sbz_draw_gamma(sbz_ctx *ctx, int32_t n, const double *alpha, uint64_t seed, 
 enum sbz_op {
     SBZ_OP_SHRINK_ZONE = 0, SBZ_OP_GROW_ZONE = 1, SBZ_OP_SWAP_ZONE = 2, SBZ_OP_ALTER_WEIGHTS = 3,
     SBZ_OP_ALTER_P_GLOBAL = 4, SBZ_OP_ALTER_P_ZONES = 5, SBZ_OP_ALTER_P_FAMILIES = 6,
-    SBZ_OP_GIBBSISH_SAMPLE_ZONES = 7, /* reference weight 0 (mcmc_setup.py:77); must stay 0 */
+    SBZ_OP_GIBBSISH_SAMPLE_ZONES = 7, /* zone_sampling.py:619-702; weight 0 in the reference's table (mcmc_setup.py:77) */
     /* SAMPLE_SOURCE = true operators (mcmc_setup.py:80-87, zone_sampling.py:180-406) */
     SBZ_OP_GIBBS_SAMPLE_SOURCES = 8, SBZ_OP_GIBBS_SAMPLE_WEIGHTS = 9,
     SBZ_OP_GIBBS_SAMPLE_P_GLOBAL = 10, SBZ_OP_GIBBS_SAMPLE_P_ZONES = 11,
@@ -341,7 +341,7 @@ typedef struct sbz_trace {            /* per-step trace, [B][n_steps] each, or N
 int sbz_mh_run(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg, uint64_t seed,
                const sbz_tape *tape, sbz_state *io_state, sbz_trace *out_trace);
 
-/* Bytes of LDS the sampler needs per chain for these dims (0 if above the 64 KiB limit). */
+/* Bytes of LDS the sampler needs per chain for these dims (0 if above the 160 KiB of a CU). */
 uint64_t sbz_mh_lds_bytes(const sbz_dims *dims);
 
 #ifdef __cplusplus

@@ -15,6 +15,8 @@ on p_global / p_families and 'uniform' / 'quadratic' on zone sizes (``Model.log_
   alter_weights zone_sampling.py:408-452
   alter_p_global / alter_p_zones / alter_p_families   :454-535, :571-612
   dirichlet_proposal  :537-569  (q = exp(scipy dirichlet._logpdf), then log)
+  gibbsish_sample_zones :619-702 (warm-up :1323-1326: max_size[c]; SAMPLE_SOURCE: sources of the
+                                  available sites redrawn)
   get_neighbours      sbayes/util.py:139-155  (adj . zone > 0, minus occupied sites)
 
 Each random decision the reference draws is read from the tape instead (see the capture
@@ -32,7 +34,7 @@ OPS = ["shrink_zone", "grow_zone", "swap_zone", "alter_weights", "alter_p_global
        "alter_p_zones", "alter_p_families", "gibbsish_sample_zones",
        "gibbs_sample_sources", "gibbs_sample_weights", "gibbs_sample_p_global",
        "gibbs_sample_p_zones", "gibbs_sample_p_families"]
-SHRINK, GROW, SWAP, WEIGHTS, P_GLOBAL, P_ZONES, P_FAMILIES = range(7)
+SHRINK, GROW, SWAP, WEIGHTS, P_GLOBAL, P_ZONES, P_FAMILIES, GIBBSISH = range(8)
 G_SOURCES, G_WEIGHTS, G_P_GLOBAL, G_P_ZONES, G_P_FAMILIES = range(8, 13)
 NONE = 255
 
@@ -309,6 +311,63 @@ def op_p_families(m, st, c, tape):
     return new, log_q, log_q_back
 
 
+def _cells(m, st, zos):
+    """feature_lh = sum_c(all_lh * weights) (N, F) of every site under the zone assignment zos
+    (gibbsish_sample_zones :644-667; the same cells as combine_lh, model.py:175)."""
+    all_lh = lik_numpy.component_lh(m.obs, m.fam, zos, st["pg"], st["pz"], st.get("pf"), m.inheritance)
+    weights = lik_numpy.normalized_weights(st["w"], m.fam, zos, m.inheritance)
+    return np.sum(all_lh * weights, axis=-1)
+
+
+def op_gibbsish(m, st, c, tape):
+    """gibbsish_sample_zones (zone_sampling.py:619-702): one zone's available sites (free, or in
+    the zone; a random subset of ~100 when more) each resampled in / out of the zone from its
+    marginal likelihood with and without the zone."""
+    zos = st["zos"]
+    occupied = zos != NONE
+    z = tape.int()                                   # np.random.choice(range(n_zones)) :625
+    zone = zos == z
+    available = ~occupied | zone
+    n_available = np.count_nonzero(available)
+    if n_available > 100:                            # :631-633
+        available[available] &= tape.reals(n_available) < (100 / n_available)
+        n_available = np.count_nonzero(available)
+    if n_available == 0:
+        return REJECT
+    if m.sample_source:                              # :638-643, the current sample's posterior
+        log_q_back_s = log_q_sources(m.posterior(st)[available], st["src"][available])
+    with_z, without_z = zos.copy(), zos.copy()
+    with_z[available] = z
+    without_z[available] = NONE
+    lh_with = _cells(m, st, with_z)[available]
+    lh_without = _cells(m, st, without_z)[available]
+    marginal_with = np.exp(np.sum(np.log(lh_with), axis=-1))
+    marginal_without = np.exp(np.sum(np.log(lh_without), axis=-1))
+    posterior_zone = marginal_with / (marginal_with + marginal_without)
+    new_zone = tape.reals(n_available) < posterior_zone
+    new = dict(st, zos=zos.copy())
+    new["zos"][available] = np.where(new_zone, z, NONE)
+    size = np.count_nonzero(new["zos"] == z)
+    if not (m.min_size <= size <= m.max_size[c]):  # :678-681
+        return REJECT
+    q_per_site = posterior_zone * new_zone + (1 - posterior_zone) * (1 - new_zone)
+    log_q = np.sum(np.log(q_per_site))
+    old = zone[available]
+    q_back_per_site = posterior_zone * old + (1 - posterior_zone) * (1 - old)
+    if np.any(q_back_per_site == 0):
+        return REJECT
+    log_q_back = np.sum(np.log(q_back_per_site))
+    if m.sample_source:                              # :694-698
+        post = m.posterior(new)[available]
+        src = new["src"] = st["src"].copy()
+        src[available] = sample_categorical(post, tape)
+        if m.warmup:  # ZoneMCMCWarmup.gibbs_sample_sources returns Q_GIBBS = -inf (:1293-1296)
+            return new, -np.inf, log_q_back + log_q_back_s
+        log_q = log_q + log_q_sources(post, src[available])
+        log_q_back = log_q_back + log_q_back_s
+    return new, log_q, log_q_back
+
+
 # ---- SAMPLE_SOURCE = true ------------------------------------------------------------------
 
 def sample_categorical(p, tape):
@@ -428,7 +487,7 @@ def op_gibbs_p_families(m, st, c, tape, fraction_of_features=0.4):
 
 OPERATORS = {SHRINK: op_shrink, GROW: op_grow, SWAP: op_swap, WEIGHTS: op_weights,
              P_GLOBAL: op_p_global, P_ZONES: op_p_zones, P_FAMILIES: op_p_families,
-             G_SOURCES: op_gibbs_sources, G_WEIGHTS: op_gibbs_weights,
+             GIBBSISH: op_gibbsish, G_SOURCES: op_gibbs_sources, G_WEIGHTS: op_gibbs_weights,
              G_P_GLOBAL: op_gibbs_p_global, G_P_ZONES: op_gibbs_p_zones,
              G_P_FAMILIES: op_gibbs_p_families}
 SOURCE_MOVES = {SHRINK: with_sources(op_shrink), GROW: with_sources(op_grow),

@@ -146,7 +146,7 @@ def install_recorders(seed, zs_mod, mg_mod):
     return restore
 
 
-def run_case(name, data, model_cfg, mcmc_cfg, steps, seed, warmup, n_chains):
+def run_case(name, data, model_cfg, mcmc_cfg, steps, seed, warmup, n_chains, gibbsish=0.0):
     from sbayes.model import Model
     from sbayes.sampling import zone_sampling as zs
     from sbayes.sampling import mcmc_generative as mg
@@ -158,7 +158,7 @@ def run_case(name, data, model_cfg, mcmc_cfg, steps, seed, warmup, n_chains):
         model = Model(data=data, config=model_cfg)
         a = mcmc_cfg["STEPS"]
         ops = {"shrink_zone": a["area"] * 0.4, "grow_zone": a["area"] * 0.4,
-               "swap_zone": a["area"] * 0.2, "gibbsish_sample_zones": a["area"] * 0.0}
+               "swap_zone": a["area"] * 0.2, "gibbsish_sample_zones": a["area"] * gibbsish}
         if model_cfg["SAMPLE_SOURCE"]:  # MCMC.steps_per_operator (mcmc_setup.py:80-87)
             ops.update({"gibbs_sample_sources": a.get("source", 0.0),
                         "gibbs_sample_weights": a["weights"],
@@ -502,7 +502,40 @@ def real_cases():
         run_case(f"src_{tag}_z{z}", data, model, mcmc, steps=100, seed=seed, warmup=False, n_chains=2)
 
 
+def gibbsish_cases():
+    """gibbsish_sample_zones (zone_sampling.py:619-702) with a non-zero operator weight.  The
+    reference's own operator table gives it weight 0 (mcmc_setup.py:77, 'area' * 0.0), so these
+    captures set the weight in the capture's table only (run_case(gibbsish=...)); the reference
+    files are not touched.  Mixture and SAMPLE_SOURCE, ZoneMCMC and ZoneMCMCWarmup, a small network
+    (every free site available) and the 951-site simulation (more than 100 available sites: the
+    random subset of :631-633)."""
+    s = small_data()
+    run_case("gibbsish_small", s, model_cfg(2, True, min_m=3, max_m=25), mcmc_cfg(area=0.6, m_initial=4),
+             steps=300, seed=41, warmup=False, n_chains=3, gibbsish=0.6)
+    run_case("gibbsish_small_warmup", s, model_cfg(2, True, min_m=3, max_m=25),
+             mcmc_cfg(area=0.6, m_initial=4), steps=200, seed=42, warmup=True, n_chains=4, gibbsish=0.6)
+    d3 = sim_data(inheritance_families=3)
+    run_case("gibbsish_sim", d3, model_cfg(2, True, min_m=3, max_m=120), mcmc_cfg(area=0.6),
+             steps=200, seed=43, warmup=False, n_chains=2, gibbsish=0.6)
+    run_case("src_gibbsish_small", s, model_cfg(2, True, min_m=3, max_m=25, source=True),
+             mcmc_cfg(area=0.4, m_initial=4, source=0.05), steps=200, seed=44, warmup=False,
+             n_chains=3, gibbsish=0.6)
+    run_case("src_gibbsish_warmup", s, model_cfg(2, True, min_m=3, max_m=25, source=True),
+             mcmc_cfg(area=0.4, m_initial=4, source=0.05), steps=150, seed=45, warmup=True,
+             n_chains=3, gibbsish=0.6)
+    run_case("src_gibbsish_noinh", s, model_cfg(2, False, min_m=3, max_m=25, source=True),
+             mcmc_cfg(area=0.4, m_initial=4, inheritance=0.0, source=0.05), steps=150, seed=46,
+             warmup=False, n_chains=2, gibbsish=0.6)
+    # zone moves redraw all 951 x 35 sources (33 k tape items each): few steps, mostly gibbsish
+    run_case("src_gibbsish_sim", d3, model_cfg(2, True, min_m=3, max_m=120, source=True),
+             mcmc_cfg(area=0.5, source=0.0), steps=24, seed=47, warmup=False, n_chains=1,
+             gibbsish=6.0)
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "gibbsish":
+        gibbsish_cases()
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "geo":
         geo_cases()
         return

@@ -58,8 +58,8 @@ def test_tape_replay_matches_reference(gpu_available, case):
     prop = st.proposed.cpu().numpy()
     for b in range(st.B):
         ops = fx["step_op"][b]
-        np.testing.assert_array_equal(prop[b, :7], np.bincount(ops, minlength=8)[:7])
-        np.testing.assert_array_equal(acc[b, :7], np.bincount(ops[fx["step_accept"][b]], minlength=8)[:7])
+        np.testing.assert_array_equal(prop[b, :8], np.bincount(ops, minlength=8)[:8])
+        np.testing.assert_array_equal(acc[b, :8], np.bincount(ops[fx["step_accept"][b]], minlength=8)[:8])
 
 
 @pytest.mark.parametrize("case", MH_CASES[:2])
@@ -318,3 +318,40 @@ def test_gamma_generator_distribution(gpu_available, alpha):
     eng._lib.sbz_draw_gamma(eng.ctx, n, a.ctypes.data_as(ctypes.c_void_p), 12345 + int(alpha * 10),
                             out2.ctypes.data_as(ctypes.c_void_p))
     np.testing.assert_array_equal(out, out2)
+
+
+@pytest.mark.parametrize("case", ["mh_gibbsish_small", "mh_gibbsish_sim", "mh_small_geo", "mh_small_priors"])
+def test_philox_gibbsish_invariants(gpu_available, case):
+    """gibbsish_sample_zones (zone_sampling.py:619-702) under Philox draws, its weight set to the
+    zone moves' total, with the fixture's priors ('counts' and uniform zone size; the geo prior's
+    last-zone MST): zones stay disjoint and within [MIN_M, max_size], the tracked ll equals a fresh
+    evaluation, the carried prior the full prior, and the trajectory does not depend on the
+    planning depth of the parameter moves around it."""
+    import torch
+    fx = dict(load_golden(case))
+    probs = fx["op_probs"].copy()
+    probs[7] = probs[:3].sum()
+    fx["op_probs"] = probs
+    runs = []
+    for la in (1, 24):
+        eng, smp, st = _setup(fx, {"mh_lookahead": la})
+        out = smp.run(st, 1500, fx["max_size"], fx["p_grow_connected"], seed=515, chain_id0=2, trace=True)
+        torch.cuda.synchronize()
+        assert out["status"].cpu().numpy().tolist() == [0] * st.B
+        s = st.to_numpy()
+        runs.append((out["op"].cpu().numpy(), out["accept"].cpu().numpy(), out["ll"].cpu().numpy(), s))
+        Z = int(fx["n_zones"])
+        for b in range(st.B):
+            sizes = np.bincount(s["zone_of_site"][b][s["zone_of_site"][b] < 255], minlength=Z)
+            assert np.all(sizes >= int(fx["min_size"])) and np.all(sizes <= fx["max_size"][b])
+        fresh = st.refresh_ll().cpu().numpy()
+        assert np.max(np.abs(s["ll"] - fresh) / np.abs(fresh)) <= REL_TOL
+        full = prior_spec(fx).log_prior(s["zone_of_site"], s["p_global"], s.get("p_fam"), fx["states"],
+                                        Z, bool(fx["inheritance"]))
+        np.testing.assert_allclose(s["prior"], full, rtol=1e-12, atol=1e-12)
+        gib = runs[-1][0] == 7
+        assert gib.sum() > 100
+        if case.startswith("mh_gibbsish"):
+            assert (gib & (runs[-1][1] != 0)).sum() > 10  # accepted gibbsish moves
+    for a, b in zip(runs[0][:3], runs[1][:3]):
+        np.testing.assert_array_equal(a, b)

@@ -238,3 +238,44 @@ def test_source_host_form_replays_reference(gpu_available, home):
     dev = st.to_numpy()
     for k in ("zone_of_site", "w", "p_global", "p_zones", "source") + (("p_fam",) if inh else ()):
         np.testing.assert_array_equal(host[k], dev[k], err_msg=k)
+
+
+@pytest.mark.parametrize("case", ["mh_src_gibbsish_small", "mh_src_gibbsish_warmup", "mh_src_geo"])
+def test_source_philox_gibbsish_invariants(gpu_available, case, src_home):
+    """gibbsish_sample_zones with source resampling of the available sites, Philox draws (weight
+    set to the zone moves' total where the fixture has none): sources only from components the
+    site has, zones within [MIN_M, max_size], tracked ll = a fresh evaluation, carried prior =
+    the full prior (geo prior's last-zone MST included), reproducible."""
+    import torch
+    fx = dict(load_golden(case))
+    probs = fx["op_probs"].copy()
+    if probs[7] == 0:
+        probs[7] = probs[:3].sum()
+    fx["op_probs"] = probs
+    finals = []
+    for _ in range(2):
+        eng, smp, st = _setup(fx, src_home)
+        out = smp.run(st, 1200, fx["max_size"], fx["p_grow_connected"], seed=313, trace=True)
+        torch.cuda.synchronize()
+        assert out["status"].cpu().numpy().tolist() == [0] * st.B
+        s = st.to_numpy()
+        finals.append(s)
+    src = s["source"]
+    in_zone = s["zone_of_site"] < 255
+    assert not np.any((src == 1) & ~in_zone[:, :, None])
+    in_fam = fx["fam_of_site"] < 255
+    assert not np.any((src == 2) & ~in_fam[None, :, None])
+    Z = int(fx["n_zones"])
+    for b in range(st.B):
+        sizes = np.bincount(s["zone_of_site"][b][s["zone_of_site"][b] < 255], minlength=Z)
+        assert np.all(sizes >= int(fx["min_size"])) and np.all(sizes <= fx["max_size"][b])
+    fresh = st.refresh_ll().cpu().numpy()
+    assert np.max(np.abs(s["ll"] - fresh) / np.abs(fresh)) <= REL_TOL
+    full = prior_spec(fx).log_prior(s["zone_of_site"], s["p_global"], s.get("p_fam"), fx["states"],
+                                    Z, bool(fx["inheritance"]))
+    np.testing.assert_allclose(s["prior"], full, rtol=1e-12, atol=1e-12)
+    ops = out["op"].cpu().numpy()
+    assert (ops == 7).sum() > 50
+    assert ((ops == 7) & (out["accept"].cpu().numpy() != 0)).sum() > 5
+    for k in finals[0]:
+        np.testing.assert_array_equal(finals[0][k], finals[1][k], err_msg=k)

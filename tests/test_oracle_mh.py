@@ -69,3 +69,22 @@ def test_fixtures_cover_the_prior_types():
         counts_g += "prior_alpha_global" in fx
         counts_f += "prior_alpha_fam" in fx
     assert sizes == {0, 1, 2} and counts_g >= 2 and counts_f >= 2
+
+
+def test_fixtures_cover_gibbsish_sample_zones():
+    """gibbsish_sample_zones (zone_sampling.py:619-702; weight 0 in the reference's own operator
+    table, so captured with a non-zero weight): accepted and rejected moves in mixture and source
+    mode, ZoneMCMC and ZoneMCMCWarmup, and networks with more than 100 available sites."""
+    kinds = {}
+    for case in MH_CASES:
+        fx = load_golden(case)
+        g = fx["step_op"] == 7
+        if not g.any():
+            continue
+        key = (bool(fx["sample_source"]), bool(fx["warmup"]), fx["obs"].shape[0] > 100)
+        acc, n = kinds.get(key, (0, 0))
+        kinds[key] = (acc + int(np.sum(g & fx["step_accept"])), n + int(np.sum(g)))
+    for key in [(False, False, False), (False, True, False), (False, False, True),
+                (True, False, False), (True, True, False), (True, False, True)]:
+        assert key in kinds and kinds[key][0] > 5, (key, kinds)
+    assert any(acc < n for acc, n in kinds.values())
