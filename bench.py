@@ -161,6 +161,24 @@ def pmc_traffic(args, B):
     return None, None
 
 
+def pmc_kernel_traffic(args, B, prefix):
+    """HBM bytes per launch of the kernel whose name starts with `prefix`, from the newest
+    committed PMC summary of this workload that holds it (tools/pmc.sh runs every leg's kernels)."""
+    import glob
+    here = os.path.dirname(os.path.abspath(__file__))
+    for fn in sorted(glob.glob(os.path.join(here, "profiles", "r*_pmc.json")), reverse=True):
+        try:
+            d = json.load(open(fn))
+        except (OSError, ValueError):
+            continue
+        if d.get("_meta", {}).get("workload_key") != workload_key(args, B):
+            continue
+        for k, v in d.get("_per_kernel", {}).items():
+            if k.startswith(prefix):
+                return v["traffic_bytes"], os.path.relpath(fn, here)
+    return None, None
+
+
 def pmc_secondary(args, B):
     """The binding on-chip resources of the dominant kernel, from the same committed PMC summary
     as `traffic` (its average counters per launch): the LDS array's busy share of the CU cycles
@@ -689,10 +707,13 @@ def source_lik_leg(args, eng, gen, dev, stream, rank, world):
     P, D, per_launch = algorithmic_bytes(a, B, True)
     launch_s = secs / K
     del pool
+    traffic, traffic_src = pmc_kernel_traffic(args, B, "lik_source_rc_kernel")
     return {"evals_per_sec": B * K * world / secs, "launch_us": launch_s * 1e6,
             "bytes_per_eval": P + D / B, "bytes_per_launch": per_launch,
             "achieved_GBs": per_launch / launch_s / 1e9,
             "frac": per_launch / launch_s / 1e9 / HBM_PEAK_GBS, "steps": K,
+            "traffic": traffic, "traffic_source": traffic_src,
+            "traffic_over_algorithmic": traffic / per_launch if traffic else None,
             "kernels": eng.last_kernels()}
 
 

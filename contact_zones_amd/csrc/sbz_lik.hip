@@ -51,6 +51,17 @@ constexpr int ZR = 2;        // zone classes per lane held in registers
 constexpr int MIX_WAVES = SBZ_MIX_WAVES; // launch bound of the dense kernel: waves per SIMD
 constexpr int RN = 4;        // product chains checked and renormalised once per RN features
 constexpr int GIF = 16;      // table reads in flight per wave (scheduling barrier every GIF)
+// Gathers: table reads issued per group before their products (0: one read per multiply, as in
+// round 3).  A/B on one box (profiles/r04_gather_groups.txt, us per 256-chain launch): the dense
+// kernel at C = 3 is equal within 0.5 % for 0 / 8 / 16 (and at 2 waves per SIMD with 32 reads in
+// flight), at C = 2 (cfg5 without families) 59.3 -> 55.5 with 8; the source kernel 121.3 -> 120.0
+// with 16.
+#ifndef SBZ_GTREE
+#define SBZ_GTREE 8
+#endif
+#ifndef SBZ_SRC_GTREE
+#define SBZ_SRC_GTREE 16
+#endif
 #ifndef SBZ_LIK_FMA
 #define SBZ_LIK_FMA 1  // (A/B only) 0: the table entries in the reference's unfused operation order
 #endif
@@ -482,14 +493,41 @@ __global__ __launch_bounds__(WAVE, MIX_WAVES) void lik_mixture_kernel(LikArgs a)
             return bs + (XS8 ? xb : (xb << 3));
         };
         if (!wide) {
+#if SBZ_GTREE
+            if constexpr (SPL >= 8) {
+                // groups of GT table reads issued back to back (sched_group_barrier: left alone,
+                // the compiler interleaves each read with its multiply and a wait, ~4 reads in
+                // flight), each half of a group multiplied as a tree into chains 2q and 2q + 1
+                constexpr int GT = SPL < SBZ_GTREE ? SPL : SBZ_GTREE, H = GT / 2;
 #pragma unroll
-            for (int k = 0; k < NO; k++)
+                for (int g = 0; g < SPL; g += GT) {
+                    double v[GT];
 #pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    m[k & 3] *= t.at(cell_at(4 * k + j));
-                    // <= GIF reads in flight
-                    if (j == 3 && (k & (GIF / 4 - 1)) == GIF / 4 - 1) __builtin_amdgcn_sched_barrier(0);
+                    for (int i = 0; i < GT; i++) v[i] = t.at(cell_at(g + i));
+                    __builtin_amdgcn_sched_group_barrier(0x0100, GT, 0);  // the GT DS reads first
+#pragma unroll
+                    for (int h = H / 2; h >= 1; h >>= 1)
+#pragma unroll
+                        for (int i = 0; i < h; i++) {
+                            v[i] = v[i] * v[i + h];
+                            v[H + i] = v[H + i] * v[H + i + h];
+                        }
+                    m[(2 * (g / GT)) & 3] *= v[0];
+                    m[(2 * (g / GT) + 1) & 3] *= v[H];
+                    __builtin_amdgcn_sched_barrier(0);
                 }
+            } else
+#endif
+            {
+#pragma unroll
+                for (int k = 0; k < NO; k++)
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        m[k & 3] *= t.at(cell_at(4 * k + j));
+                        // <= GIF reads in flight
+                        if (j == 3 && (k & (GIF / 4 - 1)) == GIF / 4 - 1) __builtin_amdgcn_sched_barrier(0);
+                    }
+            }
             if ((f - fa) % RN == RN - 1) flush();
         } else {
             // untamed inputs: renormalise after every factor (exact for any normal double)
@@ -884,13 +922,38 @@ __global__ __launch_bounds__(WAVE, SBZ_SRC_RC_WAVES) void lik_source_rc_kernel(L
             return rr * row_bytes + (XS8 ? xb : (xb << 3));
         };
         if (!wide) {
+#if SBZ_SRC_GTREE
+            if constexpr (SPL >= 8) {  // grouped reads and tree products, as lik_mixture_kernel
+                constexpr int GT = SPL < SBZ_SRC_GTREE ? SPL : SBZ_SRC_GTREE, H = GT / 2;
 #pragma unroll
-            for (int k = 0; k < NO; k++)
+                for (int g = 0; g < SPL; g += GT) {
+                    double v[GT];
 #pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    m[k & 3] *= *reinterpret_cast<const double *>(lds + addr(k, j));
-                    if (j == 3 && (k & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+                    for (int i = 0; i < GT; i++)
+                        v[i] = *reinterpret_cast<const double *>(lds + addr((g + i) >> 2, (g + i) & 3));
+                    __builtin_amdgcn_sched_group_barrier(0x0100, GT, 0);
+#pragma unroll
+                    for (int h = H / 2; h >= 1; h >>= 1)
+#pragma unroll
+                        for (int i = 0; i < h; i++) {
+                            v[i] = v[i] * v[i + h];
+                            v[H + i] = v[H + i] * v[H + i + h];
+                        }
+                    m[(2 * (g / GT)) & 3] *= v[0];
+                    m[(2 * (g / GT) + 1) & 3] *= v[H];
+                    __builtin_amdgcn_sched_barrier(0);
                 }
+            } else
+#endif
+            {
+#pragma unroll
+                for (int k = 0; k < NO; k++)
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        m[k & 3] *= *reinterpret_cast<const double *>(lds + addr(k, j));
+                        if (j == 3 && (k & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+                    }
+            }
             if ((f - fa) % RN == RN - 1) flush();
         } else {
             flush();
