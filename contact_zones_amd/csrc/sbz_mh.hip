@@ -31,19 +31,6 @@
 
 namespace sbz {
 
-#ifndef SBZ_MH_STAMP
-#define SBZ_MH_STAMP 0  // diagnostic builds only: trace_ll holds the shader cycles of phase k (1 move
-                        // draw, 2 proposal, 3 delta, 4 accept / apply, 5 whole step; sub-phases of a
-                        // parameter move: 6 wait for the altered pair, 7 Dirichlet draw, 8 lgamma /
-                        // log stage, 9 exp / log to the end of 2, 10 column store + weights,
-                        // 11 table build, 12 gathers + reductions; 13-17 the plan stages A-E,
-                        // 0 on steps that make no plans) instead of ll
-#endif
-#ifndef SBZ_MH_ABLATE
-#define SBZ_MH_ABLATE 0  // diagnostic builds only (wrong results): 1 = no parameter-move delta,
-                         // 2 = no Dirichlet proposal math, 4 = no zone-move delta
-#endif
-
 namespace {
 
 // Philox mode: step t of a launch draws its uniforms from the counter window
@@ -540,13 +527,12 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
     // normalised weights before (nwp[0..15]) and after (nwp[16..31]) the move, or null: computed
     // here into nw.
     auto delta_param = [&](const double *cl, const double *nwp, int f, int comp, int row, int ia, int ib,
-                           double va, double vb, uint32_t (&o)[OB], uint64_t *stamps) {
+                           double va, double vb, uint32_t (&o)[OB]) {
         if (!nwp) {
             if (tid < 8) norm_w(cl + (1 + Z + Fam) * S, comp, ia, ib, va, vb, tid & 3, tid >> 2, nw + tid * 4);
             bsync();
             nwp = nw;
         }
-        if (stamps) stamps[0] = __builtin_amdgcn_s_memtime();
         // tables: entry e = cls * S1 + x (zone class cls / FamC, family class cls % FamC; the
         // neutral row cls = ncls).  Thread tid takes e = tid + NT u, two entries at a time with the
         // LDS reads of both in flight (unconditional, valid indices; selects discard).
@@ -592,7 +578,6 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                 }
         }
         const bool wid = block_sum_i(wide) != 0;  // (its barrier publishes the tables)
-        if (stamps) stamps[1] = __builtin_amdgcn_s_memtime();
         // gathers: position p = 256 k + 4 lane + j of the wave's chunks k = wv + NWV * i, two
         // chunks (8 positions per lane) at a time, all 16 table reads issued together.  Safe tables
         // (every factor 0 or within 2^+-120): the 8 factors multiply as a tree, one renormalisation
@@ -638,15 +623,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                 renorm(mn, en);
             }
         }
-        if (stamps) {
-            asm volatile("" ::"v"(mn), "v"(mo));
-            stamps[8] = __builtin_amdgcn_s_memtime();
-        }
         const double r = (log(mn) - log(mo)) + (double)(en - eo) * LN2;
-        if (stamps) {
-            asm volatile("" ::"v"(r));
-            stamps[9] = __builtin_amdgcn_s_memtime();
-        }
         return r;
     };
 
@@ -673,9 +650,8 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
     // util.dirichlet_pdf) on threads k and 32 + k, the 'counts' prior change, and the normalised
     // weights before / after each move on waves 1-3.  A later accepted move patches the columns of
     // the plans it affects (step loop, phase 4), so a step never reloads its column.
-    auto make_plans = [&](int t0, uint64_t *stamps) {
+    auto make_plans = [&](int t0) {
         bsync();  // every wave is done with the previous batch
-        if (stamps) stamps[0] = __builtin_amdgcn_s_memtime();
         const uint32_t k0 = rng.key0, k1 = rng.key1;
         const uint64_t chain = rng.chain;
         const int la = LAe;
@@ -752,7 +728,6 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             pl->fm[k] = fmask;
         }
         bsync();
-        if (stamps) stamps[1] = __builtin_amdgcn_s_memtime();
         {  // (COL) element e = k * ncol + i: unconditional loads with valid indices, then the stores
             const int tot = la * ncol;
             for (int e0 = 0; e0 < tot; e0 += 8 * NT) {
@@ -769,7 +744,6 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             }
         }
         bsync();
-        if (stamps) stamps[2] = __builtin_amdgcn_s_memtime();
         if (tid < la && pl->comp[tid] >= 0) {  // (A2)
             const int k = tid, comp = pl->comp[k];
             const double c0 = plcol[k * ncol + pl->ci0[k]], c1 = plcol[k * ncol + pl->ci1[k]];
@@ -812,7 +786,6 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             pl->nv1[k] = raw ? n1 : n1 * pl->sum[k];
         }
         bsync();
-        if (stamps) stamps[3] = __builtin_amdgcn_s_memtime();
         {  // (D) dirichlet_proposal2's terms {a0, a1, a0 + a1, b0, b1, b0 + b1, n0, n1, w0, w1}
             const int k = tid / 10, q = tid - 10 * k;
             if (k < la && pl->comp[k] >= 0) {
@@ -825,7 +798,6 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             }
         }
         bsync();
-        if (stamps) stamps[4] = __builtin_amdgcn_s_memtime();
         {  // (E) -(sum gammaln(a) - gammaln(sum a)) + sum xlogy(a - 1, x); q = exp, log q
             const int kk = tid & 31, g = tid >> 5;
             if (tid < 64 && kk < la && pl->comp[kk] >= 0) {
@@ -863,7 +835,6 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             }
         }
         bsync();
-        if (stamps) stamps[5] = __builtin_amdgcn_s_memtime();
         plan_t0 = t0;
     };
 
@@ -881,17 +852,12 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
     // per-operator counts: lane op counts operator op's proposals / acceptances (every wave alike)
     int cnt_prop = 0, cnt_acc = 0;
     for (int step = 0; step < a.n_steps; step++) {
-        uint64_t tph[22];  // SBZ_MH_STAMP builds only
-        if (SBZ_MH_STAMP)
-            for (int q = 10; q < 20; q++) tph[q] = 0;  // plan stages: 0 on steps without plans
-        tph[0] = SBZ_MH_STAMP ? __builtin_amdgcn_s_memtime() : 0;
         if (rng.bad || broken) break;
         if (philox) rng.ctr = ctr0 + (uint64_t)step * WIN;
         if (philox && LAe > 1 && step >= plan_t0 + LAe) {
             fence_params();
-            make_plans(step, SBZ_MH_STAMP ? tph + 10 : nullptr);
+            make_plans(step);
         }
-        if (SBZ_MH_STAMP) tph[20] = __builtin_amdgcn_s_memtime();
 #ifdef SBZ_MH_MARK
         asm volatile("; PH1_BEGIN");
 #endif
@@ -922,7 +888,6 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
 #endif
         const bool planned = philox && LAe > 1 && uni(p_ok) != 0;
         const int op = planned ? uni(p_op) : rng.op(a.op_cdf, a.nops);
-        if (SBZ_MH_STAMP) tph[21] = __builtin_amdgcn_s_memtime();
         if (op < 0 || op > GIBBSISH || (op == P_FAMILIES && (C == 2 || Fam == 0)) ||
             ((op <= SWAP || op == GIBBSISH) && Z == 0) || (op == P_ZONES && Z == 0)) {
             broken = true;
@@ -1180,7 +1145,6 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
 #ifdef SBZ_MH_MARK
         asm volatile("; PH1_END");
 #endif
-        if (SBZ_MH_STAMP) tph[1] = __builtin_amdgcn_s_memtime();
         // ---- 2. Dirichlet proposal of the pair (zone_sampling.py:421-438, :537-569)
         if (!(planned && comp >= 0)) fence_params();  // planned steps read no parameters from HBM
         double nv0 = 0.0, nv1 = 0.0;
@@ -1195,7 +1159,6 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             dprior = uni(p_dp);
         } else if (comp >= 0) {
             const double c0 = uni(ldp(base + ia)), c1 = uni(ldp(base + ib));
-            if (SBZ_MH_STAMP) tph[5] = __builtin_amdgcn_s_memtime();
             // the move's column and observations: in flight during the proposal math
             col_load(f, cv);
             obs_load(f, 0, ow);
@@ -1204,8 +1167,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             const double sum = raw ? 1.0 : c0 + c1;
             const double t0 = raw ? c0 : c0 / sum, t1 = raw ? c1 : c1 / sum;
             double u0 = t0, u1 = t1;
-            if (SBZ_MH_ABLATE & 2) log_q = log_q_back = 0.0;
-            else dirichlet_proposal2(rng, t0, t1, prec, u0, u1, log_q, log_q_back, SBZ_MH_STAMP ? tph + 6 : nullptr);
+            dirichlet_proposal2(rng, t0, t1, prec, u0, u1, log_q, log_q_back);
             nv0 = raw ? u0 : u0 * sum;
             nv1 = raw ? u1 : u1 * sum;
             // 'counts' priors: dirichlet_logpdf(p[f, states], alpha) changes only in the two
@@ -1220,22 +1182,20 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             }
         }
 
-        if (SBZ_MH_STAMP) tph[2] = __builtin_amdgcn_s_memtime();
         // ---- 3. delta log-likelihood (one block reduction; it also makes a range-check failure
         // of any thread known to every wave)
         double delta = 0.0;
         if (sa >= 0 || comp >= 0) {
             double part = 0.0;
-            if (sa >= 0 && !(SBZ_MH_ABLATE & 4)) {
+            if (sa >= 0) {
                 part = delta_site(sa, zoa, zna);
                 if (sb >= 0) part = part + delta_site(sb, zna, NONE);
-            } else if (comp >= 0 && !(SBZ_MH_ABLATE & 1)) {
+            } else if (comp >= 0) {
                 // a planned step's column and weights are in plcol / plnw; otherwise staged here
                 if (!planned) col_store(f, cv);
                 part = delta_param(planned ? plcol + pk * ncol : col, planned ? plnw + pk * 32 : nullptr, f, comp,
-                                   row, ia, ib, nv0, nv1, ow, SBZ_MH_STAMP ? tph + 8 : nullptr);
+                                   row, ia, ib, nv0, nv1, ow);
             }
-            if (SBZ_MH_STAMP) tph[18] = __builtin_amdgcn_s_memtime();
             int n_err = 0;
             delta = block_sum_di(part, err != 0 ? 1 : 0, n_err);
             if (n_err != 0) {  // a range check failed: stop before using the move
@@ -1257,7 +1217,6 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             dprior = uni(dprior + (geo_new - geo_cur));
         }
 
-        if (SBZ_MH_STAMP) tph[3] = __builtin_amdgcn_s_memtime();
         // ---- 4. metropolis_hastings_ratio (mcmc_generative.py:331-351, uniform priors)
         bool accept = false;
         if (log_q_back == -INFINITY) {
@@ -1340,18 +1299,6 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             ch.trace_op[t] = (int8_t)op;
             ch.trace_accept[t] = accept ? 1 : 0;
             ch.trace_ll[t] = ll;
-            if (SBZ_MH_STAMP) {
-                tph[4] = __builtin_amdgcn_s_memtime();
-                // phase k = tph[k] - tph[k-1] (1..4); sub-phases: start / end stamp pairs
-                const int k = SBZ_MH_STAMP;
-                // 13..17: make_plans stages A..E (0 on steps without plans)
-                // 18 gather loop, 19 the two logs, 20 logs to the reduction, 21 reduction to the
-                // end of phase 3 (parameter moves)
-                // 22 loop top and plans, 23 plan read and operator, 24 the rest of phase 1
-                const int e_[25] = {0, 1, 2, 3, 4, 4, 5, 6, 7, 2, 8, 9, 3, 11, 12, 13, 14, 15, 16, 17, 18, 3, 20, 21, 1};
-                const int s_[25] = {0, 0, 1, 2, 3, 0, 1, 5, 6, 7, 2, 8, 9, 10, 11, 12, 13, 14, 9, 16, 17, 18, 0, 20, 21};
-                ch.trace_ll[t] = (double)(tph[e_[k]] - tph[s_[k]]);
-            }
         }
         if (ch.trace_zos) {
             uint8_t *tz = ch.trace_zos + ((size_t)b * a.n_steps + step) * N;

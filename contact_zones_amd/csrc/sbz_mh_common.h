@@ -358,13 +358,10 @@ __device__ __forceinline__ double dirichlet_logpdf2(double x0, double x1, double
 // log q as the reference (zone_sampling.py:537-569, util.py dirichlet_pdf); the ten lgamma / log
 // terms of the two densities run at once on lanes 0..9 (same functions, same arguments as
 // dirichlet_logpdf2), then exp and log on lanes 0 / 1.
-// stamps (diagnostic builds, SBZ_MH_STAMP): shader cycles after the draw and after the lgamma stage
 __device__ __forceinline__ void dirichlet_proposal2(Rng &rng, double w0, double w1, double prec, double &n0,
-                                    double &n1, double &log_q, double &log_q_back,
-                                    uint64_t *stamps = nullptr) {
+                                    double &n1, double &log_q, double &log_q_back) {
     const double a0 = 1.0 + prec * w0, a1 = 1.0 + prec * w1;
     rng.dirichlet2(a0, a1, n0, n1);
-    if (stamps) stamps[0] = __builtin_amdgcn_s_memtime();
     const double b0 = 1.0 + prec * n0, b1 = 1.0 + prec * n1;
     const int lane = threadIdx.x & 63;
     const double args[10] = {a0, a1, a0 + a1, b0, b1, b0 + b1, n0, n1, w0, w1};
@@ -377,7 +374,6 @@ __device__ __forceinline__ void dirichlet_proposal2(Rng &rng, double w0, double 
     double v[10];
 #pragma unroll
     for (int i = 0; i < 10; i++) v[i] = readlane_d(r, i);
-    if (stamps) stamps[1] = __builtin_amdgcn_s_memtime();
     // -(sum gammaln(a) - gammaln(sum a)) + sum xlogy(a - 1, x)
     const double tq0 = (a0 - 1.0) == 0.0 ? 0.0 : (a0 - 1.0) * v[6];
     const double tq1 = (a1 - 1.0) == 0.0 ? 0.0 : (a1 - 1.0) * v[7];

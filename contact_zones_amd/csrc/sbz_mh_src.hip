@@ -37,17 +37,6 @@
 
 namespace sbz {
 
-#ifndef SBZ_SRC_STAMP
-#define SBZ_SRC_STAMP 0  // diagnostic builds only: trace_ll holds the shader cycles of phase k (1 op
-                         // draw, 2 operator body, 3 accept to step end, 4 whole step, 5 resample
-                         // loop, 6 resample reductions, 7 zone move: pass_logq, 8 zone move: site
-                         // selection, 9 Gibbs p: counts, 10 Gibbs p: redraw_rows, 11 Gibbs: pass_ll,
-                         // 12 accept + commit, 13 step trailer) instead of ll
-#endif
-#define SRC_TS(i) \
-    do {          \
-        if (SBZ_SRC_STAMP) tph[i] = __builtin_amdgcn_s_memtime(); \
-    } while (0)
 
 namespace {
 
@@ -363,7 +352,6 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     int err = 0;
     long long err_val = 0;
     uint16_t stamp = 0;
-    uint64_t tr0 = 0, tr1 = 0, tr2 = 0;  // SBZ_SRC_STAMP builds only: resample start / loop end / end
 
     // ---- zone-move helpers (as the SAMPLE_SOURCE = false kernel, sbz_mh.hip).  The scans over
     // the sites run in every wave (identical results); the stamps are written by all threads.
@@ -536,7 +524,6 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     // redraw every source from the current sample's posterior into srcb; returns log q (sum log
     // posterior[new source]) and the new log-likelihood
     auto pass_resample = [&](double &log_q_s, double &ll_new) {
-        if (SBZ_SRC_STAMP) tr0 = __builtin_amdgcn_s_memtime();
         ensure_staged();
         LaneRng lr;
         lr.initw(rng, tid);
@@ -560,11 +547,9 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         } else {
             rng.ctr++;
         }
-        if (SBZ_SRC_STAMP) tr1 = __builtin_amdgcn_s_memtime();
         log_q_s = bsum(acc_q.value());
         const double v = bsum(acc_l.value());
         ll_new = bor(zero_w) ? -INFINITY : v;
-        if (SBZ_SRC_STAMP) tr2 = __builtin_amdgcn_s_memtime();
     };
     auto commit_sources = [&]() {
         for (int c = tid; c < (GS ? (int)NFP : NF); c += NT) wsrc(src, c, rsrc(srcb, c));
@@ -721,9 +706,6 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
 
     bool broken = false;
     for (int step = 0; step < a.n_steps; step++) {
-        uint64_t tph[12] = {};  // SBZ_SRC_STAMP builds only
-        tr0 = tr1 = tr2 = 0;
-        SRC_TS(0);
         if (rng.bad || broken) break;
         // rng.op with the CDF in LDS: numpy choice(p), the number of cdf entries <= u
         int op;
@@ -736,7 +718,6 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             for (int k = 0; k < SBZ_N_OPS - 1; k++) i += (k < a.nops - 1 && !(u < cdf3[k])) ? 1 : 0;
             op = uni(i);
         }
-        SRC_TS(1);
         const bool zone_op = op <= SWAP;
         if (!(zone_op || op == GIBBSISH || (op >= G_SOURCES && op <= G_P_FAMILIES)) ||
             ((zone_op || op == GIBBSISH) && Z == 0) ||
@@ -757,7 +738,6 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         if (zone_op) {
             // ---- zone move with source resampling
             const double log_q_back_s = pass_logq();
-            SRC_TS(6);
             log_q = 0.0;
             log_q_back = -INFINITY;
             const int n_free = N - occupied;
@@ -828,7 +808,6 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                     if (sb >= 0) zos[sb] = NONE;
                 }
                 sync();
-                SRC_TS(7);
                 if (a.geo_cost && (zna == Z - 1 || zoa == Z - 1)) {  // the last zone changed
                     geo_new = geo_prior();
                     dprior = uni(dprior + (geo_new - geo_cur));
@@ -1088,7 +1067,6 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                 if (in) atomicAdd(&cnt[f * S + x], 1);
             });
             sync();
-            SRC_TS(8);
             double *base = comp == 0 ? pg : (comp == 1 ? pz + (size_t)row * F * S : pf + (size_t)row * F * S);
             int64_t rpos = rng.pos;
             uint64_t rctr = rng.ctr;
@@ -1104,11 +1082,9 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             // before the parameters are staged)
             if (stg && stg_ok) sync();
             else gsync();
-            SRC_TS(9);
             ll_new = pass_ll(src);
         }
 
-        SRC_TS(2);
         // ---- metropolis_hastings_ratio (mcmc_generative.py:307-318)
         bool accept;
         if (log_q_back == -INFINITY) accept = false;
@@ -1146,7 +1122,6 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             }
             sync();
         }
-        SRC_TS(10);
         if (alias && accept && op != G_SOURCES && op != G_P_GLOBAL && op != G_P_ZONES &&
             op != G_P_FAMILIES) {
             gsync();  // every thread's parameter stores have landed
@@ -1161,25 +1136,11 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                     ch.alias_p_fam[b * Fam * fs + k] = ldp(pf + k);
             alias = 0;
         }
-        if (SBZ_SRC_STAMP) {
-            sync();
-            SRC_TS(3);
-        }
         if (ch.trace_op && tid == 0) {
             const size_t t = (size_t)b * a.n_steps + step;
             ch.trace_op[t] = (int8_t)op;
             ch.trace_accept[t] = accept ? 1 : 0;
             ch.trace_ll[t] = ll;
-            if (SBZ_SRC_STAMP) {
-                tph[11] = tr0;
-                tph[4] = tr1;
-                tph[5] = tr2;
-                // phase k: [end, start] time points
-                constexpr int PE[14] = {0, 1, 2, 3, 3, 4, 5, 6, 7, 8, 9, 2, 10, 3};
-                constexpr int PS[14] = {0, 0, 1, 2, 0, 11, 4, 1, 6, 1, 8, 9, 2, 10};
-                constexpr int k = SBZ_SRC_STAMP;
-                ch.trace_ll[t] = tph[PE[k]] >= tph[PS[k]] && tph[PS[k]] != 0 ? (double)(tph[PE[k]] - tph[PS[k]]) : 0.0;
-            }
         }
 
         if (ch.trace_zos) {

@@ -1,6 +1,9 @@
 #!/bin/bash
 # Build a diagnostic variant of libsbz with extra hipcc defines for the sampler kernel:
-#   tools/build_mh_variant.sh NAME -DSBZ_MH_ABLATE=1 ...
+#   tools/build_mh_variant.sh NAME -DSBZ_MH_MARK ...
+# The phase-stamp (SBZ_MH_STAMP) and ablation (SBZ_MH_ABLATE) instrumentation left the product
+# source in round 4; build those variants from the last revision that has it:
+#   tools/build_rev.sh d12ba3a stK -DSBZ_MH_STAMP=K
 # Output: contact_zones_amd/libsbz_NAME.so (git-ignored; travels to the GPU box with gpurun).
 set -e
 cd "$(dirname "$0")/../contact_zones_amd/csrc"

@@ -1,5 +1,6 @@
 #!/bin/bash
-# Sampler phase stamps (SBZ_MH_STAMP builds, tools/build_mh_variant.sh stK -DSBZ_MH_STAMP=K): mean
+# Sampler phase stamps (SBZ_MH_STAMP builds of revision d12ba3a, the last with the instrumentation:
+# tools/build_rev.sh d12ba3a stK -DSBZ_MH_STAMP=K): mean
 # shader cycles per step of each phase / sub-phase, by operator, at the bench's cfg5 shape.
 mkdir -p gpurun_out
 for k in ${KS:-1 2 3 4 5 6 7 8 9 10 11 12}; do

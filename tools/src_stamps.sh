@@ -1,6 +1,6 @@
 #!/bin/bash
-# Source-mode sampler phase stamps (SBZ_SRC_STAMP builds, tools/build_src_variant.sh sst<k>
-# -DSBZ_SRC_STAMP=<k>; KS selects which were built): the production library first, then each k,
+# Source-mode sampler phase stamps (SBZ_SRC_STAMP builds of revision d12ba3a, the last with the
+# instrumentation: tools/build_rev.sh d12ba3a sst<k> -DSBZ_SRC_STAMP=<k>; KS selects which were built): the production library first, then each k,
 # on the Balkan- and South-America-shaped synthetic legs.
 mkdir -p gpurun_out
 : > gpurun_out/src_stamps.txt
