@@ -31,6 +31,17 @@
 
 namespace sbz {
 
+// A/B knobs (profiles/r04_sampler_micro.txt): loads per thread and round of the planned columns
+// (16 makes cfg5's one round trip, but the wider unroll costs the rest of the kernel registers:
+// 5.25 vs 5.09 us per step), and one log of mn / mo instead of two in a parameter move's delta
+// (5.05 vs 5.25)
+#ifndef SBZ_MH_COLR
+#define SBZ_MH_COLR 8
+#endif
+#ifndef SBZ_MH_LOG1
+#define SBZ_MH_LOG1 1
+#endif
+
 namespace {
 
 // Philox mode: step t of a launch draws its uniforms from the counter window
@@ -623,7 +634,11 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                 renorm(mn, en);
             }
         }
+#if SBZ_MH_LOG1
+        const double r = log(mn / mo) + (double)(en - eo) * LN2;  // one log: mn, mo in [0.5, 1)
+#else
         const double r = (log(mn) - log(mo)) + (double)(en - eo) * LN2;
+#endif
         return r;
     };
 
@@ -730,16 +745,17 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
         bsync();
         {  // (COL) element e = k * ncol + i: unconditional loads with valid indices, then the stores
             const int tot = la * ncol;
-            for (int e0 = 0; e0 < tot; e0 += 8 * NT) {
-                double v[8];
+            constexpr int RC = SBZ_MH_COLR;
+            for (int e0 = 0; e0 < tot; e0 += RC * NT) {
+                double v[RC];
 #pragma unroll
-                for (int j = 0; j < 8; j++) {
+                for (int j = 0; j < RC; j++) {
                     const int e = min(e0 + j * NT + tid, tot - 1);
                     const int k = e / ncol;
                     v[j] = ldp(col_src(pl->f[k], e - k * ncol));
                 }
 #pragma unroll
-                for (int j = 0; j < 8; j++)
+                for (int j = 0; j < RC; j++)
                     if (e0 + j * NT + tid < tot) plcol[e0 + j * NT + tid] = v[j];
             }
         }
