@@ -544,6 +544,11 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             bsync();
             nwp = nw;
         }
+        // the class rows of the wave's first two chunks, read before the tables are built (they
+        // do not depend on them), so the gathers start one LDS round trip earlier
+        const int nci0 = (nch - wv + NWV - 1) / NWV;
+        const uint4 ra0 = *reinterpret_cast<const uint4 *>(rowp + min(wv, nch - 1) * 256 + 4 * lane);
+        const uint4 rb0 = *reinterpret_cast<const uint4 *>(rowp + min(wv + NWV * (nci0 > 1 ? 1 : 0), nch - 1) * 256 + 4 * lane);
         // tables: entry e = cls * S1 + x (zone class cls / FamC, family class cls % FamC; the
         // neutral row cls = ncls).  Thread tid takes e = tid + NT u, two entries at a time with the
         // LDS reads of both in flight (unconditional, valid indices; selects discard).
@@ -595,7 +600,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
         // per pair of chunks; otherwise renormalise after every factor.
         double mn = 1.0, mo = 1.0;
         int en = 0, eo = 0;
-        const int nci = (nch - wv + NWV - 1) / NWV;  // this wave's chunks
+        const int nci = nci0;  // this wave's chunks
         const unsigned char *tbo = reinterpret_cast<const unsigned char *>(tabo);
         const unsigned char *tbn = reinterpret_cast<const unsigned char *>(tabn);
         const uint32_t xsh = a.xs8 ? 0u : 3u;
@@ -603,8 +608,8 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             if (i0 > 0 && (i0 & (OB - 1)) == 0) obs_load(f, i0, o);
             const bool two = i0 + 1 < nci;
             const int ka = wv + NWV * i0, kb = wv + NWV * (two ? i0 + 1 : i0);
-            const uint4 ra = *reinterpret_cast<const uint4 *>(rowp + ka * 256 + 4 * lane);
-            const uint4 rb = *reinterpret_cast<const uint4 *>(rowp + kb * 256 + 4 * lane);
+            const uint4 ra = i0 == 0 ? ra0 : *reinterpret_cast<const uint4 *>(rowp + ka * 256 + 4 * lane);
+            const uint4 rb = i0 == 0 ? rb0 : *reinterpret_cast<const uint4 *>(rowp + kb * 256 + 4 * lane);
             const uint32_t oa = (i0 & 2) ? o[2] : o[0], ob = (i0 & 2) ? o[3] : o[1];
             const uint32_t r8[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
             double vo[8], vn[8];
