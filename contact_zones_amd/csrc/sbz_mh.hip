@@ -1012,6 +1012,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             }
             gib = true;
             gz = z;
+            fence_params();  // the marginals below read parameters: a pending accepted store first
             const uint64_t slot = ctr0 + (uint64_t)step * WIN;
             auto site_u = [&](int64_t p0, int k, int sl) {
                 return rng.tape ? rng.tape[p0 + k] : site_uniform(rng.key0, rng.key1, rng.chain, slot + sl, (uint32_t)k);
