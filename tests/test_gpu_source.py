@@ -279,3 +279,26 @@ def test_source_philox_gibbsish_invariants(gpu_available, case, src_home):
     assert ((ops == 7) & (out["accept"].cpu().numpy() != 0)).sum() > 5
     for k in finals[0]:
         np.testing.assert_array_equal(finals[0][k], finals[1][k], err_msg=k)
+
+
+def test_concurrent_contexts_match_sequential(gpu_available):
+    """Two contexts sampling on their own HIP streams at once (the bench's concurrent K sweep)
+    give exactly the states they give when run one after the other."""
+    import torch
+    cases = ["mh_src_sa_z1", "mh_src_sa_z6"]
+
+    def run(concurrent):
+        setups = [_setup(load_golden(c)) for c in cases]
+        streams = [torch.cuda.Stream() for _ in cases] if concurrent else [torch.cuda.current_stream()] * 2
+        torch.cuda.synchronize()
+        for (eng, smp, st), c, s in zip(setups, cases, streams):
+            fx = load_golden(c)
+            with torch.cuda.stream(s):
+                smp.run(st, 800, fx["max_size"], fx["p_grow_connected"], seed=21, chain_id0=5)
+        torch.cuda.synchronize()
+        return [st.to_numpy() for _, _, st in setups]
+
+    seq, con = run(False), run(True)
+    for a, b in zip(seq, con):
+        for k in a:
+            np.testing.assert_array_equal(a[k], b[k], err_msg=k)
