@@ -33,13 +33,14 @@ namespace sbz {
 
 // A/B knobs (profiles/r04_sampler_micro.txt): loads per thread and round of the planned columns
 // (16 makes cfg5's one round trip, but the wider unroll costs the rest of the kernel registers:
-// 5.25 vs 5.09 us per step), and one log of mn / mo instead of two in a parameter move's delta
-// (5.05 vs 5.25)
+// 5.25 vs 5.09 us per step).  A parameter move's delta takes one log of mn / mo (5.05 us per
+// step against 5.25 for two library logs; two flog()s: 5.01 against 4.85 for one library log,
+// profiles/r04_flog_ab.txt); SBZ_MH_DLOG picks flog or the library log for it.
 #ifndef SBZ_MH_COLR
 #define SBZ_MH_COLR 8
 #endif
-#ifndef SBZ_MH_LOG1
-#define SBZ_MH_LOG1 1
+#ifndef SBZ_MH_DLOG
+#define SBZ_MH_DLOG 1
 #endif
 
 namespace {
@@ -427,7 +428,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             renorm(mo, eo);
             renorm(mn, en);
         }
-        return (log(mn) - log(mo)) + (double)(en - eo) * LN2;  // this thread's part (block_sum)
+        return (flog(mn) - flog(mo)) + (double)(en - eo) * LN2;  // this thread's part (block_sum)
     };
 
     // gibbsish_sample_zones (zone_sampling.py:644-665): site s's log marginal likelihood with
@@ -453,8 +454,8 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             renorm(mw, ew);
             renorm(mo, eo);
         }
-        lw = wave_sum(log(mw) + (double)ew * LN2);
-        lwo = wave_sum(log(mo) + (double)eo * LN2);
+        lw = wave_sum(flog(mw) + (double)ew * LN2);
+        lwo = wave_sum(flog(mo) + (double)eo * LN2);
     };
     double *gib_lw = reinterpret_cast<double *>(lds + L.gib);  // [N] per available site
     double *gib_lwo = gib_lw + N;                               // [N]
@@ -639,10 +640,10 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                 renorm(mn, en);
             }
         }
-#if SBZ_MH_LOG1
-        const double r = log(mn / mo) + (double)(en - eo) * LN2;  // one log: mn, mo in [0.5, 1)
+#if SBZ_MH_DLOG
+        const double r = flog(fdiv_pos(mn, mo)) + (double)(en - eo) * LN2;  // mn, mo in [0.5, 1)
 #else
-        const double r = (log(mn) - log(mo)) + (double)(en - eo) * LN2;
+        const double r = log(mn / mo) + (double)(en - eo) * LN2;
 #endif
         return r;
     };
@@ -1354,7 +1355,10 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
     }
 }
 
-constexpr int MH_WAVES = 4;  // waves per chain (one workgroup per chain)
+#ifndef SBZ_MH_WAVES
+#define SBZ_MH_WAVES 4  // A/B builds only (tools/build_mh_variant.sh NAME -DSBZ_MH_WAVES=8)
+#endif
+constexpr int MH_WAVES = SBZ_MH_WAVES;  // waves per chain (one workgroup per chain)
 
 }  // namespace
 

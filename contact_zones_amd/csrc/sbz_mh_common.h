@@ -110,6 +110,67 @@ __device__ __forceinline__ void renorm(double &m, int &e) {
     m = __builtin_amdgcn_frexp_mant(m);
 }
 
+// log(x) in ~30 dependent f64 operations: x = m 2^e with m in [sqrt(1/2), sqrt(2)), log m =
+// 2 atanh(s), s = (m - 1) / (m + 1) (v_rcp_f64, two Newton steps and the residual of m + 1's
+// rounding), the atanh series to s^21, e ln 2 in two parts.  <= 1.43 ulp (mean 0.31 ulp against a
+// long-double log over 1e7 arguments, denormals included); 0 -> -inf, +inf -> +inf, x < 0 or NaN
+// -> NaN.  The library's log is correctly rounded through double-double steps: ~670 cycles of
+// latency on gfx950 against ~550 (tools/gamma_lat.hip, profiles/r04_gamma_lat.txt; a dependent
+// f64 operation costs ~18 cycles).  (An Estrin form of the series trips a gfx950 code-generation
+// error in mh_src_kernel<2, false, 4> with ROCm 7.2's compiler: "V_CMP_NE_U32_e32 0,
+// $src_shared_base", an illegal operand after post-RA pseudo expansion.)  Used where a log sits on a step's critical path and the value is
+// a likelihood / acceptance term (the tape replays' decisions and the 1e-9 parity bar are
+// unaffected); SBZ_FLOG=0 builds (A/B only) use the library log everywhere.
+#ifndef SBZ_FLOG
+#define SBZ_FLOG 1
+#endif
+__device__ __forceinline__ double flog(double x) {
+#if SBZ_FLOG
+    double m = __builtin_amdgcn_frexp_mant(x);
+    int e = __builtin_amdgcn_frexp_exp(x);
+    const bool lo = m < 0.70710678118654752440;
+    m = lo ? m * 2.0 : m;
+    e = lo ? e - 1 : e;
+    const double f = m - 1.0, d = m + 1.0;  // f exact
+    const double dl = m - (d - 1.0);        // m + 1 = d + dl exactly
+    double r = __builtin_amdgcn_rcp(d);
+    r = fma(fma(-d, r, 1.0), r, r);
+    r = fma(fma(-d, r, 1.0), r, r);
+    const double s0 = f * r;
+    const double sv = fma(r, fma(-s0, d, f) - s0 * dl, s0);
+    const double z = sv * sv;
+    double p = 2.0 / 21.0;
+    p = fma(p, z, 2.0 / 19.0);
+    p = fma(p, z, 2.0 / 17.0);
+    p = fma(p, z, 2.0 / 15.0);
+    p = fma(p, z, 2.0 / 13.0);
+    p = fma(p, z, 2.0 / 11.0);
+    p = fma(p, z, 2.0 / 9.0);
+    p = fma(p, z, 2.0 / 7.0);
+    p = fma(p, z, 2.0 / 5.0);
+    p = fma(p, z, 2.0 / 3.0);
+    const double lm = fma(sv * z, p, 2.0 * sv);
+    const double de = (double)e;
+    double v = fma(de, 6.93147180369123816490e-01, fma(de, 1.90821492927058770002e-10, lm));
+    v = x == 0.0 ? -INFINITY : v;
+    v = x == INFINITY ? INFINITY : v;
+    return (x < 0.0 || x != x) ? __builtin_nan("") : v;
+#else
+    return log(x);
+#endif
+}
+
+// a / b for normal positive a, b away from the range limits (v_rcp_f64, two Newton steps and
+// one residual correction: <= 1 ulp): ~7 dependent operations against the IEEE sequence's
+// div_scale / div_fmas / div_fixup (~310 cycles, profiles/r04_gamma_lat.txt).
+__device__ __forceinline__ double fdiv_pos(double a, double b) {
+    double r = __builtin_amdgcn_rcp(b);
+    r = fma(fma(-b, r, 1.0), r, r);
+    r = fma(fma(-b, r, 1.0), r, r);
+    const double q = a * r;
+    return fma(r, fma(-b, q, a), q);
+}
+
 // ---------------------------------------------------------------------------------------
 // Random draws (wave-uniform).
 // ---------------------------------------------------------------------------------------
@@ -300,7 +361,7 @@ struct LaneRng {
         const double u1 = 1.0 - u();
         const double u2 = u();
         // cos(2 pi u2) as cospi(2 u2): no large-argument reduction (u2 in [0, 1))
-        return sqrt(-2.0 * log(u1)) * cospi(2.0 * u2);
+        return sqrt(-2.0 * flog(u1)) * cospi(2.0 * u2);
     }
     // Marsaglia-Tsang (alpha >= 1; boosted by u^(1/alpha) below 1), at most 64 rounds (each
     // accepts with probability > 0.95; reaching 64 has probability < 1e-80).  A two-candidate
@@ -318,7 +379,12 @@ struct LaneRng {
             if (v <= 0.0) continue;
             v = v * v * v;
             const double w = u();
-            if (w < 1.0 - 0.0331 * (x * x) * (x * x) || log(w) < 0.5 * x * x + d * (1.0 - v + log(v))) {
+            bool ok = w < 1.0 - 0.0331 * (x * x) * (x * x);
+            if (!ok) {
+                const double lw = flog(w), lv = flog(v);
+                ok = lw < 0.5 * x * x + d * (1.0 - v + lv);
+            }
+            if (ok) {
                 r = d * v;
                 break;
             }

@@ -491,7 +491,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                 m = __builtin_amdgcn_frexp_mant(m);
             }
         }
-        __device__ __forceinline__ double value() const { return log(m) + (double)e * LN2; }
+        __device__ __forceinline__ double value() const { return flog(m) + (double)e * LN2; }
     };
     // sum over observations of log posterior[src] for the current sample (zone_sampling.py:718-722)
     auto pass_logq = [&]() -> double {
@@ -1089,7 +1089,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         bool accept;
         if (log_q_back == -INFINITY) accept = false;
         else if (log_q == -INFINITY) accept = true;
-        else accept = log(rng.real()) < ((ll_new - ll) * 1.0) - (log_q - log_q_back) + dprior;
+        else accept = flog(rng.real()) < ((ll_new - ll) * 1.0) - (log_q - log_q_back) + dprior;
         if (tid == 0) stat[op]++;
         if (accept) {
             if (tid == 0) stat[SBZ_N_OPS + op]++;
