@@ -105,6 +105,17 @@ __device__ __forceinline__ void stp(double *p, double v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// A read of LDS through a local-address-space pointer (ds_read).  A generic-pointer read of an
+// LDS array beside a read of a global array under a uniform select (`staged ? lds[i] :
+// global[i]`) lets the optimiser merge the two into one flat load of a selected pointer: slower
+// than ds_read, and it has the shared aperture base allocated to VCC, whose copy ROCm 7.2's
+// gfx950 back end lowers to an illegal "V_CMP_NE_U32_e32 0, $src_shared_base".  Reading the LDS
+// side through this keeps the two loads apart.
+template <class T>
+__device__ __forceinline__ T lds_rd(const T *p) {
+    return *(const __attribute__((address_space(3))) T *)p;
+}
+
 __device__ __forceinline__ void renorm(double &m, int &e) {
     e += __builtin_amdgcn_frexp_exp(m);
     m = __builtin_amdgcn_frexp_mant(m);
@@ -138,17 +149,13 @@ __device__ __forceinline__ double flog(double x) {
     r = fma(fma(-d, r, 1.0), r, r);
     const double s0 = f * r;
     const double sv = fma(r, fma(-s0, d, f) - s0 * dl, s0);
+    // the series' tail sum_k 2 / (2k + 3) z^k, k = 0..9, by Estrin (4 dependent levels after z)
     const double z = sv * sv;
-    double p = 2.0 / 21.0;
-    p = fma(p, z, 2.0 / 19.0);
-    p = fma(p, z, 2.0 / 17.0);
-    p = fma(p, z, 2.0 / 15.0);
-    p = fma(p, z, 2.0 / 13.0);
-    p = fma(p, z, 2.0 / 11.0);
-    p = fma(p, z, 2.0 / 9.0);
-    p = fma(p, z, 2.0 / 7.0);
-    p = fma(p, z, 2.0 / 5.0);
-    p = fma(p, z, 2.0 / 3.0);
+    const double z2 = z * z, z4 = z2 * z2, z8 = z4 * z4;
+    const double a0 = fma(2.0 / 5.0, z, 2.0 / 3.0), a1 = fma(2.0 / 9.0, z, 2.0 / 7.0);
+    const double a2 = fma(2.0 / 13.0, z, 2.0 / 11.0), a3 = fma(2.0 / 17.0, z, 2.0 / 15.0);
+    const double a4 = fma(2.0 / 21.0, z, 2.0 / 19.0);
+    const double p = fma(a4, z8, fma(fma(a3, z2, a2), z4, fma(a1, z2, a0)));
     const double lm = fma(sv * z, p, 2.0 * sv);
     const double de = (double)e;
     double v = fma(de, 6.93147180369123816490e-01, fma(de, 1.90821492927058770002e-10, lm));

@@ -105,6 +105,15 @@ size_t mh_src_const_bytes(const sbz_dims &d, int C, bool alg, bool alf, bool gcg
            (size_t)d.n_features + 16;
 }
 
+// A/B knobs: the log-likelihood pass reads only the selected component's weight and likelihood
+// (SBZ_SRC_LL1), and the N * F passes are unrolled SBZ_SRC_UNR cells deep
+#ifndef SBZ_SRC_LL1
+#define SBZ_SRC_LL1 1
+#endif
+#ifndef SBZ_SRC_UNR
+#define SBZ_SRC_UNR 1
+#endif
+
 namespace {
 
 // (p, f) of position-major cell i = f * Np + p, advanced by NT cells per step
@@ -216,19 +225,19 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     double *c_gcf = c_gcg + (a.gc_g ? FS : 0);                     // [Fam][F][S] if gc_f
     uint8_t *c_app = reinterpret_cast<uint8_t *>(c_gcf + (a.gc_f ? Fam * FS : 0));  // [F][S]
     uint8_t *c_acnt = c_app + FS;                                                   // [F]
-    auto app_cnt = [&](int f) -> int { return cst ? (int)c_acnt[f] : a.app_cnt[f]; };
-    auto app_list = [&](int f, int j) -> int { return cst ? (int)c_app[f * S + j] : a.app_list[(size_t)f * S + j]; };
+    auto app_cnt = [&](int f) -> int { return cst ? (int)lds_rd(c_acnt + f) : a.app_cnt[f]; };
+    auto app_list = [&](int f, int j) -> int { return cst ? (int)lds_rd(c_app + f * S + j) : a.app_list[(size_t)f * S + j]; };
     // Gibbs prior count of component comp's row `row` at i = f * S + x (1 where none is set)
     auto gcv = [&](int comp, int row, int i) -> double {
-        if (comp == 0 && a.gc_g) return cst ? c_gcg[i] : ldp(a.gc_g + i);
-        if (comp == 2 && a.gc_f) return cst ? c_gcf[(size_t)row * FS + i] : ldp(a.gc_f + (size_t)row * FS + i);
+        if (comp == 0 && a.gc_g) return cst ? lds_rd(c_gcg + i) : ldp(a.gc_g + i);
+        if (comp == 2 && a.gc_f) return cst ? lds_rd(c_gcf + (size_t)row * FS + i) : ldp(a.gc_f + (size_t)row * FS + i);
         return 1.0;
     };
     // 'counts' prior alpha (p_global, p_families) at i, where set
     auto has_al = [&](int comp) { return (comp == 0 && a.alpha_g) || (comp == 2 && a.alpha_f); };
     auto alv = [&](int comp, int row, int i) -> double {
-        if (comp == 0) return cst ? c_alg[i] : ldp(a.alpha_g + i);
-        return cst ? c_alf[(size_t)row * FS + i] : ldp(a.alpha_f + (size_t)row * FS + i);
+        if (comp == 0) return cst ? lds_rd(c_alg + i) : ldp(a.alpha_g + i);
+        return cst ? lds_rd(c_alf + (size_t)row * FS + i) : ldp(a.alpha_f + (size_t)row * FS + i);
     };
 
     uint8_t *gzos = ch.zone_of_site + (size_t)b * N;
@@ -460,18 +469,20 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     auto for_cells = [&](auto &&body) {
         if constexpr (!GS) {
             CellWalk cw{tid / F, tid - (tid / F) * F, cdS, cdF, F};
+#pragma unroll SBZ_SRC_UNR
             for (int c = tid; c < NF; c += NT, cw.next()) {
-                const int x = stg ? lobs[c] : a.obs_sm[c];
+                const int x = stg ? lds_rd(lobs + c) : a.obs_sm[c];
                 body(cw.s, cw.f, x, c, c);
             }
         } else {
             PosWalk pw{tid - (tid / Np) * Np, tid / Np, pdP, pdF, Np};
+#pragma unroll SBZ_SRC_UNR
             for (int i = tid; i < (int)NFP; i += NT, pw.next()) {
                 const int p = pw.p, f = pw.f;
                 if (p >= N) continue;
                 const int s = a.perm[p];
                 const int c = s * F + f;
-                const int x = stg ? lobs[c] : a.obs_fm[i] / xdiv;
+                const int x = stg ? lds_rd(lobs + c) : a.obs_fm[i] / xdiv;
                 body(s, f, x, i, c);
             }
         }
@@ -511,13 +522,34 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         ensure_staged();
         LogAcc acc;
         int zero_w = 0;
-        for_cells([&](int s, int f, int x, int g, int) {
-            double l[3], wn[3];
-            terms(s, f, x, l, wn);
-            const int k = rsrc(sv, g);
-            zero_w |= wn[k] == 0.0;
-            acc.add(wn[k] * l[k]);
-        });
+        if (SBZ_SRC_LL1 && stg) {
+            // staged: only the selected component's weight and likelihood, two LDS reads per
+            // cell whose addresses come straight from the cell's bytes (the same products as
+            // terms(): a component the site lacks has weight 0, so its likelihood is irrelevant)
+            for_cells([&](int s, int f, int x, int g, int) {
+                const int k = rsrc(sv, g);
+                const int zc = zos[s], fc = C == 3 ? lfam[s] : 0;
+                const bool na = x >= S;
+                const int xc = na ? 0 : x;
+                const int h = (zc < Z ? 1 : 0) | ((C == 3 && fc > 0) ? 2 : 0);
+                const double wk = lnw[(f * 4 + h) * 3 + k];
+                const int zr = zc < Z ? zc : 0, fr = fc > 0 ? fc - 1 : 0;
+                // lpg, lpz, lpf are consecutive: [F][S], [Z][F][S], [Fam][F][S]
+                const int pi = k == 0 ? f * S + xc
+                                      : (k == 1 ? (F + zr * F + f) * S + xc : (F + Z * F + fr * F + f) * S + xc);
+                const double lk = na ? 1.0 : lpg[pi];
+                zero_w |= wk == 0.0;
+                acc.add(wk * lk);
+            });
+        } else {
+            for_cells([&](int s, int f, int x, int g, int) {
+                double l[3], wn[3];
+                terms(s, f, x, l, wn);
+                const int k = rsrc(sv, g);
+                zero_w |= wn[k] == 0.0;
+                acc.add(wn[k] * l[k]);
+            });
+        }
         const double v = bsum(acc.value());
         return bor(zero_w) ? -INFINITY : v;
     };
@@ -655,7 +687,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             const int x = app_list(f, j);
             double *prow = base + (size_t)f * S;
             // the current value: the staged copy once staged (an exact copy), else the global row
-            const double old = stg_ok ? lbase[(size_t)f * S + x] : ldp(prow + x);
+            const double old = stg_ok ? lds_rd(lbase + (size_t)f * S + x) : ldp(prow + x);
             stp(prow + x, g);
             if (stg) lbase[(size_t)f * S + x] = g;  // the staged copy follows
             if (al) {
@@ -687,7 +719,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     // the source-array index of observation (s, f)
     auto cell_of = [&](int s, int f) -> int { return GS ? f * Np + (int)g_pos[s] : s * F + f; };
     // the observed state of (s, f) (S = NA)
-    auto obs_of = [&](int s, int f) -> int { return stg ? lobs[s * F + f] : a.obs_sm[(size_t)s * F + f]; };
+    auto obs_of = [&](int s, int f) -> int { return stg ? lds_rd(lobs + s * F + f) : a.obs_sm[(size_t)s * F + f]; };
     // the n sites of the list, compacted in ascending order by `keep` (wave 0 writes; every wave
     // gets the count).  Reads of a chunk precede its writes, so the compaction may be in place.
     auto compact = [&](int n, auto &&site_at, auto &&keep) -> int {
@@ -982,7 +1014,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             }
             clear_cnt();
             for_cells([&](int s, int f, int, int g, int) {
-                const bool in = (C == 2 || fixed == 0) ? zos[s] < Z : (stg ? lfam[s] : a.fam_site[s]) > 0;
+                const bool in = (C == 2 || fixed == 0) ? zos[s] < Z : (stg ? lds_rd(lfam + s) : a.fam_site[s]) > 0;
                 if (in) atomicAdd(&cnt[f * C + rsrc(src, g)], 1);
             });
             sync();
@@ -1063,7 +1095,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             for_cells([&](int s, int f, int x, int g, int) {
                 bool in = sub[f] && rsrc(src, g) == comp && x < S;
                 if (comp == 1) in = in && zos[s] == row;
-                if (comp == 2) in = in && (stg ? lfam[s] : a.fam_site[s]) == row + 1;
+                if (comp == 2) in = in && (stg ? lds_rd(lfam + s) : a.fam_site[s]) == row + 1;
                 if (in) atomicAdd(&cnt[f * S + x], 1);
             });
             sync();
