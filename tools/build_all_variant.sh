@@ -8,7 +8,8 @@ name=$1; shift
 TORCH_LIB=$(python -c 'import os,torch;print(os.path.join(os.path.dirname(torch.__file__),"lib"))')
 mkdir -p build_$name
 for f in sbz_api sbz_lik sbz_mh sbz_mh_src; do
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off "$@" -c $f.hip -o build_$name/$f.o &
+  extra=""; [ $f = sbz_mh ] && extra="-mllvm -disable-machine-licm"  # as the Makefile
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off $extra "$@" -c $f.hip -o build_$name/$f.o &
 done
 wait
 g++ -shared -o ../libsbz_$name.so build_$name/sbz_api.o build_$name/sbz_lik.o build_$name/sbz_mh.o build_$name/sbz_mh_src.o \
