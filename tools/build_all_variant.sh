@@ -8,7 +8,7 @@ name=$1; shift
 TORCH_LIB=$(python -c 'import os,torch;print(os.path.join(os.path.dirname(torch.__file__),"lib"))')
 mkdir -p build_$name
 for f in sbz_api sbz_lik sbz_mh sbz_mh_src; do
-  extra=""; [ $f = sbz_mh ] && extra="-mllvm -disable-machine-licm"  # as the Makefile
+  extra=""; [ $f = sbz_mh ] || [ $f = sbz_lik ] && extra="-mllvm -disable-machine-licm"  # as the Makefile
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off $extra "$@" -c $f.hip -o build_$name/$f.o &
 done
 wait

@@ -8,6 +8,6 @@ name=$1; shift
 TORCH_LIB=$(python -c 'import os,torch;print(os.path.join(os.path.dirname(torch.__file__),"lib"))')
 mkdir -p build_$name
 make -s build/sbz_api.o build/sbz_mh.o build/sbz_mh_src.o
-/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off "$@" -c sbz_lik.hip -o build_$name/sbz_lik.o
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -mllvm -disable-machine-licm "$@" -c sbz_lik.hip -o build_$name/sbz_lik.o
 g++ -shared -o ../libsbz_$name.so build/sbz_api.o build_$name/sbz_lik.o build/sbz_mh_src.o build/sbz_mh.o \
     -L$TORCH_LIB -lamdhip64 -Wl,--disable-new-dtags,-rpath,$TORCH_LIB -Wl,--no-undefined
