@@ -46,6 +46,8 @@ def parse():
     p.add_argument("--mode", choices=["mixture", "source"], default="mixture")
     p.add_argument("--cpu-seconds", type=float, default=12.0,
                    help="bounded CPU-baseline sample (0 disables)")
+    p.add_argument("--cpu-sampler-seconds", type=float, default=12.0,
+                   help="sampler CPU baseline: seconds per worker process (0 disables)")
     p.add_argument("--cpu-procs", type=int, default=0,
                    help="CPU baseline: worker processes, one per core (0: the cores this process "
                         "may run on, at most 16 = a one-GPU box's CPU share)")
@@ -57,6 +59,11 @@ def parse():
     p.add_argument("--mh-burnin", type=int, default=200000, help="sampler leg: untimed MH steps")
     p.add_argument("--source-lik-steps", type=int, default=20,
                    help="source-branch likelihood leg: timed launches (0: off)")
+    p.add_argument("--src-sampler-steps", type=int, default=2000,
+                   help="cfg5 SAMPLE_SOURCE = true sampler leg (the reference default mode): timed MH "
+                        "steps per chain (0 disables the leg)")
+    p.add_argument("--src-sampler-burnin", type=int, default=500,
+                   help="cfg5 SAMPLE_SOURCE = true sampler leg: untimed MH steps")
     p.add_argument("--src-steps", type=int, default=2000,
                    help="real-data sampler legs (the reference's Balkan / South America configs, "
                         "SAMPLE_SOURCE = true): timed MH steps (0 = skip)")
@@ -207,11 +214,11 @@ def pmc_secondary(args, B):
     return None
 
 
-def _cpu_worker(shape, seconds, seed, q):
+def _cpu_worker(shape, seconds, seed):
     """One CPU-baseline process: Likelihood.__call__(caching=False) restated in numpy
     (oracle/lik_numpy.py, bit-exact with the reference on the golden vectors) on one chain of
-    the bench workload, repeated for `seconds`.  Started with the spawn method and
-    OMP_NUM_THREADS = OPENBLAS_NUM_THREADS = 1, so it is one core's worth of work."""
+    the bench workload, repeated for `seconds`.  A child interpreter with OMP_NUM_THREADS =
+    OPENBLAS_NUM_THREADS = 1, so it is one core's worth of work."""
     import argparse
     import numpy as np
     from oracle import lik_numpy
@@ -237,7 +244,53 @@ def _cpu_worker(shape, seconds, seed, q):
         el = time.perf_counter() - t0
         if el >= seconds:
             break
-    q.put((n, el))
+    return {"n": n, "seconds": el}
+
+
+def _cpu_sampler_worker(shape, seconds, seed):
+    """One CPU-baseline sampler process: the MH step loop restated in numpy (oracle/mh_numpy.step,
+    MCMCGenerative.step with the ZoneMCMC operators, every candidate's log-likelihood a full
+    lik_numpy evaluation) with its decisions drawn from a numpy Generator (DrawTape), on one chain
+    of the sampler leg's workload (the same synthetic data, network, initial sample, operator
+    table and proposal precisions), run for `seconds`: steps and the log-likelihood trace."""
+    import argparse
+    import random
+    import numpy as np
+    from contact_zones_amd import packing
+    from contact_zones_amd.mcmc import InitialSamples
+    from oracle import mh_numpy
+    args = argparse.Namespace(**shape)
+    obs, fam = make_shared(args, np.random.default_rng(args.seed))
+    N, F, S, Z, Fam = args.sites, args.features, args.states, args.zones, args.families
+    indptr, indices = make_network(N, np.random.default_rng(args.seed + 17))
+    states = np.ones((F, S), bool)
+    init = InitialSamples(packing.obs_to_features(obs, S), states, indptr, indices,
+                          packing.index_to_groups(fam, Fam), Z, MH_M_INITIAL, True, None,
+                          random.Random(seed * 1000003))
+    zones = init.zones()
+    st = {"zos": packing.zones_to_zone_of_site(zones, N), "w": init.weights(), "pg": init.p_global()[0],
+          "pz": init.p_zones(zones), "pf": init.p_families()}
+    ops = mh_operators()
+    prec = [MH_PRECISION[k] for k in ("weights", "universal", "contact", "inheritance")]
+    fx = {"obs": obs, "fam_of_site": fam, "states": states, "inheritance": True, "warmup": False,
+          "min_size": MH_MIN_M, "max_size": np.array([MH_MAX_M]), "p_grow_connected": np.array([MH_P_GROW]),
+          "precision": np.array(prec, np.float64), "adj_indptr": indptr, "adj_indices": indices,
+          "n_zones": Z}
+    m = mh_numpy.Model(fx)
+    tape = mh_numpy.DrawTape(np.random.default_rng(seed), [ops[k] for k in mh_numpy.OPS[:7]])
+    ll, prior = m.loglik(st), m.log_prior(st)
+    lls = []
+    t0 = time.perf_counter()
+    while True:
+        st, ll, prior, _, _ = mh_numpy.step(m, st, ll, prior, 0, tape)
+        lls.append(ll)
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"n": len(lls), "seconds": el, "ll": [float(v) for v in lls]}
+
+
+CPU_WORKERS = {"lik": _cpu_worker, "sampler": _cpu_sampler_worker}
 
 
 def _cgroup_cpus():
@@ -249,43 +302,54 @@ def _cgroup_cpus():
         return None
 
 
-def cpu_baseline(args, seconds):
-    """SURVEY.md §8d CPU timing: one process per host core (spawned, single-threaded BLAS/OpenMP),
-    each evaluating one chain of the bench workload for `seconds`; per-core and all-core evals/s
-    with os.cpu_count() stated.  Kind 'port': the numpy restatement of the reference's
-    Likelihood.__call__ (the reference itself never travels to the GPU box); its speed relative to
-    the reference, both timed in the build container, is in profiles/r03_cpu_reference_ratio.json."""
-    import multiprocessing as mp
+def _cpu_procs(args):
+    """Worker processes of a CPU-baseline leg: one per core this process may use — the affinity
+    mask, bounded by the cgroup's CPU quota (more processes than the quota only time-slice) and by
+    the GPU box's CPU share of 16 (the pool's rule for one-GPU jobs)."""
     try:
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = os.cpu_count() or 1
     quota = _cgroup_cpus()
-    # one process per core this process may use: the affinity mask, bounded by the cgroup's CPU
-    # quota (more processes than the quota only time-slice) and by the GPU box's CPU share of 16
-    # (the pool's rule for one-GPU jobs: the host's other cores serve the other GPUs' jobs)
     usable = min(avail, int(quota)) if quota else avail
     procs = args.cpu_procs if args.cpu_procs > 0 else max(1, min(16, usable))
-    shape = {k: getattr(args, k) for k in ("sites", "features", "states", "zones", "families", "zone_size")}
-    keep = {k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS")}
-    for k in keep:
-        os.environ[k] = "1"
-    ctx = mp.get_context("spawn")  # fresh interpreters: nothing of this process's GPU state
-    q = ctx.Queue()
-    ps = [ctx.Process(target=_cpu_worker, args=(shape, seconds, args.seed, q)) for _ in range(procs)]
+    return procs, avail, quota, usable
+
+
+def _run_cpu_workers(kind, shape, seconds, seeds):
+    """Run one CPU worker per seed as a child interpreter (`bench.py --cpu-worker`, single-threaded
+    BLAS / OpenMP, nothing of this process's GPU state), all at once; every child has exited when
+    this returns.  Returns their JSON results."""
+    import subprocess
+    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    ps = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-worker",
+                            json.dumps({"kind": kind, "shape": shape, "seconds": seconds, "seed": sd})],
+                           stdout=subprocess.PIPE, env=env) for sd in seeds]
+    out = []
     try:
         for p in ps:
-            p.start()
-        res = [q.get(timeout=seconds * 10 + 300) for _ in ps]
-        for p in ps:
-            p.join()
+            so, _ = p.communicate(timeout=seconds * 10 + 300)
+            if p.returncode != 0:
+                raise SystemExit(f"CPU baseline worker ({kind}) failed with status {p.returncode}")
+            out.append(json.loads(so.decode().strip().splitlines()[-1]))
     finally:
-        for k, v in keep.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
-    rates = [n / el for n, el in res]
+        for p in ps:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return out
+
+
+def cpu_baseline(args, seconds):
+    """SURVEY.md §8d CPU timing: one process per host core (single-threaded BLAS/OpenMP), each
+    evaluating one chain of the bench workload for `seconds`; per-core and all-core evals/s
+    with os.cpu_count() stated.  Kind 'port': the numpy restatement of the reference's
+    Likelihood.__call__ (the reference itself never travels to the GPU box); its speed relative to
+    the reference, both timed in the build container, is in profiles/r03_cpu_reference_ratio.json."""
+    procs, avail, quota, usable = _cpu_procs(args)
+    shape = {k: getattr(args, k) for k in ("sites", "features", "states", "zones", "families", "zone_size")}
+    res = _run_cpu_workers("lik", shape, seconds, [args.seed] * procs)
+    rates = [r["n"] / r["seconds"] for r in res]
     N, F, S, Z, Fam = args.sites, args.features, args.states, args.zones, args.families
     ratio = None  # restatement / reference speed, both timed in the build container
     try:
@@ -309,7 +373,43 @@ def cpu_baseline(args, seconds):
                                              "mask, cgroup quota); not run"},
             "sample": f"numpy restatement of Likelihood.__call__(caching=False) (oracle/lik_numpy.py), "
                       f"one chain at {N}x{F}x{S}, Z={Z}, Fam={Fam} per process, {procs} processes x "
-                      f"{seconds:.0f} s, 1 thread each ({sum(n for n, _ in res)} evals)"}
+                      f"{seconds:.0f} s, 1 thread each ({sum(r['n'] for r in res)} evals)"}
+
+
+def cpu_baseline_sampler(args, seconds):
+    """The sampler's CPU baseline, timed: one process per usable core, each running the numpy
+    restatement of the MH step loop (oracle/mh_numpy.step, decisions drawn from numpy) on its own
+    chain of the sampler leg's cfg5 workload for `seconds`: steps/s per core and all-core, ESS/s of
+    the log-likelihood traces (Tracer's estimator on every step; a trace of this length is mostly
+    the chain's initial transient, so the ESS is an upper bound of little weight).  The
+    restatement's speed against the reference's own ZoneMCMC on the same shape, both timed in the
+    build container, is in profiles/r05_cpu_reference_sampler_ratio.json."""
+    import numpy as np
+    from contact_zones_amd.diagnostics import ess
+    procs, avail, quota, usable = _cpu_procs(args)
+    shape = {k: getattr(args, k) for k in ("sites", "features", "states", "zones", "families", "zone_size",
+                                           "seed")}
+    res = _run_cpu_workers("sampler", shape, seconds, [args.seed * 7919 + i for i in range(procs)])
+    rates = [r["n"] / r["seconds"] for r in res]
+    e = [float(ess(np.asarray(r["ll"])[None, :], max_lag=None)[0]) if r["n"] > 3 else 0.0 for r in res]
+    wall = max(r["seconds"] for r in res)
+    out = {"value": float(sum(rates)), "unit": "MH steps/s", "cores": procs, "kind": "port",
+           "per_core": float(sum(rates) / procs), "per_core_min": float(min(rates)),
+           "ess_per_sec": float(sum(e) / wall), "steps_per_process": [r["n"] for r in res],
+           "host_cpu_count": os.cpu_count(), "cores_available": avail, "cgroup_cpu_quota": quota,
+           "sample": f"numpy restatement of MCMCGenerative.step + ZoneMCMC operators "
+                     f"(oracle/mh_numpy.step, DrawTape decisions), one chain of the sampler leg's "
+                     f"workload per process, {procs} processes x {seconds:.0f} s, 1 thread each"}
+    try:
+        with open(os.path.join(ROOT, "profiles", "r05_cpu_reference_sampler_ratio.json")) as f:
+            r = json.load(f)
+        out.update({"restatement_over_reference": r["restatement_over_reference"],
+                    "reference_equivalent_value": out["value"] / r["restatement_over_reference"],
+                    "ratio_source": "profiles/r05_cpu_reference_sampler_ratio.json "
+                                    "(tools/time_reference_sampler.py cfg5)"})
+    except (OSError, ValueError, KeyError):
+        pass
+    return out
 
 
 # sampler leg: the reference defaults (config/default_config.json:6-20, 29-30)
@@ -453,10 +553,12 @@ def src_operators(inh=True):
     return {k: v / tot for k, v in ops.items()}
 
 
-def source_sampler_leg(shape, B, K, burnin, seed, rank=0, world=1, device=0):
+def source_sampler_leg(shape, B, K, burnin, seed, rank=0, world=1, device=0, gpu_init=False):
     """SAMPLE_SOURCE = true (the reference default) on synthetic data of `shape`: B chains per GPU
     x K Philox MH steps in one launch after `burnin` untimed steps; steps/s and ESS/s of the
-    log-likelihood traces, max wall over ranks."""
+    log-likelihood traces, max wall over ranks.  gpu_init: the chains' initial sources are drawn
+    by one gibbs_sample_sources step on the GPU (every source on the global component first),
+    instead of generate_initial_sample's host draw (0.2 s of numpy per chain at the cfg5 shape)."""
     import random
     import numpy as np
     import torch
@@ -487,17 +589,23 @@ def source_sampler_leg(shape, B, K, burnin, seed, rank=0, world=1, device=0):
     pf0 = init.p_families() if inh else None
     zos = np.empty((B, N), np.uint8)
     pz = np.empty((B, Z, F, S))
-    src = np.empty((B, N, F), np.uint8)
+    src = np.zeros((B, N, F), np.uint8)
     draws = np.random.default_rng(seed + 31 * rank)
     for b in range(B):  # generate_initial_sample per chain, with its initial source draw
         zones = init.zones()
         zos[b] = packing.zones_to_zone_of_site(zones, N)
         pz[b] = init.p_zones(zones)
-        src[b] = draw_sources(source_posterior(obs, fam, zos[b], w0, pg0, pz[b], pf0, inh), draws.random)
+        if not gpu_init:
+            src[b] = draw_sources(source_posterior(obs, fam, zos[b], w0, pg0, pz[b], pf0, inh), draws.random)
     rep = lambda x: np.broadcast_to(x, (B,) + x.shape).copy()  # noqa: E731
     st = ChainState(eng, zos, rep(w0), rep(pg0), pz, rep(pf0) if inh else None, source=src)
+    del src
     smp = Sampler(eng, states, indptr, indices, src_operators(inh), precisions(MH_PRECISION), MH_MIN_M,
                   sample_source=True)
+    if gpu_init:  # the initial Gibbs draw of every source (generate_initial_sample's last step)
+        Sampler(eng, states, indptr, indices, {"gibbs_sample_sources": 1.0}, precisions(MH_PRECISION),
+                MH_MIN_M, sample_source=True).run(st, 1, MH_MAX_M, MH_P_GROW, seed=seed * 7919 + 1,
+                                                  chain_id0=rank * B)
     if burnin:
         smp.run(st, burnin, MH_MAX_M, MH_P_GROW, seed=seed * 7919, chain_id0=rank * B)
     torch.cuda.synchronize()
@@ -521,8 +629,9 @@ def source_sampler_leg(shape, B, K, burnin, seed, rank=0, world=1, device=0):
         _all_reduce(sm, dist.ReduceOp.SUM)
         t = torch.stack([mx[0], sm[1], sm[2] / world])
     wall_max, ess_tot, acc_mean = (float(v) for v in t)
+    kernel = eng.last_kernels()
     eng.close()
-    return {"workload": f"{N}x{F}x{S} Z{Z} Fam{Fam}, SAMPLE_SOURCE = true, {B} chains/GPU",
+    return {"workload": f"{N}x{F}x{S} Z{Z} Fam{Fam}, SAMPLE_SOURCE = true, {B} chains/GPU", "kernel": kernel,
             "mh_steps_per_sec": B * K * world / wall_max, "ess_per_sec": ess_tot / wall_max,
             "ess_per_chain_mean": ess_tot / (B * world), "chains": B * world, "steps": K,
             "burnin": burnin, "wall_s": wall_max, "us_per_step": wall_max / K * 1e6,
@@ -807,6 +916,10 @@ def self_launch(n):
 
 
 def main():
+    if len(sys.argv) == 3 and sys.argv[1] == "--cpu-worker":  # a CPU-baseline child (no GPU)
+        spec = json.loads(sys.argv[2])
+        print(json.dumps(CPU_WORKERS[spec["kind"]](spec["shape"], spec["seconds"], spec["seed"])), flush=True)
+        return
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         raise SystemExit(self_launch(args.gpus))
@@ -915,6 +1028,13 @@ def main():
     sampler = None
     if args.mh_steps > 0 and args.mode == "mixture" and args.families > 0:
         sampler = sampler_leg(args, eng, obs, fam, dev, rank, world, stream)
+    sampler_src = None
+    if args.src_sampler_steps > 0 and args.mode == "mixture" and args.families > 0:
+        # the reference's default mode (SAMPLE_SOURCE = true, config/default_config.json:32) on the
+        # same cfg5 shape and chains per GPU: sources in HBM, the feature-table passes
+        shape = {k: getattr(args, k) for k in ("sites", "features", "states", "zones", "families")}
+        sampler_src = source_sampler_leg(shape, B, args.src_sampler_steps, args.src_sampler_burnin, args.seed,
+                                         rank, world, local_rank, gpu_init=True)
     other = None
     if args.other_steps > 0 and not src_mode:
         other = other_configs_leg(args, dev, stream, rank, world, local_rank)
@@ -977,17 +1097,16 @@ def main():
             line["likelihood_other_configs"] = other
         if sampler is not None:
             line["sampler"] = sampler
+        if sampler_src is not None:
+            line["sampler_source_mode"] = sampler_src
         if real is not None:
             line["sampler_real_data"] = real
         if world == 1 and args.cpu_seconds > 0:
             line["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
             line["speedup_vs_cpu"] = value / line["cpu_baseline"]["value"]
-            if sampler is not None:
-                # a reference MH step costs one Likelihood.__call__ (combine + weights are ~94% of
-                # the step at cfg5): its steps/s is the CPU evals/s
-                cpu_steps = line["cpu_baseline"]["value"]
-                sampler["cpu_reference_steps_per_sec_est"] = cpu_steps
-                sampler["speedup_vs_cpu_steps"] = sampler["mh_steps_per_sec"] / cpu_steps
+            if sampler is not None and args.cpu_sampler_seconds > 0:
+                sampler["cpu_baseline"] = cpu_baseline_sampler(args, args.cpu_sampler_seconds)
+                sampler["speedup_vs_cpu_steps"] = sampler["mh_steps_per_sec"] / sampler["cpu_baseline"]["value"]
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -206,6 +206,7 @@ void sbz_close(sbz_ctx *ctx) {
     free_buf(ctx->mh_stage);
     free_buf(ctx->src_t);
     free_buf(ctx->src_cand);
+    free_buf(ctx->src_ctab);
     free_buf(ctx->ticket);
     free_buf(ctx->stage);
     free_buf(ctx->out);
@@ -285,6 +286,7 @@ int sbz_set_option(sbz_ctx *ctx, int32_t option, int64_t value) {
         case SBZ_OPT_SRC_TABLE: return flag(ctx->src_rc);
         case SBZ_OPT_SRC_HBM: return flag(ctx->src_hbm);
         case SBZ_OPT_SRC_STAGE: return flag(ctx->src_stage);
+        case SBZ_OPT_SRC_PASS_TABLES: return flag(ctx->src_pass_tables);
         case SBZ_OPT_SRC_WAVES:
             if (value != 0 && value != 1 && value != 4 && value != 8)
                 return fail(ctx, SBZ_EINVAL, "source-mode sampler waves must be 0, 1, 4 or 8");
@@ -308,6 +310,7 @@ int sbz_get_option(const sbz_ctx *ctx, int32_t option, int64_t *value) {
         case SBZ_OPT_SRC_STAGE: *value = ctx->src_stage; return SBZ_OK;
         case SBZ_OPT_SRC_WAVES: *value = ctx->src_waves; return SBZ_OK;
         case SBZ_OPT_MH_LOOKAHEAD: *value = ctx->mh_la; return SBZ_OK;
+        case SBZ_OPT_SRC_PASS_TABLES: *value = ctx->src_pass_tables; return SBZ_OK;
         default: return SBZ_EINVAL;
     }
 }

@@ -79,9 +79,11 @@ struct sbz_ctx {
     int src_waves = 0;     // SBZ_OPT_SRC_WAVES: waves per chain of the source-mode sampler (0: 8)
     int mh_la = 24;        // SBZ_OPT_MH_LOOKAHEAD: sampler proposals planned ahead per batch (1..24)
     int src_hbm = 0;       // SBZ_OPT_SRC_HBM 1: source-mode sampler keeps sources in HBM even when they fit LDS
+    int src_pass_tables = 1;  // SBZ_OPT_SRC_PASS_TABLES 0: HBM-source sampler passes per cell, no count tables
     std::string last_kernels;  // sbz_last_kernels
     sbz::DevBuf mh_stage;      // host-form sampler staging (sbz_mh_run)
     sbz::DevBuf partial, ticket, zflag, src_t, stage, out, src_cand, flags;
+    sbz::DevBuf src_ctab;      // source-mode sampler count tables (current / candidate per chain)
     std::string err;
 };
 

@@ -104,6 +104,9 @@ __device__ __forceinline__ double ldp(const double *p) {
 __device__ __forceinline__ void stp(double *p, double v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ int ldi(const int *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // A read of LDS through a local-address-space pointer (ds_read).  A generic-pointer read of an
 // LDS array beside a read of a global array under a uniform select (`staged ? lds[i] :
@@ -553,6 +556,8 @@ struct MhArgs {
     const double *gc_g;         // [F][S] Gibbs prior counts of p_global (sbz_set_gibbs_counts) or null = 1
     const double *gc_f;         // [Fam][F][S] of p_families, or null = 1
     uint8_t *src_scratch;       // [B][F][Np] candidate sources when they live in HBM (source mode)
+    int *ctab;                  // source mode, table passes: count tables [2][B][F][CTP] (current /
+    size_t ct_half;             //   candidate halves, B * F * CTP ints apart; TbDims)
     int src_pm;                 // ch.source is [B][F][Np] by position (SBZ_SOURCE_BY_POSITION)
     const double *geo_cost;     // [N][N] 'cost_based' geo prior costs (sbz_set_geo_prior), or null
     double geo_scale;
@@ -658,7 +663,8 @@ constexpr int MH_SRC_MAX_WAVES = 16;         // waves per chain of the source-mo
 
 // SAMPLE_SOURCE = true sampler (sbz_mh_src.hip): LDS bytes per chain (sources in LDS, or in
 // HBM: hbm_sources) and the launch.
-size_t mh_src_lds_bytes(const sbz_dims &d, int C, bool hbm_sources = false, bool geo = false, bool stage = false);
+size_t mh_src_lds_bytes(const sbz_dims &d, int C, bool hbm_sources = false, bool geo = false, bool stage = false,
+                        bool tb = false, int Np = 0);
 int launch_mh_source(sbz_ctx *ctx, int B, const MhArgs &a);
 
 }  // namespace sbz

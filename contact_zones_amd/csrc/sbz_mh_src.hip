@@ -83,16 +83,90 @@ __device__ __forceinline__ int posterior_draw(const double (&l)[3], const double
 
 }  // namespace
 
-size_t mh_src_lds_bytes(const sbz_dims &d, int C, bool hbm_sources, bool geo, bool stage) {
+// ---- Feature-table passes (the sources in HBM, TB).  One pass over the N * F observations walks
+// the features in order, two per pipeline phase; per feature the workgroup builds the table of the
+// three component terms t_k = l_k * w_norm_k of every (zone class, family class, state) cell kind
+// (obs_terms' operations: the source branch's factors, model.py:177-184, and the unnormalised
+// posterior of gibbs_sample_sources, zone_sampling.py:200-202), and a cell costs one table read, a
+// compare chain and one product.  A resample draw with Philox uniforms compares u * s against the
+// partial sums of the terms (s = their sum: the same categorical distribution as the reference's
+// u < cumsum(t / s), sample_categorical preprocessing.py:335-338, without its divisions); a tape
+// replay takes the reference's own quotients and partial sums per cell, so its draws are the
+// reference's bit for bit.  Each thread owns the same 4 positions of every feature (one source /
+// observation dword, coalesced), so a thread only ever reads back the source bytes it wrote.  The
+// pass also counts the new sources per (component row, state) and per (class, component) into the
+// chain's count table in HBM, from which the Gibbs parameter operators take their Dirichlet counts
+// and their log-likelihood change without a pass of their own.  The stages run as a software
+// pipeline over the feature pairs, one barrier per pair: the parameter columns of pair i are
+// loaded, the normalised weights of pair i - 1 computed, the tables of pair i - 2 built, the
+// cells of pair i - 3 processed and the counts of pair i - 4 written out.
+constexpr int TB_FP = 2;  // features per pipeline phase
+struct TbDims {
+    int E;     // table entries per feature: (Z + 1) zone classes x FamC family classes x (S + 1) states
+    int FamC;  // family classes (Fam + 1 with inheritance, else 1)
+    int NL;    // column values loaded per feature: the C raw weights, then p_global, p_zones, p_families
+    int NCOL;  // doubles per column slot: w_norm [4][3], raw weights [3], the parameters
+    int CTP;   // counters per feature: p_global [S], p_zones [Z][S], p_families [Fam][S], classes [4][3]
+    int WOFF;  // offset of the class counters [h][k] (h = has_zone | has_family << 1)
+};
+__host__ __device__ inline TbDims tb_dims(int S, int Z, int Fam, int C) {
+    TbDims t;
+    const int Fm = C == 3 ? Fam : 0;
+    t.FamC = Fm + 1;
+    t.E = (Z + 1) * t.FamC * (S + 1);
+    t.NL = C + S * (1 + Z + Fm);
+    t.NCOL = 15 + S * (1 + Z + Fm);
+    t.WOFF = S * (1 + Z + Fm);
+    t.CTP = t.WOFF + 12;
+    return t;
+}
+// byte offsets (from the pass region's 16-B aligned base) of the tables [2][TB_FP][E + 1][3]
+// doubles (entry E: the padding positions' neutral entry), the column ring [3][TB_FP][cs]
+// doubles, the count blocks [2][TB_FP][ks] ints, the zero-weight masks [4][TB_FP] ints and the
+// per-position class words [Np]
+struct TbLayout {
+    size_t tbl, col, kcnt, zm, pinfo, end;
+};
+// count block of one feature in LDS: the component-row counters [WOFF] (LDS atomics), then each
+// wave's class counts [16 waves][16] (ballot counts, written by one lane each, summed when the
+// block is written out)
+__host__ __device__ inline int tb_kslots(const TbDims &t) { return t.WOFF + 16 * 16; }
+__host__ __device__ inline int tb_cslots(const TbDims &t) { return ((t.NCOL * 8 + 15) & ~15) / 8; }
+__host__ __device__ inline int tb_kstride(const TbDims &t) { return ((tb_kslots(t) * 4 + 15) & ~15) / 4; }
+__host__ __device__ inline TbLayout tb_layout(const TbDims &t, int Np) {
+    TbLayout L;
+    L.tbl = 0;
+    L.col = L.tbl + (((size_t)2 * TB_FP * (t.E + 1) * 24 + 15) & ~(size_t)15);
+    L.kcnt = L.col + (size_t)3 * TB_FP * tb_cslots(t) * 8;
+    L.zm = L.kcnt + (size_t)2 * TB_FP * tb_kstride(t) * 4;
+    L.pinfo = L.zm + 4 * TB_FP * 4;
+    L.end = L.pinfo + (size_t)Np * 4;
+    return L;
+}
+// the table passes apply: one source dword per thread and feature; per phase one column value and
+// one counter per thread
+__host__ __device__ inline bool tb_fits(const TbDims &t, int Np, int nt) {
+    return Np / 4 <= nt && TB_FP * t.NL <= nt && TB_FP * t.CTP <= nt && t.E <= 65535 - 256;
+}
+
+// LDS bytes of the redraw scratch (redraw_rows / weight gammas: draws [F][max(S, 2)] doubles,
+// per-feature tape offsets and counter ranks [F] ints, two totals)
+static inline size_t redraw_bytes(size_t F, size_t S) { return F * (S > 2 ? S : 2) * 8 + 2 * F * 4 + 8; }
+
+size_t mh_src_lds_bytes(const sbz_dims &d, int C, bool hbm_sources, bool geo, bool stage, bool tb, int Np) {
     const size_t N = d.n_sites, F = d.n_features, S = d.n_states, Z = d.n_zones;
     const size_t cnt = F * (S > (size_t)C ? S : (size_t)C);
-    return MH_SRC_MAX_WAVES * 2 * (8 + 4) + cnt * 4 + ((Z + 1) & ~(size_t)1) * 4 + MH_STAT_INTS * 4 +
-           ((N + 1) & ~(size_t)1) * 2 +
-           (hbm_sources ? 0 : ((N * F + 15) & ~(size_t)15) * 2) + ((N + 15) & ~(size_t)15) +
-           ((F + 15) & ~(size_t)15) + (geo ? 16 + geo_scratch_bytes((int)N) : 0) +
-           // redraw_rows / weight gammas: draws [F][max(S, 2)] doubles, per-feature tape offsets and
-           // counter ranks [F] ints
-           16 + F * (S > 2 ? S : 2) * 8 + 2 * F * 4 + 8 + 8 + SBZ_N_OPS * 8 +
+    const size_t head = MH_SRC_MAX_WAVES * 2 * (8 + 4) + cnt * 4 + ((Z + 1) & ~(size_t)1) * 4 + MH_STAT_INTS * 4 +
+                        ((N + 1) & ~(size_t)1) * 2 +
+                        (hbm_sources ? 0 : ((N * F + 15) & ~(size_t)15) * 2) + ((N + 15) & ~(size_t)15) +
+                        ((F + 15) & ~(size_t)15) + (geo ? 16 + geo_scratch_bytes((int)N) : 0);
+    if (tb) {
+        // the operator CDF, then one region that holds the redraw scratch or the pass buffers
+        const TbDims t = tb_dims((int)S, (int)Z, d.n_families, C);
+        const size_t pass = tb_layout(t, Np).end, rd = redraw_bytes(F, S);
+        return head + 16 + SBZ_N_OPS * 8 + 16 + (pass > rd ? pass : rd);
+    }
+    return head + 16 + redraw_bytes(F, S) + 8 + SBZ_N_OPS * 8 +
            // staged parameters: normalised weights [F][4][3], p_global, p_zones, p_families
            (stage ? 16 + (12 * F + (1 + Z + (C == 3 ? (size_t)d.n_families : 0)) * F * S) * 8 + N * F + N : 0);
 }
@@ -105,6 +179,17 @@ size_t mh_src_const_bytes(const sbz_dims &d, int C, bool alg, bool alf, bool gcg
            (size_t)d.n_features + 16;
 }
 
+// table passes: timing ablations of diagnostic builds (bit 1 no count atomics, 4 no table build, 8 a
+// constant uniform, 16 no log-likelihood product; results invalid)
+#ifndef SBZ_TB_ABL
+#define SBZ_TB_ABL 0
+#endif
+// table passes: stage cycle stamps of diagnostic builds (SBZ_TB_STAMP=1): per chain, the shader
+// cycles of each pipeline stage summed over the launch replace the first 16 entries of the ll trace
+// (wave 0: 0..7, the last wave: 8..15; results invalid)
+#ifndef SBZ_TB_STAMP
+#define SBZ_TB_STAMP 0
+#endif
 // A/B knobs: the log-likelihood pass reads only the selected component's weight and likelihood
 // (SBZ_SRC_LL1), and the N * F passes are unrolled SBZ_SRC_UNR cells deep
 #ifndef SBZ_SRC_LL1
@@ -142,6 +227,389 @@ struct CellWalk {
     }
 };
 
+// ---- The feature-table pass (TbDims), a function of its own: its phase loop gets its own register
+// allocation instead of sharing the sampler kernel's (inlined, its in-flight loads met spill
+// reloads and waits).  LDS arrays come in as local-address-space pointers (cast back to generic
+// ones inside, where the compiler infers ds_* accesses from the casts).
+// (global arrays likewise come in as global-address-space pointers: a generic one would make its
+// loads flat loads, which a barrier's lgkmcnt wait waits for)
+template <class T>
+using lds_ptr = __attribute__((address_space(3))) T *;
+template <class T>
+using gbl_ptr = __attribute__((address_space(1))) T *;
+struct TbPassArgs {
+    int N, F, S, Z, Np, xs8;
+    TbDims td;
+    int es, cs, ks;
+    gbl_ptr<const int> perm;
+    gbl_ptr<const uint8_t> famc, obs_fm;
+    lds_ptr<uint8_t> zos;
+    lds_ptr<double> tbl, col;
+    lds_ptr<int> kc, zm;
+    lds_ptr<uint32_t> pi;
+    lds_ptr<double> red;
+    lds_ptr<int> redi;
+    gbl_ptr<const double> cb;
+    int cstr, ch, cj;
+    gbl_ptr<const uint8_t> sv;
+    gbl_ptr<uint8_t> dst;
+    gbl_ptr<int> ct;
+    gbl_ptr<const double> tape;
+    int64_t pos0, len;
+    uint32_t key0, key1;
+    uint64_t chain, ctr;
+    uint64_t *stamps;  // SBZ_TB_STAMP builds
+};
+struct TbPassOut {
+    double ll;
+    int err, bad;
+    long long err_val;
+};
+// the per-cell uniforms of a Philox resample pass: xoroshiro128+ seeded per thread and pass from
+// one Philox block keyed (seed; thread, counter, chain, 0xFD tag) — a stream no LaneRng / site
+// stream shares; its top 53 bits are the uniform
+struct Xoro {
+    uint64_t s0, s1;
+    __device__ __forceinline__ double u() {
+        const uint64_t r = s0 + s1;
+        const uint64_t t = s1 ^ s0;
+        s0 = ((s0 << 24) | (s0 >> 40)) ^ t ^ (t << 16);
+        s1 = (t << 37) | (t >> 27);
+        return (double)(r >> 11) * 0x1p-53;
+    }
+};
+// per-thread sum of logs as one log: mantissas multiplied, exponents added (exact for any factor)
+struct TbLogAcc {
+    double m = 1.0;
+    int e = 0;
+    __device__ __forceinline__ double value() const { return flog(m) + (double)e * LN2; }
+};
+
+// MODE 0 / 2 resample: every source is redrawn from the current sample's posterior into `dst`
+// (gibbs_sample_sources), with Philox uniforms (0) or the tape's (2); MODE 1 reads the sources
+// `sv`.  All count the pass's sources into the count table `ct` and return the source-branch
+// log-likelihood of the pass's sources, sum log t[k] (-inf when a selected normalised weight is 0,
+// model.py:181-182).  Every thread of the workgroup calls it (it holds block barriers).
+template <int C, int NW, int MODE>
+__device__ __noinline__ TbPassOut tb_pass(TbPassArgs pa) {
+    constexpr int NT = NW * WAVE;
+    constexpr bool RS = MODE != 1, TP = MODE == 2;
+    const int tid = threadIdx.x, lane = tid % WAVE, wv = uni(tid / WAVE);
+    const int N = pa.N, F = pa.F, S = pa.S, Z = pa.Z, Np = pa.Np;
+    const int NF = N * F;
+    const size_t NFP = (size_t)F * Np;
+    const TbDims td = pa.td;
+    const int tb_es = pa.es, tb_cs = pa.cs, tb_ks = pa.ks;
+    double *tb_tbl = (double *)pa.tbl;
+    double *tb_col = (double *)pa.col;
+    int *tb_kc = (int *)pa.kc;
+    int *tb_zm = (int *)pa.zm;
+    uint32_t *tb_pi = (uint32_t *)pa.pi;
+    const uint8_t *zos = (const uint8_t *)pa.zos;
+    double *red = (double *)pa.red;
+    int *redi = (int *)pa.redi;
+    const double *tb_cb = (const double *)pa.cb;
+    const int tb_cstr = pa.cstr, tb_ch = pa.ch, tb_cj = pa.cj;
+    const uint8_t *sv = (const uint8_t *)pa.sv;
+    uint8_t *dst = (uint8_t *)pa.dst;
+    int *ct = (int *)pa.ct;
+    struct {
+        const int *perm;
+        const uint8_t *famc, *obs_fm;
+        int xs8;
+    } a{(const int *)pa.perm, (const uint8_t *)pa.famc, (const uint8_t *)pa.obs_fm, pa.xs8};
+    struct {
+        const double *tape;
+        int64_t pos, len;
+        uint32_t key0, key1;
+        uint64_t chain, ctr;
+    } rng{(const double *)pa.tape, pa.pos0, pa.len, pa.key0, pa.key1, pa.chain, pa.ctr};
+    uint64_t *tbst = pa.stamps;
+    int err = 0;
+    long long err_val = 0;
+    using LogAcc = TbLogAcc;
+    // block reductions, wave partials added in wave order; a trailing barrier, so the caller's next
+    // reduction may reuse the slots
+    auto bsum = [&](double v) -> double {
+        v = wave_sum(v);
+        if (lane == 0) red[wv] = v;
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        double t = red[0];
+#pragma unroll
+        for (int i = 1; i < NW; i++) t += red[i];
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        return uni(t);
+    };
+    auto bor = [&](int v) -> int {
+        const int wvv = __ballot(v != 0) ? 1 : 0;
+        if (lane == 0) redi[wv] = wvv;
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        int t = 0;
+#pragma unroll
+        for (int i = 0; i < NW; i++) t |= redi[i];
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        return uni(t);
+    };
+    constexpr int ABL = SBZ_TB_ABL;  // timing ablations (diagnostic builds only, results invalid)
+    // per-position class words: table row base | zone class << 16 | family class << 24
+    for (int p = tid; p < Np; p += NT) {
+        uint32_t pw = 0;
+        if (p < N) {
+            const int z0 = zos[a.perm[p]];
+            const int zc = z0 < Z ? z0 : Z;
+            const int fc = C == 3 ? (int)a.famc[p] : 0;
+            pw = (uint32_t)((zc * td.FamC + fc) * (S + 1)) | ((uint32_t)zc << 16) | ((uint32_t)fc << 24);
+        }
+        tb_pi[p] = pw;
+    }
+    for (int i = tid; i < 2 * TB_FP * tb_ks; i += NT) tb_kc[i] = 0;
+    if (tid < 2 * TB_FP * 3)  // the neutral entry of every table: t = 1 (and below any u * s: k = 0)
+        tb_tbl[(size_t)(tid / 3) * tb_es + (size_t)td.E * 3 + tid % 3] = 1.0;
+    const int NQ = Np / 4;
+    const int q = tid < NQ ? tid : NQ - 1;  // this thread's positions 4q .. 4q + 3
+    const bool hasq = tid < NQ;
+    Xoro xr{0, 0};
+    const int64_t pos0 = rng.pos;
+    const bool have = !rng.tape || pos0 + NF <= rng.len;
+    if (MODE == 0) {
+        uint32_t c[4] = {(uint32_t)tid, (uint32_t)rng.ctr, (uint32_t)rng.chain,
+                         (uint32_t)(rng.ctr >> 32) ^ 0xFD000000u};
+        philox4x32_10(c, rng.key0, rng.key1);
+        xr.s0 = ((uint64_t)c[1] << 32) | c[0];
+        xr.s1 = ((uint64_t)c[3] << 32) | c[2];
+        if ((xr.s0 | xr.s1) == 0) xr.s0 = 1;
+    }
+    // out-of-range stores (features outside [0, F), threads without positions or counters) are
+    // dropped by the buffer range check, so every phase issues the same memory operations
+    const __amdgpu_buffer_rsrc_t rdst = __builtin_amdgcn_make_buffer_rsrc(
+        dst, (short)0, RS ? (int)NFP : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rct = __builtin_amdgcn_make_buffer_rsrc(ct, (short)0, F * td.CTP * 4, 0x00020000);
+    const int FX = S * (1 + Z);  // counter offset of the family rows
+    LogAcc acc;
+    int zf = 0;
+    const int NPH = (F + TB_FP - 1) / TB_FP;  // feature pairs
+    // values in flight, each loaded two phases before its use: the column value of pair i and the
+    // observation (MODE 1: source) words of the cells of pair i - 1 (colA, obA, swA for even
+    // phases, colB, obB, swB for odd ones).  The loop runs two phases per iteration so that each
+    // load lands in the register its consumer reads (a copy of an in-flight load across the
+    // loop's back edge would wait for it there).
+    auto col_at = [&](int pr) { return ldp(tb_cb + (size_t)min(TB_FP * pr + tb_ch, F - 1) * tb_cstr); };
+    double colA = col_at(0), colB = col_at(min(1, NPH - 1));
+    uint32_t obA[TB_FP] = {}, obB[TB_FP] = {}, swA[TB_FP] = {}, swB[TB_FP] = {};
+    const uint8_t *obq = a.obs_fm + 4 * q;
+    const uint8_t *svq = sv + 4 * q;
+    auto phase = [&](int i, uint32_t (&obw)[TB_FP], uint32_t (&sww)[TB_FP], double &colw) {
+        const int pC = i - 3, pB = i - 2, pW = i - 1, pD = i - 4;
+        uint64_t st_prev = SBZ_TB_STAMP ? __builtin_amdgcn_s_memtime() : 0;
+        auto stamp = [&](int k) {
+            if (SBZ_TB_STAMP) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                const uint64_t t = __builtin_amdgcn_s_memtime();
+                tbst[k] += t - st_prev;
+                st_prev = t;
+            }
+        };
+        uint32_t outw[TB_FP] = {};
+        // C: the cells of pair pC, the thread's four positions of both features at once (no
+        // branch: a padding position reads the neutral entry E and is not counted)
+        if (pC >= 0 && pC < NPH) {
+            const uint4 pin = *reinterpret_cast<const uint4 *>(tb_pi + 4 * q);
+            const uint32_t pis[4] = {pin.x, pin.y, pin.z, pin.w};
+            bool val[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) val[j] = hasq && 4 * q + j < N;
+#pragma unroll
+            for (int h = 0; h < TB_FP; h++) {
+                const int f = TB_FP * pC + h;
+                if (TB_FP > 1 && f >= F) break;  // (uniform: an odd F's last pair)
+                const double *T = tb_tbl + (size_t)((pC & 1) * TB_FP + h) * tb_es;
+                int *kc = tb_kc + ((pC & 1) * TB_FP + h) * tb_ks;
+                int e[4], x[4], k[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int xb = (obw[h] >> (8 * j)) & 255;
+                    x[j] = a.xs8 ? xb >> 3 : xb;
+                    e[j] = val[j] ? (int)(pis[j] & 0xffffu) + x[j] : td.E;
+                }
+                double t0[4], t1[4], t2[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    t0[j] = T[e[j] * 3];
+                    t1[j] = T[e[j] * 3 + 1];
+                    t2[j] = C == 3 ? T[e[j] * 3 + 2] : 0.0;
+                }
+                if constexpr (RS) {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        double sum = t0[j] + t1[j];
+                        if (C == 3) sum = sum + t2[j];
+                        if constexpr (TP) {
+                            // the reference's normalize + sample_categorical, bit for bit
+                            const double u = (have && val[j]) ? rng.tape[pos0 + (int64_t)a.perm[4 * q + j] * F + f] : 0.0;
+                            const double p0 = t0[j] / sum, p1 = t1[j] / sum, p2 = C == 3 ? t2[j] / sum : 0.0;
+                            const double c1 = p0 + p1, c2 = c1 + p2;
+                            k[j] = u < p0 ? 0 : (u < c1 ? 1 : ((C == 3 && u < c2) ? 2 : 0));
+                        } else {
+                            const double us = ((ABL & 8) ? 0.5 : xr.u()) * sum;
+                            k[j] = us < t0[j] ? 0 : (us < t0[j] + t1[j] ? 1 : ((C == 3 && us < sum) ? 2 : 0));
+                        }
+                        outw[h] |= (uint32_t)k[j] << (8 * j);
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        k[j] = (sww[h] >> (8 * j)) & 255;
+                        if (k[j] >= C) {
+                            if (val[j] && !err) {
+                                err = 14;
+                                err_val = k[j];
+                            }
+                            k[j] = 0;
+                        }
+                    }
+                }
+                if (!(ABL & 16)) {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const double t = k[j] == 0 ? t0[j] : (k[j] == 1 ? t1[j] : t2[j]);
+                        acc.m *= __builtin_amdgcn_frexp_mant(t);
+                        acc.e += __builtin_amdgcn_frexp_exp(t);
+                    }
+                    renorm(acc.m, acc.e);
+                }
+                if (!(ABL & 1)) {
+                    int hk[4];
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const int zc = (pis[j] >> 16) & 255, fc = (int)(pis[j] >> 24);
+                        int ci = -1;
+                        if (x[j] < S) {
+                            if (k[j] == 0) ci = x[j];
+                            else if (k[j] == 1 && zc < Z) ci = S + zc * S + x[j];
+                            else if (k[j] == 2 && fc > 0) ci = FX + (fc - 1) * S + x[j];
+                        }
+                        if (val[j] && ci >= 0) atomicAdd(&kc[ci], 1);
+                        hk[j] = val[j] ? ((zc < Z ? 1 : 0) | (fc > 0 ? 2 : 0)) * 3 + k[j] : 15;
+                    }
+                    // the (class, component) counts of this wave's cells by ballot: lane c gets
+                    // category c's count and writes it to the wave's slot
+                    int myc = 0;
+#pragma unroll
+                    for (int c = 0; c < 12; c++) {
+                        int n = 0;
+#pragma unroll
+                        for (int j = 0; j < 4; j++) n += __popcll(__ballot(hk[j] == c));
+                        myc = lane == c ? n : myc;
+                    }
+                    if (lane < 12) kc[td.WOFF + 16 * wv + lane] = myc;
+                }
+            }
+        }
+        stamp(0);
+        // D: the counts of pair pD out to the count table (the class counts summed over the
+        // waves), the component-row counters cleared for pD + 2
+        int cv = 0;
+        const int dh = tid / td.CTP, dt = tid - dh * td.CTP, fD = TB_FP * pD + dh;
+        const bool dok = pD >= 0 && pD < NPH && dh < TB_FP && fD < F;
+        if (dok) {
+            int *kc = tb_kc + ((pD & 1) * TB_FP + dh) * tb_ks;
+            const int hk = dt - td.WOFF;
+            if (hk < 0) {
+                cv = kc[dt];
+                kc[dt] = 0;
+            } else {  // (every wave rewrites its slots for each feature: no clearing)
+#pragma unroll
+                for (int w2 = 0; w2 < NW; w2++) cv += kc[td.WOFF + 16 * w2 + hk];
+                // a selected normalised weight 0 (the table's zero mask) with a source on it
+                if (((tb_zm[(pD & 3) * TB_FP + dh] >> hk) & 1) && cv > 0) zf = 1;
+            }
+        }
+        stamp(1);
+        // B: the tables of pair pB (obs_terms' operations: t_k = l_k * w_norm_k)
+        if (pB >= 0 && pB < NPH && !(ABL & 4)) {
+            for (int e2 = tid; e2 < TB_FP * td.E; e2 += NT) {
+                const int h = e2 / td.E, e = e2 - h * td.E;
+                if (TB_FP * pB + h >= F) continue;
+                const int x = e % (S + 1), r = e / (S + 1);
+                const int zc = r / td.FamC, fc = r - zc * td.FamC;
+                const double *cs = tb_col + (size_t)((pB % 3) * TB_FP + h) * tb_cs;
+                const bool hz = zc < Z, hf = C == 3 && fc > 0, na = x >= S;
+                const int xc = na ? 0 : x;
+                const double *wn = cs + ((hz ? 1 : 0) | (hf ? 2 : 0)) * 3;
+                const double *pp = cs + 15;
+                const double l0 = na ? 1.0 : pp[xc];
+                const double l1 = na ? 1.0 : (hz ? pp[S + zc * S + xc] : 0.0);
+                const double l2 = C == 3 ? (na ? 1.0 : (hf ? pp[FX + (fc - 1) * S + xc] : 0.0)) : 0.0;
+                double *Ep = tb_tbl + (size_t)((pB & 1) * TB_FP + h) * tb_es + e * 3;
+                Ep[0] = l0 * wn[0];
+                Ep[1] = l1 * wn[1];
+                Ep[2] = C == 3 ? l2 * wn[2] : 0.0;
+            }
+            if (tid < TB_FP) {
+                const double *cs = tb_col + (size_t)((pB % 3) * TB_FP + tid) * tb_cs;
+                int m = 0;
+#pragma unroll
+                for (int hk = 0; hk < 12; hk++)
+                    if (hk % 3 < C && cs[hk] == 0.0) m |= 1 << hk;
+                tb_zm[(pB & 3) * TB_FP + tid] = m;
+            }
+        }
+        stamp(2);
+        // W: normalize_weights (model.py:436-452) of pair pW for the 4 classes
+        if (pW >= 0 && pW < NPH && tid < 12 * TB_FP) {
+            const int h2 = tid / 12, t12 = tid - h2 * 12;
+            double *cs = tb_col + (size_t)((pW % 3) * TB_FP + h2) * tb_cs;
+            const int h = t12 / 3, k = t12 - h * 3;
+            const double w0 = cs[12] * 1.0, w1 = cs[13] * ((h & 1) ? 1.0 : 0.0);
+            double sum = w0 + w1, w2 = 0.0;
+            if (C == 3) {
+                w2 = cs[14] * ((h & 2) ? 1.0 : 0.0);
+                sum = sum + w2;
+            }
+            cs[t12] = k == 0 ? w0 / sum : (k == 1 ? w1 / sum : (C == 3 ? w2 / sum : 0.0));
+        }
+        // A: the column of pair i (loaded two phases before) into its slot
+        if (i < NPH && tb_cj >= 0) tb_col[(size_t)((i % 3) * TB_FP + tb_ch) * tb_cs + tb_cj] = colw;
+        stamp(3);
+        // memory operations, the same every phase: the new source words of pC, the counts of pD,
+        // then the loads of the column of pair i + 2 and of the observation (source) words of pair
+        // i - 1 (their cells are processed in phase i + 2)
+        if (RS) {
+#pragma unroll
+            for (int h = 0; h < TB_FP; h++) {
+                const int f = TB_FP * pC + h;
+                __builtin_amdgcn_raw_buffer_store_b32(outw[h], rdst, (pC >= 0 && f < F && hasq) ? f * Np + 4 * q : 0x7ffffff0,
+                                                      0, 16);
+            }
+        }
+        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)cv, rct, dok ? (fD * td.CTP + dt) * 4 : 0x7ffffff0, 0, 16);
+        colw = col_at(min(i + 2, NPH - 1));
+#pragma unroll
+        for (int h = 0; h < TB_FP; h++) {
+            const int fo = min(max(TB_FP * (i - 1) + h, 0), F - 1);
+            obw[h] = *reinterpret_cast<const uint32_t *>(obq + (size_t)fo * Np);
+            if (!RS)
+                sww[h] = __hip_atomic_load(reinterpret_cast<const uint32_t *>(svq + (size_t)fo * Np),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        stamp(4);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        stamp(5);
+    };
+    for (int i = 0; i <= NPH + 3; i += 2) {
+        phase(i, obA, swA, colA);
+        phase(i + 1, obB, swB, colB);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sources and counts have landed
+    TbPassOut o;
+    o.ll = bsum(acc.value());  // (bsum's barrier publishes them)
+    if (bor(zf)) o.ll = -INFINITY;
+    o.err = err;
+    o.err_val = err_val;
+    o.bad = TP && !have ? 1 : 0;
+    return o;
+}
+
 // One workgroup of NW waves runs one chain.  Every decision is uniform across the workgroup:
 // all waves draw the same values from identical RNG states and take the same branches; the
 // NW * 64 threads share the N * F passes (block reductions through LDS, summed in wave order)
@@ -155,8 +623,12 @@ struct CellWalk {
 // touch them; they exchange cells through agent-scope (sc1, L1-bypassing) byte accesses and a
 // vmcnt(0) wait at every barrier.  Without GS the sources live in LDS as [N][F]; a.src_pm says
 // which layout the chain's array in HBM has (copied in and out at the launch's ends).
-template <int C, bool GS, int NW>
+// TB (with GS): the N * F passes are the feature-table passes above and the Gibbs parameter
+// operators take their counts from the chain's count table; the current and candidate sources
+// (and count tables) swap roles on an accepted move instead of being copied.
+template <int C, bool GS, int NW, bool TB = false>
 __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
+    static_assert(GS || !TB, "the table passes walk sources kept in HBM");
     constexpr int NT = NW * WAVE;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int tid = threadIdx.x;
@@ -192,14 +664,17 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     int *geo_ri = reinterpret_cast<int *>(geo_rd + 16);
     // redraw_rows scratch, 16-B aligned after the geo scratch
     const size_t par_off = (geo_off + (a.geo_cost ? geo_scratch_bytes(N) : 0) + 15) & ~(size_t)15;
-    double *gbuf = reinterpret_cast<double *>(lds + par_off);  // [F][max(S, 2)] draws
+    // TB: the operator CDF first, then one region holding either the redraw scratch (Gibbs
+    // parameter operators) or the table-pass buffers (tb_layout)
+    const size_t uni_off = TB ? ((par_off + (size_t)SBZ_N_OPS * 8 + 15) & ~(size_t)15) : par_off;
+    double *gbuf = reinterpret_cast<double *>(lds + uni_off);  // [F][max(S, 2)] draws
     int *fpre = reinterpret_cast<int *>(gbuf + (size_t)F * max(S, 2));  // [F] tape offset of feature f
     int *frank = fpre + F;                                      // [F] counter rank of feature f
     int *misc_i = frank + F;                                    // [2] totals of those scans
     // a.stage: the N*F passes read the chain's parameters and normalised weights from LDS copies
     // (staged when a pass starts after the parameters changed) instead of L2
     // the operator CDF (once per launch), 8-B aligned after misc_i
-    const size_t cdf_off = (par_off + (size_t)F * max(S, 2) * 8 + (size_t)F * 8 + 8 + 7) & ~(size_t)7;
+    const size_t cdf_off = TB ? par_off : (par_off + (size_t)F * max(S, 2) * 8 + (size_t)F * 8 + 8 + 7) & ~(size_t)7;
     double *cdf = reinterpret_cast<double *>(lds + cdf_off);  // [SBZ_N_OPS]
     // (read through a local-address-space pointer: ds_read, not a flat load)
     const __attribute__((address_space(3))) double *cdf3 =
@@ -587,6 +1062,105 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         for (int c = tid; c < (GS ? (int)NFP : NF); c += NT) wsrc(src, c, rsrc(srcb, c));
         sync();
     };
+
+    // ---- TB: the feature-table passes (TbDims) and the chain's count tables (current / candidate)
+    const TbDims td = tb_dims(S, Z, Fam, C);
+    const TbLayout tl = tb_layout(td, Np);
+    unsigned char *tbase = lds + uni_off;
+    const int tb_es = (td.E + 1) * 3;                              // doubles per feature table
+    double *tb_tbl = reinterpret_cast<double *>(tbase + tl.tbl);   // [2][TB_FP][E + 1][3]: t0 t1 t2
+    const int tb_cs = tb_cslots(td);
+    double *tb_col = reinterpret_cast<double *>(tbase + tl.col);   // [3][TB_FP][cs]
+    const int tb_ks = tb_kstride(td);
+    int *tb_kc = reinterpret_cast<int *>(tbase + tl.kcnt);         // [2][TB_FP][ks]
+    int *tb_zm = reinterpret_cast<int *>(tbase + tl.zm);           // [4][TB_FP]
+    uint32_t *tb_pi = reinterpret_cast<uint32_t *>(tbase + tl.pinfo);  // [Np]
+    int *ct_cur = TB ? a.ctab + (size_t)b * F * td.CTP : nullptr;
+    int *ct_alt = TB ? a.ctab + a.ct_half + (size_t)b * F * td.CTP : nullptr;
+    // this thread's column value (TbDims::NL) of a phase: feature TB_FP * pair + tb_ch, base +
+    // feature * stride (a dummy w[0] beyond TB_FP * NL)
+    const double *tb_cb = w;
+    int tb_cstr = 0, tb_ch = 0, tb_cj = -1;
+    if (tid < TB_FP * td.NL) {
+        tb_ch = tid / td.NL;
+        const int j0 = tid - tb_ch * td.NL;
+        tb_cj = j0 < C ? 12 + j0 : 15 + j0 - C;  // its slot in the column
+        if (j0 < C) {
+            tb_cb = w + j0;
+            tb_cstr = C;
+        } else {
+            const int j = j0 - C;
+            tb_cstr = S;
+            if (j < S) {
+                tb_cb = pg + j;
+            } else if (j < S * (1 + Z)) {
+                const int z = (j - S) / S;
+                tb_cb = pz + (size_t)z * F * S + (j - S - z * S);
+            } else {
+                const int r = (j - S * (1 + Z)) / S;
+                tb_cb = pf + (size_t)r * F * S + (j - S * (1 + Z) - r * S);
+            }
+        }
+    }
+    // One pass over every observation (tb_pass), the generator advanced as the pass drew
+    uint64_t tbst[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    auto tpass = [&](auto mode_c, const uint8_t *sv, uint8_t *dst, int *ct) -> double {
+        constexpr int MODE = decltype(mode_c)::value;
+        TbPassArgs pa;
+        pa.N = N;
+        pa.F = F;
+        pa.S = S;
+        pa.Z = Z;
+        pa.Np = Np;
+        pa.xs8 = a.xs8;
+        pa.td = td;
+        pa.es = tb_es;
+        pa.cs = tb_cs;
+        pa.ks = tb_ks;
+        pa.perm = (gbl_ptr<const int>)a.perm;
+        pa.famc = (gbl_ptr<const uint8_t>)a.famc;
+        pa.obs_fm = (gbl_ptr<const uint8_t>)a.obs_fm;
+        pa.zos = (lds_ptr<uint8_t>)zos;
+        pa.tbl = (lds_ptr<double>)tb_tbl;
+        pa.col = (lds_ptr<double>)tb_col;
+        pa.kc = (lds_ptr<int>)tb_kc;
+        pa.zm = (lds_ptr<int>)tb_zm;
+        pa.pi = (lds_ptr<uint32_t>)tb_pi;
+        pa.red = (lds_ptr<double>)red;
+        pa.redi = (lds_ptr<int>)redi;
+        pa.cb = (gbl_ptr<const double>)tb_cb;
+        pa.cstr = tb_cstr;
+        pa.ch = tb_ch;
+        pa.cj = tb_cj;
+        pa.sv = (gbl_ptr<const uint8_t>)sv;
+        pa.dst = (gbl_ptr<uint8_t>)dst;
+        pa.ct = (gbl_ptr<int>)ct;
+        pa.tape = (gbl_ptr<const double>)rng.tape;
+        pa.pos0 = rng.pos;
+        pa.len = rng.len;
+        pa.key0 = rng.key0;
+        pa.key1 = rng.key1;
+        pa.chain = rng.chain;
+        pa.ctr = rng.ctr;
+        pa.stamps = SBZ_TB_STAMP ? tbst : nullptr;
+        const TbPassOut o = tb_pass<C, NW, MODE>(pa);
+        if (o.err && !err) {
+            err = o.err;
+            err_val = o.err_val;
+        }
+        if (MODE == 2) {
+            if (o.bad) rng.bad = 1;
+            rng.pos = uni64(rng.pos + NF);
+        } else if (MODE == 0) {
+            rng.ctr++;
+        }
+        return uni(o.ll);
+    };
+    // a resample pass with the draws' source (tape or Philox)
+    auto tresample = [&](int *ct) -> double {
+        return rng.tape ? tpass(std::integral_constant<int, 2>(), src, srcb, ct)
+                        : tpass(std::integral_constant<int, 0>(), src, srcb, ct);
+    };
     // per-feature counts of sources / states into cnt
     auto clear_cnt = [&]() {
         for (int i = tid; i < ncnt; i += NT) cnt[i] = 0;
@@ -618,9 +1192,13 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     // if al != null.
     // (the generator's fields come in as values and go out through pos / ctr / bad: the lambda
     // does not touch `rng`, which keeps it in registers)
+    // want_dl (TB): also the source log-likelihood's change, sum over the redrawn entries of
+    // cnt * (log new - log old) (the cells whose source is this row's component and state); dzf set
+    // where that sum is not exact (an old or new value 0 / not finite under a non-zero count)
     auto redraw_rows = [&](double *base, double *lbase, int comp, int row,
                            const double *tape, int64_t len, uint32_t key0, uint32_t key1,
-                           uint64_t chain, int64_t &pos, uint64_t &ctr, int &bad) -> double {
+                           uint64_t chain, int64_t &pos, uint64_t &ctr, int &bad, bool want_dl, double &dll,
+                           int &dzf) -> double {
         // every (feature, state) draw at once: thread t <-> (f, j) = (t / S, t % S).  Feature f's
         // draws are its tape values pos + fpre[f] + j, or the gammas of lane stream j at counter
         // ctr + frank[f] (LaneRng, as one wave per feature drew them), fpre / frank the exclusive
@@ -672,7 +1250,8 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             gbuf[t] = g;
         }
         sync();
-        double dp = 0.0;
+        double dp = 0.0, dl = 0.0;
+        int zfl = 0;
         const bool al = has_al(comp);
         for (int t = tid; t < FS; t += NT) {
             const int f = t / S, j = t - f * S;
@@ -694,6 +1273,17 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                 const double am1 = alv(comp, row, f * S + x) - 1.0;
                 dp += xlogy(am1, g) - xlogy(am1, old);
             }
+            if (want_dl) {
+                const int c = cnt[f * S + x];
+                if (c > 0) {
+                    if (g > 0.0 && old > 0.0 && g < INFINITY && old < INFINITY) dl += (double)c * (flog(g) - flog(old));
+                    else zfl = 1;
+                }
+            }
+        }
+        if (want_dl) {
+            dll = bsum(dl);
+            dzf = bor(zfl);
         }
         bad = have ? 0 : 1;
         pos = uni64(pos0 + (tape ? tot_n : 0));
@@ -720,6 +1310,26 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     auto cell_of = [&](int s, int f) -> int { return GS ? f * Np + (int)g_pos[s] : s * F + f; };
     // the observed state of (s, f) (S = NA)
     auto obs_of = [&](int s, int f) -> int { return stg ? lds_rd(lobs + s * F + f) : a.obs_sm[(size_t)s * F + f]; };
+    // TB zone moves: the mixture log-likelihood of site s's F cells with zone class zc minus with
+    // zone class zo (sum log sum_k l_k w_k, the same operations as the posterior's normaliser).
+    // With every source resampled, ll_new - ll - (log q_s - log q_back_s) of the reference's
+    // ratio is exactly this sum over the moved sites: the sources' terms cancel.
+    auto site_mix_delta = [&](int s, int zc, int zo) -> double {
+        LogAcc an, ao;
+        for (int f = tid; f < F; f += NT) {
+            const int x = obs_of(s, f);
+            double l[3], wn[3];
+            terms_z(s, f, x, zc, l, wn);
+            double v = l[0] * wn[0] + l[1] * wn[1];
+            if (C == 3) v = v + l[2] * wn[2];
+            an.add(v);
+            terms_z(s, f, x, zo, l, wn);
+            v = l[0] * wn[0] + l[1] * wn[1];
+            if (C == 3) v = v + l[2] * wn[2];
+            ao.add(v);
+        }
+        return bsum(an.value() - ao.value());
+    };
     // the n sites of the list, compacted in ascending order by `keep` (wave 0 writes; every wave
     // gets the count).  Reads of a chunk precede its writes, so the compaction may be in place.
     auto compact = [&](int n, auto &&site_at, auto &&keep) -> int {
@@ -735,6 +1345,9 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         sync();
         return uni(kept);
     };
+
+    // TB: the chain's count table from its current sources (one pass per launch)
+    if constexpr (TB) (void)tpass(std::integral_constant<int, 1>(), src, nullptr, ct_cur);
 
     bool broken = false;
     for (int step = 0; step < a.n_steps; step++) {
@@ -766,10 +1379,14 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         // proposal (undone on rejection)
         bool gtent = false;
         int gz = 0, gn = 0, gsize = 0, gdocc = 0;
+        // TB zone move: the proposal's q, q_back and the moved sites' mixture delta
+        bool tb_zone = false;
+        double tb_q = 0.0, tb_qb = 0.0, tb_ds = 0.0;
 
         if (zone_op) {
             // ---- zone move with source resampling
-            const double log_q_back_s = pass_logq();
+            double log_q_back_s = 0.0;
+            if constexpr (!TB) log_q_back_s = pass_logq();
             log_q = 0.0;
             log_q_back = -INFINITY;
             const int n_free = N - occupied;
@@ -844,11 +1461,21 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                     geo_new = geo_prior();
                     dprior = uni(dprior + (geo_new - geo_cur));
                 }
-                double log_q_s;
-                pass_resample(log_q_s, ll_new);
+                if constexpr (TB) {
+                    ll_new = tresample(ct_alt);
+                    double ds = site_mix_delta(sa, zna, zoa);
+                    if (sb >= 0) ds = ds + site_mix_delta(sb, NONE, zna);
+                    tb_zone = true;
+                    tb_q = q;
+                    tb_qb = q_back;
+                    tb_ds = uni(ds);
+                } else {
+                    double log_q_s;
+                    pass_resample(log_q_s, ll_new);
+                    log_q = a.warmup ? -INFINITY : uni(log(q) + log_q_s);
+                    log_q_back = uni(log(q_back) + log_q_back_s);
+                }
                 new_sources = true;
-                log_q = a.warmup ? -INFINITY : uni(log(q) + log_q_s);
-                log_q_back = uni(log(q_back) + log_q_back_s);
             }
         } else if (op == GIBBSISH) {
             // ---- gibbsish_sample_zones (zone_sampling.py:619-702), as the SAMPLE_SOURCE = false
@@ -994,7 +1621,8 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                         log_q_s = bsum(acc.value());
                     }
                     sync();
-                    ll_new = pass_ll(srcb);
+                    if constexpr (TB) ll_new = tpass(std::integral_constant<int, 1>(), srcb, nullptr, ct_alt);
+                    else ll_new = pass_ll(srcb);
                     new_sources = true;
                     // ZoneMCMCWarmup.gibbs_sample_sources returns Q_GIBBS = -inf (:1293-1296)
                     log_q = a.warmup ? -INFINITY : uni(LQ + log_q_s);
@@ -1002,8 +1630,12 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                 }
             }
         } else if (op == G_SOURCES) {
-            double log_q_s;
-            pass_resample(log_q_s, ll_new);
+            if constexpr (TB) {
+                ll_new = tresample(ct_alt);
+            } else {
+                double log_q_s;
+                pass_resample(log_q_s, ll_new);
+            }
             new_sources = true;
         } else if (op == G_WEIGHTS) {
             // source counts per feature over the sites of a zone (or of a family)
@@ -1012,11 +1644,21 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                 broken = true;
                 break;
             }
-            clear_cnt();
-            for_cells([&](int s, int f, int, int g, int) {
-                const bool in = (C == 2 || fixed == 0) ? zos[s] < Z : (stg ? lds_rd(lfam + s) : a.fam_site[s]) > 0;
-                if (in) atomicAdd(&cnt[f * C + rsrc(src, g)], 1);
-            });
+            if constexpr (TB) {
+                // from the count table's class counters [h][k]: zoned sites are h = 1, 3, sites
+                // with a family h = 2, 3
+                for (int f = tid; f < F; f += NT) {
+                    const int *wc = ct_cur + (size_t)f * td.CTP + td.WOFF;
+                    const int h1 = (C == 2 || fixed == 0) ? 1 : 2;
+                    for (int k = 0; k < C; k++) cnt[f * C + k] = ldi(wc + h1 * 3 + k) + ldi(wc + 9 + k);
+                }
+            } else {
+                clear_cnt();
+                for_cells([&](int s, int f, int, int g, int) {
+                    const bool in = (C == 2 || fixed == 0) ? zos[s] < Z : (stg ? lds_rd(lfam + s) : a.fam_site[s]) > 0;
+                    if (in) atomicAdd(&cnt[f * C + rsrc(src, g)], 1);
+                });
+            }
             sync();
             LaneRng lr;
             lr.initw(rng, tid);
@@ -1034,8 +1676,11 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                 }
                 sync();
             }
+            double wdl = 0.0;  // TB: the log-likelihood change from the class counters
+            int wzf = 0;
             for (int f = tid; f < F; f += NT) {
                 double *wf = w + (size_t)f * C;
+                double o[3] = {ldp(wf), ldp(wf + 1), C == 3 ? ldp(wf + 2) : 0.0}, n[3] = {0.0, 0.0, 0.0};
                 if (C == 2) {
                     double d0, d1;
                     if (rng.tape) {
@@ -1049,6 +1694,8 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                     stp(wf, d0);
                     stp(wf + 1, d1);
                     if (stg) stage_nw(f, d0, d1, 0.0);
+                    n[0] = d0;
+                    n[1] = d1;
                 } else {
                     double r;
                     if (rng.tape) {
@@ -1057,7 +1704,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                         const double ga = gbuf[2 * f], gb = gbuf[2 * f + 1];
                         r = ga / (ga + gb);
                     }
-                    double w0 = ldp(wf), w1 = ldp(wf + 1), w2 = ldp(wf + 2);
+                    double w0 = o[0], w1 = o[1], w2 = o[2];
                     if (fixed == 0) w1 = r * w0 / (1.0 - r);
                     else w2 = r * w0 / (1.0 - r);
                     const double sum = (w0 + w1) + w2;
@@ -1065,6 +1712,32 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                     stp(wf + 1, w1 / sum);
                     stp(wf + 2, w2 / sum);
                     if (stg) stage_nw(f, w0 / sum, w1 / sum, w2 / sum);
+                    n[0] = w0 / sum;
+                    n[1] = w1 / sum;
+                    n[2] = w2 / sum;
+                }
+                if constexpr (TB) {
+                    // sum over classes h and components k of count * (log w_norm new - log w_norm old)
+                    const int *wc = ct_cur + (size_t)f * td.CTP + td.WOFF;
+#pragma unroll
+                    for (int h = 0; h < 4; h++) {
+                        const double on1 = o[1] * ((h & 1) ? 1.0 : 0.0), nn1 = n[1] * ((h & 1) ? 1.0 : 0.0);
+                        const double on2 = C == 3 ? o[2] * ((h & 2) ? 1.0 : 0.0) : 0.0;
+                        const double nn2 = C == 3 ? n[2] * ((h & 2) ? 1.0 : 0.0) : 0.0;
+                        double so = o[0] * 1.0 + on1, sn = n[0] * 1.0 + nn1;
+                        if (C == 3) {
+                            so = so + on2;
+                            sn = sn + nn2;
+                        }
+                        const double ov[3] = {o[0] * 1.0, on1, on2}, nv[3] = {n[0] * 1.0, nn1, nn2};
+                        for (int k = 0; k < C; k++) {
+                            const int c = ldi(wc + h * 3 + k);
+                            if (c <= 0) continue;
+                            const double wo = ov[k] / so, wn = nv[k] / sn;
+                            if (wo > 0.0 && wn > 0.0 && wo < INFINITY && wn < INFINITY) wdl += (double)c * (flog(wn) - flog(wo));
+                            else wzf = 1;
+                        }
+                    }
                 }
             }
             if (rng.tape) {
@@ -1074,7 +1747,14 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                 rng.ctr++;
             }
             gsync();  // the new weights are visible to every thread (and their staged forms)
-            ll_new = pass_ll(src);
+            if constexpr (TB) {
+                const double d = bsum(wdl);
+                ll_new = (bor(wzf) || !(ll > -INFINITY && ll < INFINITY))
+                             ? tpass(std::integral_constant<int, 1>(), src, nullptr, ct_alt)
+                             : uni(ll + d);
+            } else {
+                ll_new = pass_ll(src);
+            }
         } else {
             // ---- gibbs_sample_p_global / p_zones / p_families
             int row = 0;
@@ -1091,13 +1771,23 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                 draw_subset();
             }
             const int comp = op == G_P_GLOBAL ? 0 : (op == G_P_ZONES ? 1 : 2);
-            clear_cnt();
-            for_cells([&](int s, int f, int x, int g, int) {
-                bool in = sub[f] && rsrc(src, g) == comp && x < S;
-                if (comp == 1) in = in && zos[s] == row;
-                if (comp == 2) in = in && (stg ? lds_rd(lfam + s) : a.fam_site[s]) == row + 1;
-                if (in) atomicAdd(&cnt[f * S + x], 1);
-            });
+            if constexpr (TB) {
+                // the count table's row of this component: p_global [S], p_zones [row][S],
+                // p_families [row][S] per feature (subset features only)
+                const int off = comp == 0 ? 0 : (comp == 1 ? S + row * S : S * (1 + Z) + row * S);
+                for (int i = tid; i < FS; i += NT) {
+                    const int f = i / S, x = i - f * S;
+                    cnt[i] = sub[f] ? ldi(ct_cur + (size_t)f * td.CTP + off + x) : 0;
+                }
+            } else {
+                clear_cnt();
+                for_cells([&](int s, int f, int x, int g, int) {
+                    bool in = sub[f] && rsrc(src, g) == comp && x < S;
+                    if (comp == 1) in = in && zos[s] == row;
+                    if (comp == 2) in = in && (stg ? lds_rd(lfam + s) : a.fam_site[s]) == row + 1;
+                    if (in) atomicAdd(&cnt[f * S + x], 1);
+                });
+            }
             sync();
             double *base = comp == 0 ? pg : (comp == 1 ? pz + (size_t)row * F * S : pf + (size_t)row * F * S);
             int64_t rpos = rng.pos;
@@ -1105,8 +1795,10 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             int rbad = 0;
             // (an LDS address, used only when the parameters are staged)
             double *lbase = comp == 0 ? lpg : (comp == 1 ? lpz + (size_t)row * F * S : lpf + (size_t)row * F * S);
+            double dll = 0.0;
+            int dzf = 0;
             dprior = redraw_rows(base, lbase, comp, row, rng.tape, rng.len, rng.key0, rng.key1, rng.chain,
-                                 rpos, rctr, rbad);
+                                 rpos, rctr, rbad, TB, dll, dzf);
             rng.pos = rpos;
             rng.ctr = rctr;
             if (rbad) rng.bad = 1;
@@ -1114,12 +1806,28 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             // before the parameters are staged)
             if (stg && stg_ok) sync();
             else gsync();
-            ll_new = pass_ll(src);
+            if constexpr (TB) {
+                ll_new = (dzf || !(ll > -INFINITY && ll < INFINITY))
+                             ? tpass(std::integral_constant<int, 1>(), src, nullptr, ct_alt)
+                             : uni(ll + dll);
+            } else {
+                ll_new = pass_ll(src);
+            }
         }
 
         // ---- metropolis_hastings_ratio (mcmc_generative.py:307-318)
         bool accept;
-        if (log_q_back == -INFINITY) accept = false;
+        if (tb_zone) {
+            // TB zone move: log q_back = -inf when q_back is 0 or a current source has posterior 0
+            // (then ll = -inf); log q = -inf (accepted) in the warm-up, when q is 0, or when a new
+            // source landed on a zero-posterior component (ll_new = -inf beside a finite mixture
+            // delta; an all-zero moved cell is a 0/0 posterior, NaN in the reference: rejected
+            // after the uniform); otherwise the ratio with the sources' terms cancelled
+            if (tb_qb == 0.0 || !(ll > -INFINITY)) accept = false;
+            else if (a.warmup || tb_q == 0.0 || (ll_new == -INFINITY && tb_ds > -INFINITY && tb_ds < INFINITY))
+                accept = true;
+            else accept = flog(rng.real()) < (log(tb_qb) - log(tb_q)) + tb_ds + dprior;
+        } else if (log_q_back == -INFINITY) accept = false;
         else if (log_q == -INFINITY) accept = true;
         else accept = flog(rng.real()) < ((ll_new - ll) * 1.0) - (log_q - log_q_back) + dprior;
         if (tid == 0) stat[op]++;
@@ -1128,7 +1836,18 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             ll = ll_new;
             prior = prior + dprior;
             geo_cur = geo_new;
-            if (new_sources) commit_sources();
+            if (new_sources) {
+                if constexpr (TB) {  // the candidate sources and their counts become current
+                    uint8_t *t = src;
+                    src = srcb;
+                    srcb = t;
+                    int *c = ct_cur;
+                    ct_cur = ct_alt;
+                    ct_alt = c;
+                } else {
+                    commit_sources();
+                }
+            }
             if (sa >= 0) {
                 if (tid == 0) {
                     if (zoa < Z) zsize[zoa]--;
@@ -1184,6 +1903,13 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
 
     sync();
     for (int s = tid; s < N; s += NT) gzos[s] = zos[s];
+    if (TB && src != gsrc) {  // the current sources are the scratch row: back into the chain's array
+        const uint32_t *s32 = reinterpret_cast<const uint32_t *>(src);
+        uint32_t *d32 = reinterpret_cast<uint32_t *>(gsrc);
+        for (int i = tid; i < (int)(NFP / 4); i += NT)
+            __hip_atomic_store(d32 + i, __hip_atomic_load(s32 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (!GS) {
         if (a.src_pm) {  // back to [F][Np] by position (padding positions untouched)
             for (int i = tid; i < (int)NFP; i += NT) {
@@ -1193,6 +1919,9 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         } else {
             for (int c = tid; c < NF; c += NT) gsrc[c] = src[c];
         }
+    }
+    if (SBZ_TB_STAMP && ch.trace_ll && a.n_steps >= 16 && (tid == 0 || tid == NT - 64)) {
+        for (int k = 0; k < 8; k++) ch.trace_ll[(size_t)b * a.n_steps + (tid ? 8 : 0) + k] = (double)tbst[k];
     }
     if (tid == 0) {
         ch.ll[b] = ll;
@@ -1220,25 +1949,39 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
 int launch_mh_source(sbz_ctx *ctx, int B, const MhArgs &a0) {
     MhArgs a = a0;
     constexpr size_t LDS_MAX = 160 * 1024;
+    const sbz_dims &d = ctx->d;
     const bool geo = a.geo_cost != nullptr;
-    const bool gs = ctx->src_hbm || mh_src_lds_bytes(ctx->d, ctx->C, false, geo, false) > LDS_MAX;  // do not fit: HBM
-    // parameters staged in LDS when they fit too (SBZ_SRC_STAGE=0: off)
-    a.stage = ctx->src_stage && mh_src_lds_bytes(ctx->d, ctx->C, gs, geo, true) <= LDS_MAX ? 1 : 0;
-    size_t lds = mh_src_lds_bytes(ctx->d, ctx->C, gs, geo, a.stage != 0);
+    // gibbsish_sample_zones scratch (a non-zero weight): part of every placement decision below,
+    // so a shape at the edge falls back to HBM sources / no staging instead of failing
+    const size_t gib = a.gib ? 16 + (size_t)d.n_sites * 21 : 0;
+    // waves per chain: 8 (SBZ_OPT_SRC_WAVES overrides: 1, 4 or 8).  8 waves = 2 per SIMD, so up to
+    // 256 VGPRs: no spills.  Measured against 4 on the real-data shapes (tools/src_optime.py):
+    // Balkan 12.4 -> 11.2 us per step, South America 18.0 -> 14.2.
+    int nw = 8;
+    if (ctx->src_waves == 1 || ctx->src_waves == 4 || ctx->src_waves == 8) nw = ctx->src_waves;
+    const bool gs = ctx->src_hbm || mh_src_lds_bytes(d, ctx->C, false, geo, false) + gib > LDS_MAX;  // do not fit: HBM
+    // sources in HBM: the feature-table passes and count tables where they apply (4 or 8 waves,
+    // one source dword per thread and feature, the tables within LDS; SBZ_OPT_SRC_PASS_TABLES 0: off)
+    const TbDims td = tb_dims(d.n_states, d.n_zones, d.n_families, ctx->C);
+    const bool tb = gs && ctx->src_pass_tables && nw >= 4 && tb_fits(td, ctx->Np, nw * WAVE) &&
+                    mh_src_lds_bytes(d, ctx->C, true, geo, false, true, ctx->Np) + gib <= LDS_MAX;
+    // parameters staged in LDS when they fit too (SBZ_OPT_SRC_STAGE 0: off; not with the table passes)
+    a.stage = !tb && ctx->src_stage && mh_src_lds_bytes(d, ctx->C, gs, geo, true) + gib <= LDS_MAX ? 1 : 0;
+    size_t lds = mh_src_lds_bytes(d, ctx->C, gs, geo, a.stage != 0, tb, ctx->Np);
     // the constant tables too, when they fit beside the staged parameters
-    const size_t cst = mh_src_const_bytes(ctx->d, ctx->C, a.alpha_g != nullptr, a.alpha_f != nullptr,
+    const size_t cst = mh_src_const_bytes(d, ctx->C, a.alpha_g != nullptr, a.alpha_f != nullptr,
                                           a.gc_g != nullptr, a.gc_f != nullptr);
-    a.cstage = a.stage && ctx->d.n_states <= 255 && lds + cst <= LDS_MAX ? 1 : 0;
+    a.cstage = a.stage && d.n_states <= 255 && lds + cst + gib <= LDS_MAX ? 1 : 0;
     if (a.cstage) lds += cst;
     if (a.gib) {  // gibbsish_sample_zones scratch at the end (16-B aligned)
         lds = (lds + 15) & ~(size_t)15;
         a.gib_off = (uint32_t)lds;
-        lds += (size_t)ctx->d.n_sites * 21;
+        lds += (size_t)d.n_sites * 21;
     }
     if (lds > LDS_MAX)
         return fail(ctx, SBZ_EINVAL, "SAMPLE_SOURCE sampler needs " + std::to_string(lds) +
                                          " B of LDS per chain even with the sources in HBM (> 160 KiB)");
-    const size_t nfp = (size_t)ctx->d.n_features * ctx->Np;
+    const size_t nfp = (size_t)d.n_features * ctx->Np;
     // the chain's sources: position-major as given, or (site-major) copied in / out by the kernel
     // (LDS) or transposed around the launch (HBM, whose passes walk them position-major)
     a.src_pm = a.ch.source_layout == SBZ_SOURCE_BY_POSITION ? 1 : 0;
@@ -1257,11 +2000,12 @@ int launch_mh_source(sbz_ctx *ctx, int B, const MhArgs &a0) {
             a.src_pm = 1;
         }
     }
-    // waves per chain: 8 (SBZ_SRC_WAVES overrides: 1, 4 or 8).  8 waves = 2 per SIMD, so up to
-    // 256 VGPRs: no spills.  Measured against 4 on the real-data shapes (tools/src_optime.py):
-    // Balkan 12.4 -> 11.2 us per step, South America 18.0 -> 14.2.
-    int nw = 8;
-    if (ctx->src_waves == 1 || ctx->src_waves == 4 || ctx->src_waves == 8) nw = ctx->src_waves;
+    if (tb) {  // count tables: current and candidate, [2][B][F][CTP] ints
+        a.ct_half = (size_t)B * d.n_features * td.CTP;
+        int rc = ensure(ctx, ctx->src_ctab, 2 * a.ct_half * sizeof(int));
+        if (rc) return rc;
+        a.ctab = static_cast<int *>(ctx->src_ctab.ptr);
+    }
     static bool configured = false;
     if (!configured) {
         const void *fns[] = {
@@ -1270,22 +2014,31 @@ int launch_mh_source(sbz_ctx *ctx, int B, const MhArgs &a0) {
             reinterpret_cast<const void *>(&mh_src_kernel<2, false, 4>), reinterpret_cast<const void *>(&mh_src_kernel<3, false, 4>),
             reinterpret_cast<const void *>(&mh_src_kernel<2, true, 4>), reinterpret_cast<const void *>(&mh_src_kernel<3, true, 4>),
             reinterpret_cast<const void *>(&mh_src_kernel<2, false, 8>), reinterpret_cast<const void *>(&mh_src_kernel<3, false, 8>),
-            reinterpret_cast<const void *>(&mh_src_kernel<2, true, 8>), reinterpret_cast<const void *>(&mh_src_kernel<3, true, 8>)};
+            reinterpret_cast<const void *>(&mh_src_kernel<2, true, 8>), reinterpret_cast<const void *>(&mh_src_kernel<3, true, 8>),
+            reinterpret_cast<const void *>(&mh_src_kernel<2, true, 4, true>), reinterpret_cast<const void *>(&mh_src_kernel<3, true, 4, true>),
+            reinterpret_cast<const void *>(&mh_src_kernel<2, true, 8, true>), reinterpret_cast<const void *>(&mh_src_kernel<3, true, 8, true>)};
         for (const void *fn : fns) {
             hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX);
             if (e != hipSuccess) return hip_fail(ctx, e, "hipFuncSetAttribute(sampler LDS)");
         }
         configured = true;
     }
-    auto go = [&](auto cc, auto gsc, auto nwc) {
+    auto go = [&](auto cc, auto gsc, auto nwc, auto tbc) {
         constexpr int CC = decltype(cc)::value, NWC = decltype(nwc)::value;
-        constexpr bool GSC = decltype(gsc)::value;
-        mh_src_kernel<CC, GSC, NWC><<<B, NWC * WAVE, lds, ctx->stream>>>(a);
+        constexpr bool GSC = decltype(gsc)::value, TBC = decltype(tbc)::value;
+        mh_src_kernel<CC, GSC, NWC, TBC><<<B, NWC * WAVE, lds, ctx->stream>>>(a);
     };
     auto by_nw = [&](auto cc, auto gsc) {
-        if (nw == 1) go(cc, gsc, std::integral_constant<int, 1>());
-        else if (nw == 4) go(cc, gsc, std::integral_constant<int, 4>());
-        else go(cc, gsc, std::integral_constant<int, 8>());
+        if constexpr (decltype(gsc)::value) {
+            if (tb) {
+                if (nw == 4) go(cc, gsc, std::integral_constant<int, 4>(), std::true_type());
+                else go(cc, gsc, std::integral_constant<int, 8>(), std::true_type());
+                return;
+            }
+        }
+        if (nw == 1) go(cc, gsc, std::integral_constant<int, 1>(), std::false_type());
+        else if (nw == 4) go(cc, gsc, std::integral_constant<int, 4>(), std::false_type());
+        else go(cc, gsc, std::integral_constant<int, 8>(), std::false_type());
     };
     auto by_gs = [&](auto cc) {
         if (gs) by_nw(cc, std::true_type());
@@ -1295,6 +2048,7 @@ int launch_mh_source(sbz_ctx *ctx, int B, const MhArgs &a0) {
     else by_gs(std::integral_constant<int, 2>());
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(ctx, e, "source-mode sampler launch");
+    ctx->last_kernels = std::string("mh_src_kernel") + (gs ? (tb ? "<hbm, tables>" : "<hbm>") : "<lds>");
     if (src_sm) return launch_source_transpose(ctx, B, a.ch.source, src_sm, false);
     return SBZ_OK;
 }

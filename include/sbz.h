@@ -113,6 +113,10 @@ int sbz_synchronize(sbz_ctx *ctx);
  *                             they fit; 0: its passes read them from L2
  *   SBZ_OPT_MH_LOOKAHEAD      sampler with Philox draws: parameter proposals planned ahead per
  *                             batch, 1..24 (default 24; 1 = none; trajectories do not depend on it)
+ *   SBZ_OPT_SRC_PASS_TABLES   1 (default): the source-mode sampler with its sources in HBM runs its
+ *                             passes over the observations on per-feature tables and keeps per-chain
+ *                             source counts, so the Gibbs parameter operators need no pass (where the
+ *                             tables fit: 4 or 8 waves, Np <= 4 x threads); 0: per-cell passes
  * SBZ_EINVAL for an unknown option or a value out of range. */
 enum sbz_option {
     SBZ_OPT_LIK_TASKS_PER_CU = 1,
@@ -122,6 +126,7 @@ enum sbz_option {
     SBZ_OPT_SRC_HBM = 5,
     SBZ_OPT_SRC_STAGE = 6,
     SBZ_OPT_MH_LOOKAHEAD = 7,
+    SBZ_OPT_SRC_PASS_TABLES = 8,
 };
 int sbz_set_option(sbz_ctx *ctx, int32_t option, int64_t value);
 int sbz_get_option(const sbz_ctx *ctx, int32_t option, int64_t *value);

@@ -40,6 +40,9 @@ NONE = 255
 
 
 class TapeReader:
+    """The reference's decisions, in order.  Every draw method names the range it draws from (n,
+    the population, alpha) so that DrawTape can make the draws itself; a tape ignores them."""
+
     def __init__(self, items):
         self.items = items
         self.pos = 0
@@ -49,14 +52,53 @@ class TapeReader:
         self.pos += 1
         return float(v)
 
-    def int(self):
+    def int(self, n=None):
         return int(self.real())
+
+    def op(self):
+        return self.int()
+
+    def pair(self, population):
+        return [self.int(), self.int()]
+
+    def dirichlet(self, alpha):
+        return np.array([self.real(), self.real()])
 
     def reals(self, n):
         v = self.items[self.pos:self.pos + n]
         assert v.size == n, "tape exhausted"
         self.pos += n
         return np.asarray(v, np.float64)
+
+
+class DrawTape(TapeReader):
+    """The decisions drawn from a numpy Generator instead of a tape (the reference's distributions:
+    np.random.choice of the operator by its probability, uniform ints, random.sample pairs,
+    np.random.dirichlet proposals, uniform reals) — the CPU baseline's sampler (bench.py), no
+    replay.  SAMPLE_SOURCE = false operators only."""
+
+    def __init__(self, rng, op_probs):
+        self.rng = rng
+        self.p = np.asarray(op_probs, np.float64) / np.sum(op_probs)
+        self.pos = 0
+
+    def real(self):
+        return float(self.rng.random())
+
+    def int(self, n=None):
+        return int(self.rng.integers(n))
+
+    def op(self):
+        return int(self.rng.choice(len(self.p), p=self.p))
+
+    def pair(self, population):
+        return [int(v) for v in self.rng.choice(np.asarray(population), 2, replace=False)]
+
+    def dirichlet(self, alpha):
+        return self.rng.dirichlet(alpha)
+
+    def reals(self, n):
+        return self.rng.random(n)
 
 
 def geo_prior_distance(zone, cost, scale):
@@ -81,7 +123,7 @@ def dirichlet_logpdf(x, alpha):
 def dirichlet_proposal(w, precision, tape):
     """zone_sampling.py:537-569 with the Dirichlet draw read from the tape."""
     alpha = 1 + precision * w
-    w_new = np.array([tape.real(), tape.real()])
+    w_new = tape.dirichlet(alpha)
     q = np.exp(dirichlet_logpdf(w_new, alpha))
     alpha_back = 1 + precision * w_new
     q_back = np.exp(dirichlet_logpdf(w, alpha_back))
@@ -185,7 +227,7 @@ REJECT = (None, 0.0, -np.inf)
 
 def op_grow(m, st, c, tape):
     zos = st["zos"]
-    z = tape.int()
+    z = tape.int(m.n_zones)
     zone = zos == z
     size = int(np.count_nonzero(zone))
     if size >= m.max_size[c]:
@@ -197,7 +239,7 @@ def op_grow(m, st, c, tape):
     candidates = nb if connected else ~occupied
     if not np.any(candidates):
         return REJECT
-    site_new = np.flatnonzero(candidates)[tape.int()]
+    site_new = np.flatnonzero(candidates)[tape.int(np.count_nonzero(candidates))]
     new = dict(st, zos=zos.copy())
     new["zos"][site_new] = z
     q = (1 - p) * (1 / np.count_nonzero(~occupied))
@@ -209,13 +251,13 @@ def op_grow(m, st, c, tape):
 
 def op_shrink(m, st, c, tape):
     zos = st["zos"]
-    z = tape.int()
+    z = tape.int(m.n_zones)
     zone = zos == z
     size = int(np.count_nonzero(zone))
     if size <= m.min_size:
         return REJECT
     removal = np.flatnonzero(zone)
-    site_removed = removal[tape.int()]
+    site_removed = removal[tape.int(len(removal))]
     new = dict(st, zos=zos.copy())
     new["zos"][site_removed] = NONE
     q = 1 / len(removal)
@@ -233,7 +275,7 @@ def op_shrink(m, st, c, tape):
 def op_swap(m, st, c, tape):
     zos = st["zos"]
     occupied = zos != NONE
-    z = tape.int()
+    z = tape.int(m.n_zones)
     zone = zos == z
     nb = m.neighbours(zone, occupied)
     p = m.p_grow[c]
@@ -241,11 +283,11 @@ def op_swap(m, st, c, tape):
     candidates = nb if connected else ~occupied
     if not np.any(candidates):
         return REJECT
-    site_new = np.flatnonzero(candidates)[tape.int()]
+    site_new = np.flatnonzero(candidates)[tape.int(np.count_nonzero(candidates))]
     new = dict(st, zos=zos.copy())
     new["zos"][site_new] = z
     removal = np.flatnonzero(zone)
-    site_removed = removal[tape.int()]
+    site_removed = removal[tape.int(len(removal))]
     new["zos"][site_removed] = NONE
     back_nb = nb  # get_neighbours(zone_current, occupied) again: the same arguments (:752)
     q = (1 - p) * (1 / np.count_nonzero(~occupied))
@@ -266,10 +308,10 @@ def _alter_pair(arr_row, idx, precision, tape):
 
 
 def op_weights(m, st, c, tape):
-    f = tape.int()
+    f = tape.int(st["w"].shape[0])
     new = dict(st, w=st["w"].copy())
     if m.inheritance:
-        idx = [tape.int(), tape.int()]
+        idx = tape.pair(np.arange(3))
         vals, log_q, log_q_back = _alter_pair(st["w"][f], idx, m.prec[0], tape)
         new["w"][f, idx] = vals
     else:
@@ -279,11 +321,11 @@ def op_weights(m, st, c, tape):
 
 
 def _states_pair(m, f, tape):
-    return [tape.int(), tape.int()]
+    return tape.pair(np.flatnonzero(m.states[f]))
 
 
 def op_p_global(m, st, c, tape):
-    f = tape.int()
+    f = tape.int(m.states.shape[0])
     idx = _states_pair(m, f, tape)
     new = dict(st, pg=st["pg"].copy())
     vals, log_q, log_q_back = _alter_pair(st["pg"][f], idx, m.prec[1], tape)
@@ -292,8 +334,8 @@ def op_p_global(m, st, c, tape):
 
 
 def op_p_zones(m, st, c, tape):
-    z = tape.int()
-    f = tape.int()
+    z = tape.int(m.n_zones)
+    f = tape.int(m.states.shape[0])
     idx = _states_pair(m, f, tape)
     new = dict(st, pz=st["pz"].copy())
     vals, log_q, log_q_back = _alter_pair(st["pz"][z, f], idx, m.prec[2], tape)
@@ -302,8 +344,8 @@ def op_p_zones(m, st, c, tape):
 
 
 def op_p_families(m, st, c, tape):
-    fam = tape.int()
-    f = tape.int()
+    fam = tape.int(st["pf"].shape[0])
+    f = tape.int(m.states.shape[0])
     idx = _states_pair(m, f, tape)
     new = dict(st, pf=st["pf"].copy())
     vals, log_q, log_q_back = _alter_pair(st["pf"][fam, f], idx, m.prec[3], tape)
@@ -497,7 +539,7 @@ SOURCE_MOVES = {SHRINK: with_sources(op_shrink), GROW: with_sources(op_grow),
 def step(m, st, ll, prior, c, tape):
     """MCMCGenerative.step (mcmc_generative.py:282-329).  Returns (state, ll, prior, op,
     accepted)."""
-    op = tape.int()
+    op = tape.op()
     fn = SOURCE_MOVES[op] if (m.sample_source and op in SOURCE_MOVES) else OPERATORS[op]
     cand, log_q, log_q_back = fn(m, st, c, tape)
     if log_q_back == -np.inf:

@@ -14,13 +14,18 @@ SRC_CASES = mh_cases(source=True)
 REL_TOL = 1e-9
 
 
-@pytest.fixture(params=["lds", "hbm", "lds-w1", "hbm-w4"])
+@pytest.fixture(params=["lds", "hbm", "lds-w1", "hbm-w4", "hbmcell"])
 def src_home(request):
     """Context options: where the sampler keeps the sources — LDS (when they fit) or HBM (option
-    src_hbm = 1, the path every N x F too large for LDS takes, walking the sources by position) —
-    and the waves per chain (default 8, or src_waves = 1 / 4)."""
+    src_hbm = 1, the path every N x F too large for LDS takes, walking the sources by position, on
+    per-feature tables with per-chain count tables; 'hbmcell': the per-cell passes instead,
+    src_pass_tables = 0, the path of shapes whose tables do not fit) — and the waves per chain
+    (default 8, or src_waves = 1 / 4)."""
     home, _, waves = request.param.partition("-w")
-    return {"src_hbm": 1 if home == "hbm" else 0, "src_waves": int(waves or 0)}
+    opts = {"src_hbm": 1 if home.startswith("hbm") else 0, "src_waves": int(waves or 0)}
+    if home == "hbmcell":
+        opts["src_pass_tables"] = 0
+    return opts
 
 
 def _setup(fx, options=None):

@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--burnin", type=int, default=200)
     ap.add_argument("--sets", default=",".join(SETS))
+    ap.add_argument("--gpu-init", action="store_true",
+                    help="initial sources from one GPU gibbs_sample_sources step (fast at large shapes)")
     a = ap.parse_args()
     shape = {k: getattr(a, k) for k in ("sites", "features", "states", "zones", "families")}
     default_ops = bench.src_operators
@@ -43,7 +45,7 @@ def main():
     for name in a.sets.split(","):
         ops = SETS[name]
         bench.src_operators = default_ops if ops is None else (lambda inh=True, o=ops: dict(o))
-        r = bench.source_sampler_leg(shape, a.chains, a.steps, a.burnin, seed=3)
+        r = bench.source_sampler_leg(shape, a.chains, a.steps, a.burnin, seed=3, gpu_init=a.gpu_init)
         out[name] = round(r["us_per_step"], 3)
         print(name, out[name], flush=True)
     print(json.dumps({"shape": shape, "chains": a.chains, "us_per_step": out}))

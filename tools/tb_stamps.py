@@ -1,0 +1,44 @@
+"""Stage cycles of the source sampler's table passes (an SBZ_TB_STAMP=1 build of libsbz, selected with
+SBZ_LIB_PATH): zone moves only at the cfg5 shape, the per-stage shader cycles per pass phase (wave 0
+and the last wave), from the first 16 ll-trace entries the stamp build writes.  Diagnostic only.
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+import bench  # noqa: E402
+
+STAGES = ["C cells", "D counts out", "B table", "W+A weights/column", "memory ops", "barrier"]
+
+
+def main():
+    shape = {"sites": 2000, "features": 500, "states": 10, "zones": 8, "families": 4}
+    ops = {"shrink_zone": 0.4, "grow_zone": 0.4, "swap_zone": 0.2}
+    bench.src_operators = lambda inh=True: dict(ops)
+    steps = int(sys.argv[1]) if len(sys.argv) > 1 else 40
+    cap = {}
+    orig = bench.logged_ess if hasattr(bench, "logged_ess") else None
+    import contact_zones_amd.diagnostics as dg
+    real = dg.logged_ess
+
+    def grab(ll):
+        cap["ll"] = np.array(ll)
+        return real(np.nan_to_num(ll[:, 16:], nan=0.0, posinf=0.0, neginf=0.0))
+    dg.logged_ess = grab
+    r = bench.source_sampler_leg(shape, 256, steps, 0, seed=3)
+    ll = cap["ll"]
+    passes = steps + 1  # one count pass per launch + one resample pass per zone move (most steps)
+    phases = passes * (shape["features"] + 4)
+    w0 = ll[:, :8].mean(0) / phases
+    w7 = ll[:, 8:16].mean(0) / phases
+    out = {"us_per_step": r["us_per_step"], "cycles_per_phase_wave0": dict(zip(STAGES, w0.round(1).tolist())),
+           "cycles_per_phase_lastwave": dict(zip(STAGES, w7.round(1).tolist())),
+           "total_wave0": float(w0.sum()), "total_lastwave": float(w7.sum())}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

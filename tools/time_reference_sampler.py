@@ -54,7 +54,71 @@ def run(name, n_zones, steps, seed=1):
         os.chdir(cwd)
 
 
+def run_cfg5(seconds=20.0, seed=5):
+    """The bench's sampler workload (bench.py sampler_leg: cfg5 2000 x 500 x 10, Z = 8, Fam = 4,
+    SAMPLE_SOURCE = false, default STEPS / PROPOSAL_PRECISION / MIN_M / MAX_M / M_INITIAL /
+    P_GROW_CONNECTED, the same synthetic data) on the reference's own ZoneMCMC (one chain, one
+    core, caching likelihood) and on the numpy restatement bench.py's CPU baseline times
+    (oracle/mh_numpy.step with drawn decisions), each for about `seconds`: steps/s per core and
+    their ratio."""
+    import types
+    import bench
+    from contact_zones_amd import packing
+    from sbayes.model import Model
+    from sbayes.preprocessing import compute_network
+    from sbayes.sampling.zone_sampling import ZoneMCMC
+    a = types.SimpleNamespace(sites=2000, features=500, states=10, zones=8, families=4, zone_size=50)
+    obs, fam = bench.make_shared(a, np.random.default_rng(seed))
+    N, F, S, Z, Fam = a.sites, a.features, a.states, a.zones, a.families
+    indptr, indices = bench.make_network(N, np.random.default_rng(seed + 17))
+    import scipy.sparse as sp
+    adj = sp.csr_matrix((np.ones(indices.size), indices, indptr), shape=(N, N))
+    net = compute_network({"id": list(range(N)), "locations": np.random.default_rng(1).random((N, 2)),
+                           "names": [str(i) for i in range(N)]})
+    net["adj_mat"] = adj  # the bench's network
+    data = types.SimpleNamespace(features=packing.obs_to_features(obs, S), states=np.ones((F, S), bool),
+                                 network=net, families=packing.index_to_groups(fam, Fam))
+    prior = {"geo": {"type": "uniform"}, "area_size": {"type": "none"}, "weights": {"type": "uniform"},
+             "universal": {"type": "uniform"}, "inheritance": {"type": "uniform"}, "contact": {"type": "uniform"}}
+    cfg = {"N_AREAS": Z, "MIN_M": bench.MH_MIN_M, "MAX_M": bench.MH_MAX_M, "INHERITANCE": True,
+           "SAMPLE_SOURCE": False, "PRIOR": prior}
+    np.random.seed(seed)
+    random.seed(seed)
+    model = Model(data=data, config=cfg)
+    smp = ZoneMCMC(data=data, model=model, n_chains=1, operators=bench.mh_operators(),
+                   var_proposal=bench.MH_PRECISION, p_grow_connected=bench.MH_P_GROW,
+                   initial_size=bench.MH_M_INITIAL, logger=None)
+    steps = 50
+    t0 = time.perf_counter()
+    smp.generate_samples(steps, 10)  # (initial sample, first evaluations, the caches filled)
+    warm = time.perf_counter() - t0
+    steps = max(steps, int(steps * seconds / max(warm, 1e-3)))  # a run of about `seconds`
+    np.random.seed(seed)
+    random.seed(seed)
+    smp = ZoneMCMC(data=data, model=model, n_chains=1, operators=bench.mh_operators(),
+                   var_proposal=bench.MH_PRECISION, p_grow_connected=bench.MH_P_GROW,
+                   initial_size=bench.MH_M_INITIAL, logger=None)
+    t0 = time.perf_counter()
+    smp.generate_samples(steps, max(1, steps // 10))
+    el = time.perf_counter() - t0
+    ref = steps / el
+    shape = {"sites": N, "features": F, "states": S, "zones": Z, "families": Fam, "zone_size": 50, "seed": seed}
+    port = bench._cpu_sampler_worker(shape, seconds, seed * 7919)
+    por = port["n"] / port["seconds"]
+    return {"case": "cfg5 2000x500x10 Z8 Fam4, SAMPLE_SOURCE = false, bench sampler operators",
+            "reference_steps_per_sec_per_core": ref, "reference_steps": steps, "reference_seconds": el,
+            "restatement_steps_per_sec_per_core": por, "restatement_steps": port["n"],
+            "restatement_over_reference": por / ref,
+            "threads": {k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS")},
+            "host_cpu_count": os.cpu_count(),
+            "where": "build container CPU, 1 thread each (tools/time_reference_sampler.py cfg5)"}
+
+
 if __name__ == "__main__":
     refenv.setup()
-    for name, z, steps in (("balkan", 3, 2000), ("south_america", 6, 1000)):
-        print(json.dumps(run(name, z, steps)), flush=True)
+    if len(sys.argv) > 1 and sys.argv[1] == "cfg5":
+        sys.path.insert(0, ROOT)
+        print(json.dumps(run_cfg5(), indent=1), flush=True)
+    else:
+        for name, z, steps in (("balkan", 3, 2000), ("south_america", 6, 1000)):
+            print(json.dumps(run(name, z, steps)), flush=True)
