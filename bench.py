@@ -147,59 +147,77 @@ def algorithmic_bytes(args, B, source=False):
     return P, D, B * P + D
 
 
+def kernel_source_hash():
+    """sha256 (16 hex digits) of the HIP sources and headers libsbz.so is built from: a committed
+    PMC profile (profiles/r*_pmc.json, its _meta.source_hash) is used for this run's counters only
+    when it was measured on the same kernel sources."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    for fn in sorted(glob.glob(os.path.join(ROOT, "contact_zones_amd", "csrc", "*.hip")) +
+                     glob.glob(os.path.join(ROOT, "contact_zones_amd", "csrc", "*.h")) +
+                     [os.path.join(ROOT, "include", "sbz.h")]):
+        with open(fn, "rb") as f:
+            h.update(os.path.basename(fn).encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
+
+
+def _pmc_profiles(args, B):
+    """The committed PMC summaries of this workload, newest first, as (file, summary, current):
+    current = measured on this build's kernel sources (kernel_source_hash)."""
+    import glob
+    here = os.path.dirname(os.path.abspath(__file__))
+    cur = kernel_source_hash()
+    out = []
+    for fn in sorted(glob.glob(os.path.join(here, "profiles", "r*_pmc*.json")), reverse=True):
+        try:
+            d = json.load(open(fn))
+        except (OSError, ValueError):
+            continue
+        if d.get("_meta", {}).get("workload_key") == workload_key(args, B):
+            out.append((os.path.relpath(fn, here), d, d["_meta"].get("source_hash") == cur))
+    return out
+
+
 def workload_key(args, B):
     return (f"{args.sites}x{args.features}x{args.states}/Z{args.zones}x{args.zone_size}/"
             f"Fam{args.families}/B{B}/{args.mode}")
 
 
 def pmc_traffic(args, B):
-    """HBM bytes per launch of the dominant kernel from the newest committed PMC summary
-    (profiles/r*_pmc.json, written by tools/pmc.sh + tools/pmc_summary.py on this workload),
-    or None when no summary matches the workload."""
-    import glob
-    here = os.path.dirname(os.path.abspath(__file__))
-    for fn in sorted(glob.glob(os.path.join(here, "profiles", "r*_pmc.json")), reverse=True):
-        try:
-            d = json.load(open(fn))
-        except (OSError, ValueError):
-            continue
-        if d.get("_meta", {}).get("workload_key") == workload_key(args, B) and "_hbm" in d:
-            return d["_hbm"]["traffic_bytes"], os.path.relpath(fn, here)
-    return None, None
+    """HBM bytes per launch of the dominant kernel from the newest committed PMC summary of this
+    workload measured on these kernel sources (profiles/r*_pmc.json, written by tools/pmc.sh +
+    tools/pmc_summary.py), or (None, None, note) when there is none."""
+    profs = _pmc_profiles(args, B)
+    for fn, d, cur in profs:
+        if cur and "_hbm" in d:
+            return d["_hbm"]["traffic_bytes"], fn, None
+    stale = next((fn for fn, d, _ in profs if "_hbm" in d), None)
+    return None, None, (f"no PMC profile of these kernel sources; the newest of an earlier build is {stale}"
+                        if stale else None)
 
 
 def pmc_kernel_traffic(args, B, prefix):
-    """HBM bytes per launch of the kernel whose name starts with `prefix`, from the newest
-    committed PMC summary of this workload that holds it (tools/pmc.sh runs every leg's kernels)."""
-    import glob
-    here = os.path.dirname(os.path.abspath(__file__))
-    for fn in sorted(glob.glob(os.path.join(here, "profiles", "r*_pmc.json")), reverse=True):
-        try:
-            d = json.load(open(fn))
-        except (OSError, ValueError):
-            continue
-        if d.get("_meta", {}).get("workload_key") != workload_key(args, B):
+    """HBM bytes per launch of the kernel whose name starts with `prefix`, from the newest committed
+    PMC summary of this workload measured on these kernel sources (tools/pmc.sh runs every leg's
+    kernels), or (None, None)."""
+    for fn, d, cur in _pmc_profiles(args, B):
+        if not cur:
             continue
         for k, v in d.get("_per_kernel", {}).items():
-            if k.startswith(prefix):
-                return v["traffic_bytes"], os.path.relpath(fn, here)
+            if k.startswith(prefix) and "traffic_bytes" in v:
+                return v["traffic_bytes"], fn
     return None, None
 
 
 def pmc_secondary(args, B):
     """The binding on-chip resources of the dominant kernel, from the same committed PMC summary
-    as `traffic` (its average counters per launch): the LDS array's busy share of the CU cycles
-    (SQ_LDS_IDX_ACTIVE counts LDS-array cycles, MI355X_MICROARCH.md) and the VALU issue share of
-    the SIMD cycles (SQ_ACTIVE_INST_VALU counts quad-cycles).  The kernel's elapsed cycles per XCD
-    are GRBM_GUI_ACTIVE / 8 (rocprofv3 sums the 8 XCDs); 256 CUs, 1024 SIMDs."""
-    import glob
-    here = os.path.dirname(os.path.abspath(__file__))
-    for fn in sorted(glob.glob(os.path.join(here, "profiles", "r*_pmc.json")), reverse=True):
-        try:
-            d = json.load(open(fn))
-        except (OSError, ValueError):
-            continue
-        if d.get("_meta", {}).get("workload_key") != workload_key(args, B) or "_hbm" not in d:
+    as `traffic` (its average counters per launch; these kernel sources only): the LDS array's busy
+    share of the CU cycles (SQ_LDS_IDX_ACTIVE counts LDS-array cycles, MI355X_MICROARCH.md) and the
+    VALU issue share of the SIMD cycles (SQ_ACTIVE_INST_VALU counts quad-cycles).  The kernel's
+    elapsed cycles per XCD are GRBM_GUI_ACTIVE / 8 (rocprofv3 sums the 8 XCDs); 256 CUs, 1024 SIMDs."""
+    for fn, d, cur in _pmc_profiles(args, B):
+        if not cur or "_hbm" not in d:
             continue
         s = d.get(d["_hbm"]["kernel"], {})
         cyc = s.get("GRBM_GUI_ACTIVE", 0.0) / 8.0
@@ -208,7 +226,7 @@ def pmc_secondary(args, B):
         return {"lds_array_busy": s["SQ_LDS_IDX_ACTIVE"] / (256 * cyc),
                 "lds_bank_conflict_share": s.get("SQ_LDS_BANK_CONFLICT", 0.0) / s["SQ_LDS_IDX_ACTIVE"],
                 "valu_issue": 4.0 * s["SQ_ACTIVE_INST_VALU"] / (1024 * cyc),
-                "source": os.path.relpath(fn, here),
+                "source": fn,
                 "formula": "lds_array_busy = SQ_LDS_IDX_ACTIVE / (256 CUs x GRBM_GUI_ACTIVE/8); "
                            "valu_issue = 4 x SQ_ACTIVE_INST_VALU / (1024 SIMDs x GRBM_GUI_ACTIVE/8)"}
     return None
@@ -1018,7 +1036,7 @@ def main():
     launch_s = ev_ms / 1e3 / args.steps  # this rank's device time per launch (HIP events)
     achieved = per_launch / step_s / 1e9
 
-    traffic, traffic_src = pmc_traffic(args, B)
+    traffic, traffic_src, traffic_note = pmc_traffic(args, B)
     secondary = pmc_secondary(args, B)
     src_leg = None
     if args.source_lik_steps > 0 and not src_mode:
@@ -1082,6 +1100,8 @@ def main():
                 "timing": "achieved = bytes_per_launch / ms_per_step (timed wall clock, max over ranks)",
                 "traffic": traffic,
                 "traffic_source": traffic_src,
+                **({"traffic_note": traffic_note} if traffic_note else {}),
+                "kernel_source_hash": kernel_source_hash(),
                 "bytes_per_eval": P + D / B,
                 "bytes_per_launch": per_launch,
                 "step_us": step_s * 1e6,

@@ -13,8 +13,9 @@
 //   * Every cell value depends only on (site class, f, x), class = (zone or none) x (family or
 //     none).  For each feature the wave builds a table T[class][x] (x = S is the NA column) in
 //     its own few KB of LDS, in the reference's operation order (products, then the component
-//     sum left to right; -ffp-contract=off), so every entry is bit-identical to the reference's
-//     per-cell value.
+//     sum left to right).  Since round 4 the entries are built with fused multiply-adds
+//     (MixTable::prep): an entry may differ from the reference's per-cell value by an ulp, which
+//     the 1e-9 tolerance (north_star) covers many times over.
 //   * The lane owns SPL sites (4*lane + 256*k + j); their class row offsets live in registers.
 //     Observations are stored feature-major (obs_fm[f][site]) as byte offsets x*8, so a cell
 //     is one v_add_u32 (row + byte), one ds_read_b64 and one v_mul_f64.
@@ -56,6 +57,9 @@ constexpr int GIF = 16;      // table reads in flight per wave (scheduling barri
 // kernel at C = 3 is equal within 0.5 % for 0 / 8 / 16 (and at 2 waves per SIMD with 32 reads in
 // flight), at C = 2 (cfg5 without families) 59.3 -> 55.5 with 8; the source kernel 121.3 -> 120.0
 // with 16.
+#ifndef SBZ_LIK_STAGGER
+#define SBZ_LIK_STAGGER 0
+#endif
 #ifndef SBZ_GTREE
 #define SBZ_GTREE 8
 #endif
@@ -194,9 +198,20 @@ __host__ __device__ constexpr int bk_lines(int Z, int FamC, int S1) {
     return Z * FamC > FamC + 1 + (WAVE + S1 - 1) / S1 ? Z * FamC : FamC + 1 + (WAVE + S1 - 1) / S1;
 }
 // first double of row (zc, fc), zc = zone + 1 (0 = no zone)
+// SBZ_BK_ROT=1 (A/B): zone z's rows start at slot S1 + z mod (33 - 2 S1) instead of the two
+// parity offsets, so build()'s writes (lanes of one state x, different zones) and the gathers of
+// zoned lanes of different zones land on different banks.
+#ifndef SBZ_BK_ROT
+#define SBZ_BK_ROT 0
+#endif
 __host__ __device__ __forceinline__ uint32_t bk_row(int zc, int fc, int FamC, int S1) {
+#if SBZ_BK_ROT
+    return zc == 0 ? (uint32_t)fc * 32u
+                   : (uint32_t)(((zc - 1) * FamC + fc) * 32 + S1 + (zc - 1) % (33 - 2 * S1));
+#else
     return zc == 0 ? (uint32_t)fc * 32u
                    : (uint32_t)(((zc - 1) * FamC + fc) * 32 + S1 + ((zc - 1) & 1) * (32 - 2 * S1));
+#endif
 }
 
 // One feature's parameters as one lane needs them (the weights come from MixTable::prep).
@@ -537,6 +552,11 @@ __global__ __launch_bounds__(WAVE, MIX_WAVES) void lik_mixture_kernel(LikArgs a)
         }
     };
 
+#if SBZ_LIK_STAGGER
+    // A/B of the phase-lock hypothesis: tasks of odd slot start SBZ_LIK_STAGGER x 1024 cycles late
+    if (blockIdx.x & 1)
+        for (int i = 0; i < SBZ_LIK_STAGGER; i++) __builtin_amdgcn_s_sleep(16);
+#endif
     for (;;) {
         for (int q = 0; q < 4; q++) m[q] = 1.0;
         e = 0;

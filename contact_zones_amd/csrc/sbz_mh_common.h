@@ -126,13 +126,17 @@ __device__ __forceinline__ void renorm(double &m, int &e) {
 
 // log(x) in ~30 dependent f64 operations: x = m 2^e with m in [sqrt(1/2), sqrt(2)), log m =
 // 2 atanh(s), s = (m - 1) / (m + 1) (v_rcp_f64, two Newton steps and the residual of m + 1's
-// rounding), the atanh series to s^21, e ln 2 in two parts.  <= 1.43 ulp (mean 0.31 ulp against a
-// long-double log over 1e7 arguments, denormals included); 0 -> -inf, +inf -> +inf, x < 0 or NaN
-// -> NaN.  The library's log is correctly rounded through double-double steps: ~670 cycles of
-// latency on gfx950 against ~550 (tools/gamma_lat.hip, profiles/r04_gamma_lat.txt; a dependent
-// f64 operation costs ~18 cycles).  (An Estrin form of the series trips a gfx950 code-generation
-// error in mh_src_kernel<2, false, 4> with ROCm 7.2's compiler: "V_CMP_NE_U32_e32 0,
-// $src_shared_base", an illegal operand after post-RA pseudo expansion.)  Used where a log sits on a step's critical path and the value is
+// rounding), the atanh series to s^21 by Estrin, e ln 2 in two parts; 0 -> -inf, +inf -> +inf,
+// x < 0 or NaN -> NaN.  Accuracy: <= 1.43 ulp (mean 0.31 ulp against a long-double log over 1e7
+// arguments, denormals included) was measured on the Horner form of the series that came first;
+// the Estrin form evaluates the same polynomial in another order (its rounding differs by a few
+// ulp of the series tail, far below an ulp of the result), and every likelihood / acceptance
+// value it feeds is held to 1e-9 by the parity tests.  The Estrin form once tripped a gfx950
+// code-generation error ("V_CMP_NE_U32_e32 0, $src_shared_base") that came from LDS reads merged
+// into flat loads, not from the series; lds_rd() keeps those apart (commit bf8a8f8).  The
+// library's log is correctly rounded through double-double steps: ~670 cycles of latency on
+// gfx950 against ~550 (tools/gamma_lat.hip, profiles/r04_gamma_lat.txt; a dependent f64
+// operation costs ~18 cycles).  Used where a log sits on a step's critical path and the value is
 // a likelihood / acceptance term (the tape replays' decisions and the 1e-9 parity bar are
 // unaffected); SBZ_FLOG=0 builds (A/B only) use the library log everywhere.
 #ifndef SBZ_FLOG
@@ -664,7 +668,7 @@ constexpr int MH_SRC_MAX_WAVES = 16;         // waves per chain of the source-mo
 // SAMPLE_SOURCE = true sampler (sbz_mh_src.hip): LDS bytes per chain (sources in LDS, or in
 // HBM: hbm_sources) and the launch.
 size_t mh_src_lds_bytes(const sbz_dims &d, int C, bool hbm_sources = false, bool geo = false, bool stage = false,
-                        bool tb = false, int Np = 0);
+                        bool tb = false, int Np = 0, int nw = 8);
 int launch_mh_source(sbz_ctx *ctx, int B, const MhArgs &a);
 
 }  // namespace sbz

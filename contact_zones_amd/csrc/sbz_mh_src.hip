@@ -83,29 +83,30 @@ __device__ __forceinline__ int posterior_draw(const double (&l)[3], const double
 
 }  // namespace
 
-// ---- Feature-table passes (the sources in HBM, TB).  One pass over the N * F observations walks
-// the features in order, two per pipeline phase; per feature the workgroup builds the table of the
-// three component terms t_k = l_k * w_norm_k of every (zone class, family class, state) cell kind
-// (obs_terms' operations: the source branch's factors, model.py:177-184, and the unnormalised
-// posterior of gibbs_sample_sources, zone_sampling.py:200-202), and a cell costs one table read, a
-// compare chain and one product.  A resample draw with Philox uniforms compares u * s against the
-// partial sums of the terms (s = their sum: the same categorical distribution as the reference's
-// u < cumsum(t / s), sample_categorical preprocessing.py:335-338, without its divisions); a tape
-// replay takes the reference's own quotients and partial sums per cell, so its draws are the
-// reference's bit for bit.  Each thread owns the same 4 positions of every feature (one source /
-// observation dword, coalesced), so a thread only ever reads back the source bytes it wrote.  The
-// pass also counts the new sources per (component row, state) and per (class, component) into the
-// chain's count table in HBM, from which the Gibbs parameter operators take their Dirichlet counts
-// and their log-likelihood change without a pass of their own.  The stages run as a software
-// pipeline over the feature pairs, one barrier per pair: the parameter columns of pair i are
-// loaded, the normalised weights of pair i - 1 computed, the tables of pair i - 2 built, the
-// cells of pair i - 3 processed and the counts of pair i - 4 written out.
-constexpr int TB_FP = 2;  // features per pipeline phase
+// ---- Feature-table passes (the sources in HBM, TB).  One pass over the N * F observations: each
+// wave takes whole features (f = wave, wave + NW, ...), with a table, a parameter column and a
+// count block of its own in LDS, and no block barrier until the pass ends.  Per feature the wave
+// loads the parameter column, normalises the weights (normalize_weights, model.py:436-452) and
+// builds the table of the three component terms t_k = l_k * w_norm_k of every (zone class, family
+// class, state) cell kind (obs_terms' operations: the source branch's factors, model.py:177-184,
+// and the unnormalised posterior of gibbs_sample_sources, zone_sampling.py:200-202); then each
+// lane takes 32 positions of the feature (8 dwords of observation / source bytes, coalesced), and
+// a cell costs one table read, a compare chain and one product.  A resample draw with Philox
+// uniforms compares u * s against the partial sums of the terms (s = their sum: the categorical
+// distribution of the reference's u < cumsum(t / s), sample_categorical preprocessing.py:335-338,
+// without its divisions); a tape replay takes the reference's own quotients and partial sums per
+// cell, so its draws are the reference's bit for bit.  A source byte is always written and read
+// back by the same thread.  The pass also counts the new sources per (component row, state) and
+// per (class, component) into the chain's count table in HBM, from which the Gibbs parameter
+// operators take their Dirichlet counts and their log-likelihood change without a pass of their
+// own.  Each wave loads the next feature's column and observation (source) words while it works on
+// the current one.
+constexpr int TB_NCH = 8;  // 256-position chunks per feature: the passes take Np <= 2048
 struct TbDims {
     int E;     // table entries per feature: (Z + 1) zone classes x FamC family classes x (S + 1) states
     int FamC;  // family classes (Fam + 1 with inheritance, else 1)
     int NL;    // column values loaded per feature: the C raw weights, then p_global, p_zones, p_families
-    int NCOL;  // doubles per column slot: w_norm [4][3], raw weights [3], the parameters
+    int NCOL;  // doubles per column: w_norm [4][3], raw weights [3], the parameters
     int CTP;   // counters per feature: p_global [S], p_zones [Z][S], p_families [Fam][S], classes [4][3]
     int WOFF;  // offset of the class counters [h][k] (h = has_zone | has_family << 1)
 };
@@ -120,40 +121,34 @@ __host__ __device__ inline TbDims tb_dims(int S, int Z, int Fam, int C) {
     t.CTP = t.WOFF + 12;
     return t;
 }
-// byte offsets (from the pass region's 16-B aligned base) of the tables [2][TB_FP][E + 1][3]
-// doubles (entry E: the padding positions' neutral entry), the column ring [3][TB_FP][cs]
-// doubles, the count blocks [2][TB_FP][ks] ints, the zero-weight masks [4][TB_FP] ints and the
-// per-position class words [Np]
+// LDS of the pass (from the pass region's 16-B aligned base): per wave a table [E + 1][3] doubles
+// (entry E: the padding positions' neutral entry), a column [NCOL] doubles and a count block
+// [CTP] ints (`wave` bytes apart), then the per-position class words [Np] and the table entries'
+// (state, zone class, family class) [E]
 struct TbLayout {
-    size_t tbl, col, kcnt, zm, pinfo, end;
+    size_t wave, col, kcnt, pinfo, ed, end;
 };
-// count block of one feature in LDS: the component-row counters [WOFF] (LDS atomics), then each
-// wave's class counts [16 waves][16] (ballot counts, written by one lane each, summed when the
-// block is written out)
-__host__ __device__ inline int tb_kslots(const TbDims &t) { return t.WOFF + 16 * 16; }
-__host__ __device__ inline int tb_cslots(const TbDims &t) { return ((t.NCOL * 8 + 15) & ~15) / 8; }
-__host__ __device__ inline int tb_kstride(const TbDims &t) { return ((tb_kslots(t) * 4 + 15) & ~15) / 4; }
-__host__ __device__ inline TbLayout tb_layout(const TbDims &t, int Np) {
+__host__ __device__ inline TbLayout tb_layout(const TbDims &t, int Np, int nw) {
     TbLayout L;
-    L.tbl = 0;
-    L.col = L.tbl + (((size_t)2 * TB_FP * (t.E + 1) * 24 + 15) & ~(size_t)15);
-    L.kcnt = L.col + (size_t)3 * TB_FP * tb_cslots(t) * 8;
-    L.zm = L.kcnt + (size_t)2 * TB_FP * tb_kstride(t) * 4;
-    L.pinfo = L.zm + 4 * TB_FP * 4;
-    L.end = L.pinfo + (size_t)Np * 4;
+    L.col = ((size_t)(t.E + 1) * 24 + 15) & ~(size_t)15;
+    L.kcnt = L.col + (((size_t)t.NCOL * 8 + 15) & ~(size_t)15);
+    L.wave = L.kcnt + (((size_t)t.CTP * 4 + 15) & ~(size_t)15);
+    L.pinfo = (size_t)nw * L.wave;
+    L.ed = L.pinfo + (size_t)Np * 4;
+    L.end = L.ed + (((size_t)t.E * 4 + 15) & ~(size_t)15);
     return L;
 }
-// the table passes apply: one source dword per thread and feature; per phase one column value and
-// one counter per thread
-__host__ __device__ inline bool tb_fits(const TbDims &t, int Np, int nt) {
-    return Np / 4 <= nt && TB_FP * t.NL <= nt && TB_FP * t.CTP <= nt && t.E <= 65535 - 256;
+// the table passes apply: at most 8 chunks of 256 positions, three column values and three counters
+// per lane
+__host__ __device__ inline bool tb_fits(const TbDims &t, int Np) {
+    return Np <= 256 * TB_NCH && t.NL <= 3 * 64 && t.CTP <= 3 * 64 && t.E <= 65535 - 256;
 }
 
 // LDS bytes of the redraw scratch (redraw_rows / weight gammas: draws [F][max(S, 2)] doubles,
 // per-feature tape offsets and counter ranks [F] ints, two totals)
 static inline size_t redraw_bytes(size_t F, size_t S) { return F * (S > 2 ? S : 2) * 8 + 2 * F * 4 + 8; }
 
-size_t mh_src_lds_bytes(const sbz_dims &d, int C, bool hbm_sources, bool geo, bool stage, bool tb, int Np) {
+size_t mh_src_lds_bytes(const sbz_dims &d, int C, bool hbm_sources, bool geo, bool stage, bool tb, int Np, int nw) {
     const size_t N = d.n_sites, F = d.n_features, S = d.n_states, Z = d.n_zones;
     const size_t cnt = F * (S > (size_t)C ? S : (size_t)C);
     const size_t head = MH_SRC_MAX_WAVES * 2 * (8 + 4) + cnt * 4 + ((Z + 1) & ~(size_t)1) * 4 + MH_STAT_INTS * 4 +
@@ -163,7 +158,7 @@ size_t mh_src_lds_bytes(const sbz_dims &d, int C, bool hbm_sources, bool geo, bo
     if (tb) {
         // the operator CDF, then one region that holds the redraw scratch or the pass buffers
         const TbDims t = tb_dims((int)S, (int)Z, d.n_families, C);
-        const size_t pass = tb_layout(t, Np).end, rd = redraw_bytes(F, S);
+        const size_t pass = tb_layout(t, Np, nw).end, rd = redraw_bytes(F, S);
         return head + 16 + SBZ_N_OPS * 8 + 16 + (pass > rd ? pass : rd);
     }
     return head + 16 + redraw_bytes(F, S) + 8 + SBZ_N_OPS * 8 +
@@ -240,17 +235,13 @@ using gbl_ptr = __attribute__((address_space(1))) T *;
 struct TbPassArgs {
     int N, F, S, Z, Np, xs8;
     TbDims td;
-    int es, cs, ks;
     gbl_ptr<const int> perm;
     gbl_ptr<const uint8_t> famc, obs_fm;
     lds_ptr<uint8_t> zos;
-    lds_ptr<double> tbl, col;
-    lds_ptr<int> kc, zm;
-    lds_ptr<uint32_t> pi;
+    lds_ptr<unsigned char> base;  // the pass region (tb_layout)
     lds_ptr<double> red;
     lds_ptr<int> redi;
-    gbl_ptr<const double> cb;
-    int cstr, ch, cj;
+    gbl_ptr<const double> w, pg, pz, pf;  // the chain's parameters
     gbl_ptr<const uint8_t> sv;
     gbl_ptr<uint8_t> dst;
     gbl_ptr<int> ct;
@@ -267,7 +258,7 @@ struct TbPassOut {
 };
 // the per-cell uniforms of a Philox resample pass: xoroshiro128+ seeded per thread and pass from
 // one Philox block keyed (seed; thread, counter, chain, 0xFD tag) — a stream no LaneRng / site
-// stream shares; its top 53 bits are the uniform
+// stream shares; its top 52 bits make the uniform (1 + r 2^-52 - 1)
 struct Xoro {
     uint64_t s0, s1;
     __device__ __forceinline__ double u() {
@@ -275,7 +266,7 @@ struct Xoro {
         const uint64_t t = s1 ^ s0;
         s0 = ((s0 << 24) | (s0 >> 40)) ^ t ^ (t << 16);
         s1 = (t << 37) | (t >> 27);
-        return (double)(r >> 11) * 0x1p-53;
+        return __longlong_as_double((long long)(0x3FF0000000000000ull | (r >> 12))) - 1.0;
     }
 };
 // per-thread sum of logs as one log: mantissas multiplied, exponents added (exact for any factor)
@@ -289,250 +280,162 @@ struct TbLogAcc {
 // (gibbs_sample_sources), with Philox uniforms (0) or the tape's (2); MODE 1 reads the sources
 // `sv`.  All count the pass's sources into the count table `ct` and return the source-branch
 // log-likelihood of the pass's sources, sum log t[k] (-inf when a selected normalised weight is 0,
-// model.py:181-182).  Every thread of the workgroup calls it (it holds block barriers).
+// model.py:181-182).  Every thread of the workgroup calls it (it holds block barriers at its ends).
 template <int C, int NW, int MODE>
 __device__ __noinline__ TbPassOut tb_pass(TbPassArgs pa) {
     constexpr int NT = NW * WAVE;
     constexpr bool RS = MODE != 1, TP = MODE == 2;
+    constexpr int ABL = SBZ_TB_ABL;  // timing ablations (diagnostic builds only, results invalid)
     const int tid = threadIdx.x, lane = tid % WAVE, wv = uni(tid / WAVE);
-    const int N = pa.N, F = pa.F, S = pa.S, Z = pa.Z, Np = pa.Np;
-    const int NF = N * F;
-    const size_t NFP = (size_t)F * Np;
+    const int N = pa.N, F = pa.F, S = pa.S, Z = pa.Z, Np = pa.Np, NF = N * F;
     const TbDims td = pa.td;
-    const int tb_es = pa.es, tb_cs = pa.cs, tb_ks = pa.ks;
-    double *tb_tbl = (double *)pa.tbl;
-    double *tb_col = (double *)pa.col;
-    int *tb_kc = (int *)pa.kc;
-    int *tb_zm = (int *)pa.zm;
-    uint32_t *tb_pi = (uint32_t *)pa.pi;
+    const int E = td.E, CTP = td.CTP, WOFF = td.WOFF, FamC = td.FamC;
+    const TbLayout L = tb_layout(td, Np, NW);
+    unsigned char *base = (unsigned char *)pa.base;
+    double *T = (double *)(base + (size_t)wv * L.wave);              // this wave's table [E + 1][3]
+    double *cs = (double *)(base + (size_t)wv * L.wave + L.col);     // its column [NCOL]
+    int *kc = (int *)(base + (size_t)wv * L.wave + L.kcnt);          // its count block [CTP]
+    uint32_t *pinfo = (uint32_t *)(base + L.pinfo);                  // [Np]
+    uint32_t *edl = (uint32_t *)(base + L.ed);                       // [E]
     const uint8_t *zos = (const uint8_t *)pa.zos;
     double *red = (double *)pa.red;
     int *redi = (int *)pa.redi;
-    const double *tb_cb = (const double *)pa.cb;
-    const int tb_cstr = pa.cstr, tb_ch = pa.ch, tb_cj = pa.cj;
+    const int *perm = (const int *)pa.perm;
+    const uint8_t *famc = (const uint8_t *)pa.famc, *obs_fm = (const uint8_t *)pa.obs_fm;
+    const double *w = (const double *)pa.w, *pg = (const double *)pa.pg, *pz = (const double *)pa.pz,
+                 *pf = (const double *)pa.pf;
     const uint8_t *sv = (const uint8_t *)pa.sv;
     uint8_t *dst = (uint8_t *)pa.dst;
     int *ct = (int *)pa.ct;
-    struct {
-        const int *perm;
-        const uint8_t *famc, *obs_fm;
-        int xs8;
-    } a{(const int *)pa.perm, (const uint8_t *)pa.famc, (const uint8_t *)pa.obs_fm, pa.xs8};
-    struct {
-        const double *tape;
-        int64_t pos, len;
-        uint32_t key0, key1;
-        uint64_t chain, ctr;
-    } rng{(const double *)pa.tape, pa.pos0, pa.len, pa.key0, pa.key1, pa.chain, pa.ctr};
+    const double *tape = (const double *)pa.tape;
     uint64_t *tbst = pa.stamps;
+    const int FX = S * (1 + Z);  // counter offset of the family rows
     int err = 0;
     long long err_val = 0;
-    using LogAcc = TbLogAcc;
-    // block reductions, wave partials added in wave order; a trailing barrier, so the caller's next
-    // reduction may reuse the slots
-    auto bsum = [&](double v) -> double {
-        v = wave_sum(v);
-        if (lane == 0) red[wv] = v;
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        double t = red[0];
-#pragma unroll
-        for (int i = 1; i < NW; i++) t += red[i];
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        return uni(t);
+    auto wsync = [&]() {  // a wave's LDS writes are seen by its later reads (LDS keeps a wave's order)
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
     };
-    auto bor = [&](int v) -> int {
-        const int wvv = __ballot(v != 0) ? 1 : 0;
-        if (lane == 0) redi[wv] = wvv;
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        int t = 0;
-#pragma unroll
-        for (int i = 0; i < NW; i++) t |= redi[i];
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        return uni(t);
+    uint64_t st_prev = SBZ_TB_STAMP ? __builtin_amdgcn_s_memtime() : 0;
+    auto stamp = [&](int k) {
+        if (SBZ_TB_STAMP) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            tbst[k] += t - st_prev;
+            st_prev = t;
+        }
     };
-    constexpr int ABL = SBZ_TB_ABL;  // timing ablations (diagnostic builds only, results invalid)
+
     // per-position class words: table row base | zone class << 16 | family class << 24
     for (int p = tid; p < Np; p += NT) {
         uint32_t pw = 0;
         if (p < N) {
-            const int z0 = zos[a.perm[p]];
+            const int z0 = zos[perm[p]];
             const int zc = z0 < Z ? z0 : Z;
-            const int fc = C == 3 ? (int)a.famc[p] : 0;
-            pw = (uint32_t)((zc * td.FamC + fc) * (S + 1)) | ((uint32_t)zc << 16) | ((uint32_t)fc << 24);
+            const int fc = C == 3 ? (int)famc[p] : 0;
+            pw = (uint32_t)((zc * FamC + fc) * (S + 1)) | ((uint32_t)zc << 16) | ((uint32_t)fc << 24);
         }
-        tb_pi[p] = pw;
+        pinfo[p] = pw;
     }
-    for (int i = tid; i < 2 * TB_FP * tb_ks; i += NT) tb_kc[i] = 0;
-    if (tid < 2 * TB_FP * 3)  // the neutral entry of every table: t = 1 (and below any u * s: k = 0)
-        tb_tbl[(size_t)(tid / 3) * tb_es + (size_t)td.E * 3 + tid % 3] = 1.0;
-    const int NQ = Np / 4;
-    const int q = tid < NQ ? tid : NQ - 1;  // this thread's positions 4q .. 4q + 3
-    const bool hasq = tid < NQ;
+    for (int e = tid; e < E; e += NT) {  // entry e: state | zone class << 8 | family class << 16
+        const int x = e % (S + 1), r = e / (S + 1);
+        const int zc = r / FamC, fc = r - zc * FamC;
+        edl[e] = (uint32_t)x | ((uint32_t)zc << 8) | ((uint32_t)fc << 16);
+    }
+    for (int i = lane; i < CTP; i += WAVE) kc[i] = 0;
+    if (lane < 3) T[(size_t)E * 3 + lane] = 1.0;  // the neutral entry: t = 1 (u * s below it: k = 0)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+
     Xoro xr{0, 0};
-    const int64_t pos0 = rng.pos;
-    const bool have = !rng.tape || pos0 + NF <= rng.len;
+    const bool have = !tape || pa.pos0 + NF <= pa.len;
     if (MODE == 0) {
-        uint32_t c[4] = {(uint32_t)tid, (uint32_t)rng.ctr, (uint32_t)rng.chain,
-                         (uint32_t)(rng.ctr >> 32) ^ 0xFD000000u};
-        philox4x32_10(c, rng.key0, rng.key1);
+        uint32_t c[4] = {(uint32_t)tid, (uint32_t)pa.ctr, (uint32_t)pa.chain, (uint32_t)(pa.ctr >> 32) ^ 0xFD000000u};
+        philox4x32_10(c, pa.key0, pa.key1);
         xr.s0 = ((uint64_t)c[1] << 32) | c[0];
         xr.s1 = ((uint64_t)c[3] << 32) | c[2];
         if ((xr.s0 | xr.s1) == 0) xr.s0 = 1;
     }
-    // out-of-range stores (features outside [0, F), threads without positions or counters) are
-    // dropped by the buffer range check, so every phase issues the same memory operations
-    const __amdgpu_buffer_rsrc_t rdst = __builtin_amdgcn_make_buffer_rsrc(
-        dst, (short)0, RS ? (int)NFP : 0, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rct = __builtin_amdgcn_make_buffer_rsrc(ct, (short)0, F * td.CTP * 4, 0x00020000);
-    const int FX = S * (1 + Z);  // counter offset of the family rows
-    LogAcc acc;
+    // this lane's column values (three: j = lane, lane + 64, lane + 128 of the NL): base + feature *
+    // stride, and the column slot (-1: none; a dummy load of w[0])
+    const double *cb[3];
+    int cstr[3], cslot[3];
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        const int j0 = lane + WAVE * i;
+        cb[i] = w;
+        cstr[i] = 0;
+        cslot[i] = -1;
+        if (j0 < C) {
+            cb[i] = w + j0;
+            cstr[i] = C;
+            cslot[i] = 12 + j0;
+        } else if (j0 < td.NL) {
+            const int j = j0 - C;
+            cstr[i] = S;
+            cslot[i] = 15 + j;
+            if (j < S) {
+                cb[i] = pg + j;
+            } else if (j < FX) {
+                const int z = (j - S) / S;
+                cb[i] = pz + (size_t)z * F * S + (j - S - z * S);
+            } else {
+                const int r = (j - FX) / S;
+                cb[i] = pf + (size_t)r * F * S + (j - FX - r * S);
+            }
+        }
+    }
+    // out-of-range stores (features beyond F, positions beyond Np, counters beyond CTP) are dropped
+    // by the buffer range check
+    const __amdgpu_buffer_rsrc_t rdst = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, RS ? F * Np : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rct = __builtin_amdgcn_make_buffer_rsrc(ct, (short)0, F * CTP * 4, 0x00020000);
+    TbLogAcc acc;
     int zf = 0;
-    const int NPH = (F + TB_FP - 1) / TB_FP;  // feature pairs
-    // values in flight, each loaded two phases before its use: the column value of pair i and the
-    // observation (MODE 1: source) words of the cells of pair i - 1 (colA, obA, swA for even
-    // phases, colB, obB, swB for odd ones).  The loop runs two phases per iteration so that each
-    // load lands in the register its consumer reads (a copy of an in-flight load across the
-    // loop's back edge would wait for it there).
-    auto col_at = [&](int pr) { return ldp(tb_cb + (size_t)min(TB_FP * pr + tb_ch, F - 1) * tb_cstr); };
-    double colA = col_at(0), colB = col_at(min(1, NPH - 1));
-    uint32_t obA[TB_FP] = {}, obB[TB_FP] = {}, swA[TB_FP] = {}, swB[TB_FP] = {};
-    const uint8_t *obq = a.obs_fm + 4 * q;
-    const uint8_t *svq = sv + 4 * q;
-    auto phase = [&](int i, uint32_t (&obw)[TB_FP], uint32_t (&sww)[TB_FP], double &colw) {
-        const int pC = i - 3, pB = i - 2, pW = i - 1, pD = i - 4;
-        uint64_t st_prev = SBZ_TB_STAMP ? __builtin_amdgcn_s_memtime() : 0;
-        auto stamp = [&](int k) {
-            if (SBZ_TB_STAMP) {
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                const uint64_t t = __builtin_amdgcn_s_memtime();
-                tbst[k] += t - st_prev;
-                st_prev = t;
-            }
-        };
-        uint32_t outw[TB_FP] = {};
-        // C: the cells of pair pC, the thread's four positions of both features at once (no
-        // branch: a padding position reads the neutral entry E and is not counted)
-        if (pC >= 0 && pC < NPH) {
-            const uint4 pin = *reinterpret_cast<const uint4 *>(tb_pi + 4 * q);
-            const uint32_t pis[4] = {pin.x, pin.y, pin.z, pin.w};
-            bool val[4];
+    // a feature's loads, issued one feature ahead (a dummy feature beyond F reads the last one)
+    struct Pre {
+        double col[3];
+        uint32_t ob[TB_NCH], sw[TB_NCH];
+    };
+    auto load = [&](int f, Pre &pr) {
+        const int fl = min(f, F - 1);
 #pragma unroll
-            for (int j = 0; j < 4; j++) val[j] = hasq && 4 * q + j < N;
+        for (int i = 0; i < 3; i++) pr.col[i] = ldp(cb[i] + (size_t)fl * cstr[i]);
 #pragma unroll
-            for (int h = 0; h < TB_FP; h++) {
-                const int f = TB_FP * pC + h;
-                if (TB_FP > 1 && f >= F) break;  // (uniform: an odd F's last pair)
-                const double *T = tb_tbl + (size_t)((pC & 1) * TB_FP + h) * tb_es;
-                int *kc = tb_kc + ((pC & 1) * TB_FP + h) * tb_ks;
-                int e[4], x[4], k[4];
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const int xb = (obw[h] >> (8 * j)) & 255;
-                    x[j] = a.xs8 ? xb >> 3 : xb;
-                    e[j] = val[j] ? (int)(pis[j] & 0xffffu) + x[j] : td.E;
-                }
-                double t0[4], t1[4], t2[4];
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    t0[j] = T[e[j] * 3];
-                    t1[j] = T[e[j] * 3 + 1];
-                    t2[j] = C == 3 ? T[e[j] * 3 + 2] : 0.0;
-                }
-                if constexpr (RS) {
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        double sum = t0[j] + t1[j];
-                        if (C == 3) sum = sum + t2[j];
-                        if constexpr (TP) {
-                            // the reference's normalize + sample_categorical, bit for bit
-                            const double u = (have && val[j]) ? rng.tape[pos0 + (int64_t)a.perm[4 * q + j] * F + f] : 0.0;
-                            const double p0 = t0[j] / sum, p1 = t1[j] / sum, p2 = C == 3 ? t2[j] / sum : 0.0;
-                            const double c1 = p0 + p1, c2 = c1 + p2;
-                            k[j] = u < p0 ? 0 : (u < c1 ? 1 : ((C == 3 && u < c2) ? 2 : 0));
-                        } else {
-                            const double us = ((ABL & 8) ? 0.5 : xr.u()) * sum;
-                            k[j] = us < t0[j] ? 0 : (us < t0[j] + t1[j] ? 1 : ((C == 3 && us < sum) ? 2 : 0));
-                        }
-                        outw[h] |= (uint32_t)k[j] << (8 * j);
-                    }
-                } else {
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        k[j] = (sww[h] >> (8 * j)) & 255;
-                        if (k[j] >= C) {
-                            if (val[j] && !err) {
-                                err = 14;
-                                err_val = k[j];
-                            }
-                            k[j] = 0;
-                        }
-                    }
-                }
-                if (!(ABL & 16)) {
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        const double t = k[j] == 0 ? t0[j] : (k[j] == 1 ? t1[j] : t2[j]);
-                        acc.m *= __builtin_amdgcn_frexp_mant(t);
-                        acc.e += __builtin_amdgcn_frexp_exp(t);
-                    }
-                    renorm(acc.m, acc.e);
-                }
-                if (!(ABL & 1)) {
-                    int hk[4];
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        const int zc = (pis[j] >> 16) & 255, fc = (int)(pis[j] >> 24);
-                        int ci = -1;
-                        if (x[j] < S) {
-                            if (k[j] == 0) ci = x[j];
-                            else if (k[j] == 1 && zc < Z) ci = S + zc * S + x[j];
-                            else if (k[j] == 2 && fc > 0) ci = FX + (fc - 1) * S + x[j];
-                        }
-                        if (val[j] && ci >= 0) atomicAdd(&kc[ci], 1);
-                        hk[j] = val[j] ? ((zc < Z ? 1 : 0) | (fc > 0 ? 2 : 0)) * 3 + k[j] : 15;
-                    }
-                    // the (class, component) counts of this wave's cells by ballot: lane c gets
-                    // category c's count and writes it to the wave's slot
-                    int myc = 0;
-#pragma unroll
-                    for (int c = 0; c < 12; c++) {
-                        int n = 0;
-#pragma unroll
-                        for (int j = 0; j < 4; j++) n += __popcll(__ballot(hk[j] == c));
-                        myc = lane == c ? n : myc;
-                    }
-                    if (lane < 12) kc[td.WOFF + 16 * wv + lane] = myc;
-                }
-            }
+        for (int r = 0; r < TB_NCH; r++) {
+            const int p0 = min(256 * r + 4 * lane, Np - 4);
+            pr.ob[r] = *reinterpret_cast<const uint32_t *>(obs_fm + (size_t)fl * Np + p0);
+            if (!RS)
+                pr.sw[r] = __hip_atomic_load(reinterpret_cast<const uint32_t *>(sv + (size_t)fl * Np + p0), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
         }
+    };
+    auto process = [&](int f, const Pre &pr) {
+        // the column, then the normalised weights of the 4 classes (lanes 0..11) and their zero mask
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+            if (cslot[i] >= 0) cs[cslot[i]] = pr.col[i];
+        wsync();
+        bool wz = false;
+        if (lane < 12) {
+            const int h = lane / 3, k = lane - h * 3;
+            const double w0 = cs[12] * 1.0, w1 = cs[13] * ((h & 1) ? 1.0 : 0.0);
+            double sum = w0 + w1, w2 = 0.0;
+            if (C == 3) {
+                w2 = cs[14] * ((h & 2) ? 1.0 : 0.0);
+                sum = sum + w2;
+            }
+            const double wn = k == 0 ? w0 / sum : (k == 1 ? w1 / sum : (C == 3 ? w2 / sum : 0.0));
+            cs[lane] = wn;
+            wz = k < C && wn == 0.0;
+        }
+        const uint32_t zmask = (uint32_t)__ballot(wz);
+        wsync();
         stamp(0);
-        // D: the counts of pair pD out to the count table (the class counts summed over the
-        // waves), the component-row counters cleared for pD + 2
-        int cv = 0;
-        const int dh = tid / td.CTP, dt = tid - dh * td.CTP, fD = TB_FP * pD + dh;
-        const bool dok = pD >= 0 && pD < NPH && dh < TB_FP && fD < F;
-        if (dok) {
-            int *kc = tb_kc + ((pD & 1) * TB_FP + dh) * tb_ks;
-            const int hk = dt - td.WOFF;
-            if (hk < 0) {
-                cv = kc[dt];
-                kc[dt] = 0;
-            } else {  // (every wave rewrites its slots for each feature: no clearing)
-#pragma unroll
-                for (int w2 = 0; w2 < NW; w2++) cv += kc[td.WOFF + 16 * w2 + hk];
-                // a selected normalised weight 0 (the table's zero mask) with a source on it
-                if (((tb_zm[(pD & 3) * TB_FP + dh] >> hk) & 1) && cv > 0) zf = 1;
-            }
-        }
-        stamp(1);
-        // B: the tables of pair pB (obs_terms' operations: t_k = l_k * w_norm_k)
-        if (pB >= 0 && pB < NPH && !(ABL & 4)) {
-            for (int e2 = tid; e2 < TB_FP * td.E; e2 += NT) {
-                const int h = e2 / td.E, e = e2 - h * td.E;
-                if (TB_FP * pB + h >= F) continue;
-                const int x = e % (S + 1), r = e / (S + 1);
-                const int zc = r / td.FamC, fc = r - zc * td.FamC;
-                const double *cs = tb_col + (size_t)((pB % 3) * TB_FP + h) * tb_cs;
+        // the table: t_k = l_k * w_norm_k (obs_terms' operations)
+        if (!(ABL & 4)) {
+#pragma unroll 2
+            for (int e = lane; e < E; e += WAVE) {
+                const uint32_t ed = edl[e];
+                const int x = ed & 255, zc = (ed >> 8) & 255, fc = (int)(ed >> 16);
                 const bool hz = zc < Z, hf = C == 3 && fc > 0, na = x >= S;
                 const int xc = na ? 0 : x;
                 const double *wn = cs + ((hz ? 1 : 0) | (hf ? 2 : 0)) * 3;
@@ -540,70 +443,143 @@ __device__ __noinline__ TbPassOut tb_pass(TbPassArgs pa) {
                 const double l0 = na ? 1.0 : pp[xc];
                 const double l1 = na ? 1.0 : (hz ? pp[S + zc * S + xc] : 0.0);
                 const double l2 = C == 3 ? (na ? 1.0 : (hf ? pp[FX + (fc - 1) * S + xc] : 0.0)) : 0.0;
-                double *Ep = tb_tbl + (size_t)((pB & 1) * TB_FP + h) * tb_es + e * 3;
-                Ep[0] = l0 * wn[0];
-                Ep[1] = l1 * wn[1];
-                Ep[2] = C == 3 ? l2 * wn[2] : 0.0;
+                T[e * 3] = l0 * wn[0];
+                T[e * 3 + 1] = l1 * wn[1];
+                T[e * 3 + 2] = C == 3 ? l2 * wn[2] : 0.0;
             }
-            if (tid < TB_FP) {
-                const double *cs = tb_col + (size_t)((pB % 3) * TB_FP + tid) * tb_cs;
-                int m = 0;
+        }
+        wsync();
+        stamp(1);
+        // the cells: chunk r holds positions 256 r + 4 lane .. + 3
+        uint32_t R[3] = {0, 0, 0};  // class counts by component, 8-bit fields by class h
+#pragma unroll 1
+        for (int r = 0; r < TB_NCH; r++) {
+            const int p0 = 256 * r + 4 * lane;
+            // the chunk's observation (source) word, selected without indexing the register array
+            uint32_t obw = pr.ob[0], sww = pr.sw[0];
 #pragma unroll
-                for (int hk = 0; hk < 12; hk++)
-                    if (hk % 3 < C && cs[hk] == 0.0) m |= 1 << hk;
-                tb_zm[(pB & 3) * TB_FP + tid] = m;
+            for (int i = 1; i < TB_NCH; i++) {
+                obw = r == i ? pr.ob[i] : obw;
+                if (!RS) sww = r == i ? pr.sw[i] : sww;
             }
+            const uint4 pin = *reinterpret_cast<const uint4 *>(pinfo + min(p0, Np - 4));
+            const uint32_t pis[4] = {pin.x, pin.y, pin.z, pin.w};
+            uint32_t outw = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                // (selects, no branches: every lane runs the same instructions)
+                const bool val = p0 + j < N;
+                const int xb = (obw >> (8 * j)) & 255;
+                const int x = pa.xs8 ? xb >> 3 : xb;
+                const int e = val ? (int)(pis[j] & 0xffffu) + x : E;
+                const double t0 = T[e * 3], t1 = T[e * 3 + 1], t2 = C == 3 ? T[e * 3 + 2] : 0.0;
+                int k;
+                if constexpr (RS) {
+                    double sum = t0 + t1;
+                    if (C == 3) sum = sum + t2;
+                    if constexpr (TP) {
+                        // the reference's normalize + sample_categorical, bit for bit
+                        const double u = (have && val) ? tape[pa.pos0 + (int64_t)perm[p0 + j] * F + f] : 0.0;
+                        const double q0 = t0 / sum, q1 = t1 / sum, q2 = C == 3 ? t2 / sum : 0.0;
+                        const double c1 = q0 + q1, c2 = c1 + q2;
+                        const int k12 = u < c1 ? 1 : ((C == 3 && u < c2) ? 2 : 0);
+                        k = u < q0 ? 0 : k12;
+                    } else {
+                        const double us = ((ABL & 8) ? 0.5 : xr.u()) * sum;
+                        const int k12 = us < t0 + t1 ? 1 : ((C == 3 && us < sum) ? 2 : 0);
+                        k = us < t0 ? 0 : k12;
+                    }
+                    outw |= (uint32_t)k << (8 * j);
+                } else {
+                    k = (sww >> (8 * j)) & 255;
+                    if (k >= C && val && !err) {
+                        err = 14;
+                        err_val = k;
+                    }
+                    k = k < C ? k : 0;
+                }
+                const double t = __longlong_as_double(
+                    k == 0 ? __double_as_longlong(t0) : (k == 1 ? __double_as_longlong(t1) : __double_as_longlong(t2)));
+                if (!(ABL & 16)) {
+                    acc.m *= __builtin_amdgcn_frexp_mant(t);
+                    acc.e += __builtin_amdgcn_frexp_exp(t);
+                }
+                const int zc = (pis[j] >> 16) & 255, fc = (int)(pis[j] >> 24);
+                const bool hz = zc < Z, hf = fc > 0;
+                if (!(ABL & 1)) {
+                    // the component row's counter: p_global [x], p_zones [zc][x], p_families [fc - 1][x]
+                    const int row = k == 0 ? 0 : (k == 1 ? S + zc * S : FX + (fc - 1) * S);
+                    const bool cnt_it = val && x < S && (k == 0 || (k == 1 && hz) || (k == 2 && hf));
+                    if (cnt_it) atomicAdd(&kc[row + x], 1);
+                }
+                const uint32_t inc = val ? 1u << (8 * ((hz ? 1 : 0) | (hf ? 2 : 0))) : 0u;
+                R[0] += k == 0 ? inc : 0u;
+                R[1] += k == 1 ? inc : 0u;
+                R[2] += k == 2 ? inc : 0u;
+            }
+            renorm(acc.m, acc.e);
+            if (RS)
+                __builtin_amdgcn_raw_buffer_store_b32(outw, rdst, (f < F && p0 < Np) ? f * Np + p0 : 0x7ffffff0, 0, 16);
         }
         stamp(2);
-        // W: normalize_weights (model.py:436-452) of pair pW for the 4 classes
-        if (pW >= 0 && pW < NPH && tid < 12 * TB_FP) {
-            const int h2 = tid / 12, t12 = tid - h2 * 12;
-            double *cs = tb_col + (size_t)((pW % 3) * TB_FP + h2) * tb_cs;
-            const int h = t12 / 3, k = t12 - h * 3;
-            const double w0 = cs[12] * 1.0, w1 = cs[13] * ((h & 1) ? 1.0 : 0.0);
-            double sum = w0 + w1, w2 = 0.0;
-            if (C == 3) {
-                w2 = cs[14] * ((h & 2) ? 1.0 : 0.0);
-                sum = sum + w2;
+        // the class counts [h][k] (wave sums of the 8-bit fields), then the block out to the count
+        // table and cleared
+        int myc = 0;
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            if (k >= C) break;
+#pragma unroll
+            for (int h = 0; h < 4; h++) {
+                const int n = wave_sum_i((int)((R[k] >> (8 * h)) & 255u));
+                myc = lane == h * 3 + k ? n : myc;
+                if (((zmask >> (h * 3 + k)) & 1) && n > 0) zf = 1;
             }
-            cs[t12] = k == 0 ? w0 / sum : (k == 1 ? w1 / sum : (C == 3 ? w2 / sum : 0.0));
         }
-        // A: the column of pair i (loaded two phases before) into its slot
-        if (i < NPH && tb_cj >= 0) tb_col[(size_t)((i % 3) * TB_FP + tb_ch) * tb_cs + tb_cj] = colw;
+        if (lane < 12) kc[WOFF + lane] = myc;
+        wsync();
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            const int idx = lane + WAVE * i;
+            int v = 0;
+            if (idx < CTP) {
+                v = kc[idx];
+                kc[idx] = 0;
+            }
+            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, rct, (f < F && idx < CTP) ? (f * CTP + idx) * 4 : 0x7ffffff0,
+                                                  0, 16);
+        }
+        wsync();
         stamp(3);
-        // memory operations, the same every phase: the new source words of pC, the counts of pD,
-        // then the loads of the column of pair i + 2 and of the observation (source) words of pair
-        // i - 1 (their cells are processed in phase i + 2)
-        if (RS) {
-#pragma unroll
-            for (int h = 0; h < TB_FP; h++) {
-                const int f = TB_FP * pC + h;
-                __builtin_amdgcn_raw_buffer_store_b32(outw[h], rdst, (pC >= 0 && f < F && hasq) ? f * Np + 4 * q : 0x7ffffff0,
-                                                      0, 16);
-            }
-        }
-        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)cv, rct, dok ? (fD * td.CTP + dt) * 4 : 0x7ffffff0, 0, 16);
-        colw = col_at(min(i + 2, NPH - 1));
-#pragma unroll
-        for (int h = 0; h < TB_FP; h++) {
-            const int fo = min(max(TB_FP * (i - 1) + h, 0), F - 1);
-            obw[h] = *reinterpret_cast<const uint32_t *>(obq + (size_t)fo * Np);
-            if (!RS)
-                sww[h] = __hip_atomic_load(reinterpret_cast<const uint32_t *>(svq + (size_t)fo * Np),
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        stamp(4);
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        stamp(5);
     };
-    for (int i = 0; i <= NPH + 3; i += 2) {
-        phase(i, obA, swA, colA);
-        phase(i + 1, obB, swB, colB);
+    Pre A, B;
+    load(wv, A);
+    load(wv + NW, B);
+    for (int f = wv; f < F; f += 2 * NW) {
+        process(f, A);
+        load(f + 2 * NW, A);
+        if (f + NW < F) process(f + NW, B);
+        load(f + 3 * NW, B);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sources and counts have landed
+    // block reductions, wave partials added in wave order; a trailing barrier, so the caller's next
+    // reduction may reuse the slots
+    double v = wave_sum(acc.value());
+    const int zw = __ballot(zf != 0) ? 1 : 0;
+    if (lane == 0) {
+        red[wv] = v;
+        redi[wv] = zw;
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    double tot = red[0];
+    int zt = redi[0];
+#pragma unroll
+    for (int i = 1; i < NW; i++) {
+        tot += red[i];
+        zt |= redi[i];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     TbPassOut o;
-    o.ll = bsum(acc.value());  // (bsum's barrier publishes them)
-    if (bor(zf)) o.ll = -INFINITY;
+    o.ll = uni(zt ? -INFINITY : tot);
     o.err = err;
     o.err_val = err_val;
     o.bad = TP && !have ? 1 : 0;
@@ -1063,45 +1039,10 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         sync();
     };
 
-    // ---- TB: the feature-table passes (TbDims) and the chain's count tables (current / candidate)
+    // ---- TB: the feature-table passes (tb_pass) and the chain's count tables (current / candidate)
     const TbDims td = tb_dims(S, Z, Fam, C);
-    const TbLayout tl = tb_layout(td, Np);
-    unsigned char *tbase = lds + uni_off;
-    const int tb_es = (td.E + 1) * 3;                              // doubles per feature table
-    double *tb_tbl = reinterpret_cast<double *>(tbase + tl.tbl);   // [2][TB_FP][E + 1][3]: t0 t1 t2
-    const int tb_cs = tb_cslots(td);
-    double *tb_col = reinterpret_cast<double *>(tbase + tl.col);   // [3][TB_FP][cs]
-    const int tb_ks = tb_kstride(td);
-    int *tb_kc = reinterpret_cast<int *>(tbase + tl.kcnt);         // [2][TB_FP][ks]
-    int *tb_zm = reinterpret_cast<int *>(tbase + tl.zm);           // [4][TB_FP]
-    uint32_t *tb_pi = reinterpret_cast<uint32_t *>(tbase + tl.pinfo);  // [Np]
     int *ct_cur = TB ? a.ctab + (size_t)b * F * td.CTP : nullptr;
     int *ct_alt = TB ? a.ctab + a.ct_half + (size_t)b * F * td.CTP : nullptr;
-    // this thread's column value (TbDims::NL) of a phase: feature TB_FP * pair + tb_ch, base +
-    // feature * stride (a dummy w[0] beyond TB_FP * NL)
-    const double *tb_cb = w;
-    int tb_cstr = 0, tb_ch = 0, tb_cj = -1;
-    if (tid < TB_FP * td.NL) {
-        tb_ch = tid / td.NL;
-        const int j0 = tid - tb_ch * td.NL;
-        tb_cj = j0 < C ? 12 + j0 : 15 + j0 - C;  // its slot in the column
-        if (j0 < C) {
-            tb_cb = w + j0;
-            tb_cstr = C;
-        } else {
-            const int j = j0 - C;
-            tb_cstr = S;
-            if (j < S) {
-                tb_cb = pg + j;
-            } else if (j < S * (1 + Z)) {
-                const int z = (j - S) / S;
-                tb_cb = pz + (size_t)z * F * S + (j - S - z * S);
-            } else {
-                const int r = (j - S * (1 + Z)) / S;
-                tb_cb = pf + (size_t)r * F * S + (j - S * (1 + Z) - r * S);
-            }
-        }
-    }
     // One pass over every observation (tb_pass), the generator advanced as the pass drew
     uint64_t tbst[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     auto tpass = [&](auto mode_c, const uint8_t *sv, uint8_t *dst, int *ct) -> double {
@@ -1114,24 +1055,17 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         pa.Np = Np;
         pa.xs8 = a.xs8;
         pa.td = td;
-        pa.es = tb_es;
-        pa.cs = tb_cs;
-        pa.ks = tb_ks;
         pa.perm = (gbl_ptr<const int>)a.perm;
         pa.famc = (gbl_ptr<const uint8_t>)a.famc;
         pa.obs_fm = (gbl_ptr<const uint8_t>)a.obs_fm;
         pa.zos = (lds_ptr<uint8_t>)zos;
-        pa.tbl = (lds_ptr<double>)tb_tbl;
-        pa.col = (lds_ptr<double>)tb_col;
-        pa.kc = (lds_ptr<int>)tb_kc;
-        pa.zm = (lds_ptr<int>)tb_zm;
-        pa.pi = (lds_ptr<uint32_t>)tb_pi;
+        pa.base = (lds_ptr<unsigned char>)(lds + uni_off);
         pa.red = (lds_ptr<double>)red;
         pa.redi = (lds_ptr<int>)redi;
-        pa.cb = (gbl_ptr<const double>)tb_cb;
-        pa.cstr = tb_cstr;
-        pa.ch = tb_ch;
-        pa.cj = tb_cj;
+        pa.w = (gbl_ptr<const double>)w;
+        pa.pg = (gbl_ptr<const double>)pg;
+        pa.pz = (gbl_ptr<const double>)pz;
+        pa.pf = (gbl_ptr<const double>)pf;
         pa.sv = (gbl_ptr<const uint8_t>)sv;
         pa.dst = (gbl_ptr<uint8_t>)dst;
         pa.ct = (gbl_ptr<int>)ct;
@@ -1963,11 +1897,11 @@ int launch_mh_source(sbz_ctx *ctx, int B, const MhArgs &a0) {
     // sources in HBM: the feature-table passes and count tables where they apply (4 or 8 waves,
     // one source dword per thread and feature, the tables within LDS; SBZ_OPT_SRC_PASS_TABLES 0: off)
     const TbDims td = tb_dims(d.n_states, d.n_zones, d.n_families, ctx->C);
-    const bool tb = gs && ctx->src_pass_tables && nw >= 4 && tb_fits(td, ctx->Np, nw * WAVE) &&
-                    mh_src_lds_bytes(d, ctx->C, true, geo, false, true, ctx->Np) + gib <= LDS_MAX;
+    const bool tb = gs && ctx->src_pass_tables && nw >= 4 && tb_fits(td, ctx->Np) &&
+                    mh_src_lds_bytes(d, ctx->C, true, geo, false, true, ctx->Np, nw) + gib <= LDS_MAX;
     // parameters staged in LDS when they fit too (SBZ_OPT_SRC_STAGE 0: off; not with the table passes)
     a.stage = !tb && ctx->src_stage && mh_src_lds_bytes(d, ctx->C, gs, geo, true) + gib <= LDS_MAX ? 1 : 0;
-    size_t lds = mh_src_lds_bytes(d, ctx->C, gs, geo, a.stage != 0, tb, ctx->Np);
+    size_t lds = mh_src_lds_bytes(d, ctx->C, gs, geo, a.stage != 0, tb, ctx->Np, nw);
     // the constant tables too, when they fit beside the staged parameters
     const size_t cst = mh_src_const_bytes(d, ctx->C, a.alpha_g != nullptr, a.alpha_f != nullptr,
                                           a.gc_g != nullptr, a.gc_f != nullptr);

@@ -130,6 +130,11 @@ def load_config(config_file, custom_settings=None, simulated=False):
             if "file" in prior:
                 prior["file"] = fix(prior["file"])
     mcmc["N_CHAINS"] = 1  # MC3 is disabled in the reference (experiment_setup.py:200-206)
+    # independent main-run chains (an extension, MC3 still off): chain 0 is the reference's logged
+    # chain; chains 1.. get results files of their own (run_experiment)
+    k = mcmc.setdefault("INDEPENDENT_CHAINS", 1)
+    if not isinstance(k, int) or k < 1:
+        raise ValueError(f"INDEPENDENT_CHAINS must be a positive integer, got {k!r}")
     if mcmc["N_STEPS"] % mcmc["N_SAMPLES"] != 0:
         raise ValueError("Non-consistent spacing between samples. Set N_STEPS to be a multiple of N_SAMPLES. ")
     steps = mcmc["STEPS"]
@@ -381,13 +386,17 @@ def run_experiment(config, data, n_zones, run=0, name="experiment", seed=None, d
                                  warm_up_steps=mc["WARM_UP"]["N_WARM_UP_STEPS"])
     logger.info("warm-up: %d chains x %d steps in %.2f s", warm.n_chains, mc["WARM_UP"]["N_WARM_UP_STEPS"],
                 time.time() - t0)
-    smp = BatchedZoneMCMC(n_chains=mc["N_CHAINS"], initial_sample=best, seed=seeds["sample"], **common)
+    # the main run: N_CHAINS (1, MC3 off) or INDEPENDENT_CHAINS chains, all starting from the
+    # warm-up's best sample, sharded over the ranks; with more than one, every chain's samples are
+    # gathered to rank 0 at the end of the run (BatchedZoneMCMC.chain_statistics)
+    n_main = max(int(mc["N_CHAINS"]), int(mc.get("INDEPENDENT_CHAINS", 1)))
+    smp = BatchedZoneMCMC(n_chains=n_main, initial_sample=best, seed=seeds["sample"],
+                          log_all_chains=n_main > 1, **common)
     smp.generate_samples(mc["N_STEPS"], mc["N_SAMPLES"])
     if getattr(smp, "rank", 0) != 0:
         # chain_idx[0] (the logged chain) lives on rank 0: the other ranks have nothing to write
         return smp.statistics, None
-    contribution_per_area(smp)
-    stats = rank_areas(match_areas(smp.statistics))
+    per_chain = smp.chain_statistics or [smp.statistics]
     info = cfg["results"]["FILE_INFO"]
     if info == "n":
         fi = f"n{n_zones}"
@@ -403,17 +412,31 @@ def run_experiment(config, data, n_zones, run=0, name="experiment", seed=None, d
         raise ValueError("file_info must be 'n', 's', 'i' or 'p'")
     pth = os.path.join(cfg["results"]["RESULTS_PATH"], name, fi)
     os.makedirs(pth, exist_ok=True)
-    paths = {"parameters": os.path.join(pth, f"stats_{fi}_{run}.txt"),
-             "areas": os.path.join(pth, f"areas_{fi}_{run}.txt"),
-             "gt": os.path.join(pth, "ground_truth", "stats.txt"),
-             "gt_areas": os.path.join(pth, "ground_truth", "areas.txt")}
-    if getattr(data, "is_simulated", False):  # MCMC.save_samples (mcmc_setup.py:227-229)
-        eval_ground_truth(smp, data, bool(cfg["model"]["INHERITANCE"]), stats)
-        os.makedirs(os.path.dirname(paths["gt"]), exist_ok=True)
-    io.samples2file(stats, data, cfg, paths)
-    logger.info("sampling: %d steps, acceptance %.3f, %.2f s; results in %s", mc["N_STEPS"],
-                stats["acceptance_ratio"], stats["sampling_time"], pth)
-    return stats, paths
+    out = None
+    for c, chain_stats in enumerate(per_chain):
+        # chain 0: the reference's files; chain c > 0: the same files with a _chain<c> suffix
+        sfx = "" if c == 0 else f"_chain{c}"
+        paths = {"parameters": os.path.join(pth, f"stats_{fi}_{run}{sfx}.txt"),
+                 "areas": os.path.join(pth, f"areas_{fi}_{run}{sfx}.txt"),
+                 "gt": os.path.join(pth, "ground_truth", "stats.txt"),
+                 "gt_areas": os.path.join(pth, "ground_truth", "areas.txt")}
+        main_stats = smp.statistics
+        smp.statistics = chain_stats
+        try:
+            contribution_per_area(smp)
+            stats = rank_areas(match_areas(smp.statistics))
+        finally:
+            smp.statistics = main_stats
+        if getattr(data, "is_simulated", False):  # MCMC.save_samples (mcmc_setup.py:227-229)
+            eval_ground_truth(smp, data, bool(cfg["model"]["INHERITANCE"]), stats)
+            os.makedirs(os.path.dirname(paths["gt"]), exist_ok=True)
+        io.samples2file(stats, data, cfg, paths)
+        if c == 0:
+            out = (stats, paths)
+    stats = out[0]
+    logger.info("sampling: %d steps x %d chain(s), acceptance %.3f, %.2f s; results in %s", mc["N_STEPS"],
+                len(per_chain), stats["acceptance_ratio"], stats["sampling_time"], pth)
+    return out
 
 
 def main(argv=None):
@@ -424,13 +447,20 @@ def main(argv=None):
     p.add_argument("--seed", type=int, default=None)
     p.add_argument("--device", type=int, default=None)
     p.add_argument("--set", default=None, help="JSON object merged into the config (custom settings)")
+    p.add_argument("--chains", type=int, default=None,
+                   help="independent main-run chains (mcmc.INDEPENDENT_CHAINS; MC3 stays off): chain 0 "
+                        "writes the reference's results files, chain c > 0 the same files with a _chain<c> "
+                        "suffix; the chains are sharded over the ranks and gathered to rank 0 at the end")
     p.add_argument("--sim-data", default=None,
                    help="simulation config: the simulated data and its ground truth (.npz, SimulatedData.from_npz)")
     a = p.parse_args(argv)
     rank, device = init_distributed(a.device)
     logging.basicConfig(level=logging.INFO if rank == 0 else logging.WARNING, format="%(message)s")
     logger = logging.getLogger("sbz")
-    config, _ = load_config(a.config, json.loads(a.set) if a.set else None, simulated=a.sim_data is not None)
+    custom = json.loads(a.set) if a.set else {}
+    if a.chains is not None:
+        custom.setdefault("mcmc", {})["INDEPENDENT_CHAINS"] = a.chains
+    config, _ = load_config(a.config, custom or None, simulated=a.sim_data is not None)
     name = a.name or time.strftime("%Y%m%d-%H%M%S")
     data = SimulatedData.from_npz(a.sim_data) if a.sim_data else ExperimentData(config)
     for line in data.log:

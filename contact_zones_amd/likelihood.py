@@ -107,7 +107,8 @@ class LikelihoodEngine:
         check(self._lib.sbz_synchronize(self.ctx), self.ctx)
 
     def last_kernels(self):
-        """Names of the kernels the last likelihood launch ran (sbz_last_kernels)."""
+        """Names of the kernels the context's last launch ran (sbz_last_kernels): a likelihood
+        launch's, or the source-mode sampler's variant."""
         return self._lib.sbz_last_kernels(self.ctx).decode()
 
     def lds_bytes(self, source_mode=False):

@@ -281,7 +281,7 @@ class BatchedZoneMCMC:
                  initial_size, initial_sample=None, mc3=False, swap_period=None, chain_swaps=None,
                  sample_from_prior=False, show_screen_log=False, logger=None, *, seed=None,
                  rng=None, device=None, group=None, refresh_every_launch=True, priors=None,
-                 gibbs_counts=None, **kwargs):
+                 gibbs_counts=None, log_all_chains=False, **kwargs):
         if mc3:
             raise NotImplementedError("MC3 chain swaps are not part of the batched sampler")
         if sample_from_prior:
@@ -339,6 +339,11 @@ class BatchedZoneMCMC:
                            'acceptance_ratio': math.nan, 'accepted_steps': 0, 'n_swaps': 0,
                            'accepted_swaps': 0, 'swap_ratio': [],
                            'accept_operator': defaultdict(int), 'reject_operator': defaultdict(int)}
+        # independent-chains runs (the runner's --chains): every chain's samples are logged too,
+        # kept on the device until the run ends and then gathered to rank 0 (chain_statistics)
+        self.log_all_chains = bool(log_all_chains)
+        self.chain_statistics = None
+        self._snaps = []
         self._ll = np.full(self.n_chains, -np.inf)
         self._prior = np.full(self.n_chains, -np.inf)
         self.t_start = time.time()
@@ -598,6 +603,8 @@ class BatchedZoneMCMC:
             self._advance(i_step + 1 - done)
             done = i_step + 1
             if i_step % steps_per_sample == 0:
+                if self.log_all_chains:
+                    self._snap(int(i_step / steps_per_sample))
                 s0 = self._chain0_sample()
                 if self.rank == 0:
                     # the logged sample's prior evaluated in full (the carried value differs by
@@ -618,6 +625,8 @@ class BatchedZoneMCMC:
             st = self._state
             self._resolve_alias(st.p_global[0], st.p_zones[0],
                                 st.p_fam[0] if st.p_fam is not None else None)
+        if self.log_all_chains:
+            self.chain_statistics = self._gather_chains()
         t_end = time.time()
         self._count_operators()
         self.statistics['sampling_time'] = t_end - t_start
@@ -625,6 +634,63 @@ class BatchedZoneMCMC:
         self.statistics['acceptance_ratio'] = self.statistics['accepted_steps'] / n_steps
         self.statistics['swap_ratio'] = 0
         return None
+
+    def _snap(self, sample_id):
+        """Copy of this rank's chains at a logging point (device tensors, gathered at the end)."""
+        import torch
+        st = self._state
+        if st is None:
+            self._snaps.append(None)
+            return
+        self._snaps.append({"id": sample_id, "zos": st.zone_of_site.clone(), "w": st.w.clone(),
+                            "pg": st.p_global.clone(), "pz": st.p_zones.clone(),
+                            "pf": st.p_fam.clone() if st.p_fam is not None else None,
+                            "ll": st.ll.clone()})
+
+    def _gather_chains(self):
+        """Every chain's logged samples on rank 0: this rank's snapshots stacked per chain
+        ([chains][samples][...]), then one gather of the shards per array over the ranks
+        (parallel.gather_rows: RCCL over xGMI with the nccl backend).  Returns, on rank 0, one
+        statistics dict per global chain with the keys samples2file reads (the logged prior is
+        evaluated in full on the host, as for the logged chain); None on the other ranks.  Chain 0
+        is the logged chain: its dict is `statistics` itself."""
+        import torch
+        from .parallel import gather_rows
+        n, B = len(self._snaps), self.hi - self.lo
+        N, F, S, Z = self.n_sites, self.n_features, self.n_states, self.n_zones
+        C = 3 if self.inheritance else 2
+        Fam = self.n_families if self.inheritance else 0
+        dev = self._state.ll.device if self._state is not None else torch.device("cpu")
+        shapes = {"zos": ((N,), torch.uint8), "w": ((F, C), torch.float64), "pg": ((F, S), torch.float64),
+                  "pz": ((Z, F, S), torch.float64), "ll": ((), torch.float64)}
+        if self.inheritance:
+            shapes["pf"] = ((Fam, F, S), torch.float64)
+        ids = [sn["id"] for sn in self._snaps] if n and self._snaps[0] is not None else list(range(n))
+        full = {}
+        for k, (shp, dt) in shapes.items():
+            loc = (torch.stack([sn[k] for sn in self._snaps], 1) if B and n
+                   else torch.zeros((B, n) + shp, dtype=dt, device=dev))
+            full[k] = gather_rows(loc, self.n_chains, self._group)
+        self._snaps = []
+        if self.rank != 0:
+            return None
+        host = {k: v.cpu().numpy() for k, v in full.items()}
+        out = [self.statistics]
+        for c in range(1, self.n_chains):
+            zos = host["zos"][c]
+            pf = host["pf"][c] if self.inheritance else None
+            prior = self.priors.log_prior(zos, host["pg"][c], pf, self.applicable_states, self.n_zones,
+                                          self.inheritance) if n else np.zeros(0)
+            st = {'sample_id': list(ids), 'sample_likelihood': [float(v) for v in host["ll"][c]],
+                  'sample_prior': [float(v) for v in prior],
+                  'sample_zones': [packing.index_to_groups(z, Z) for z in zos],
+                  'sample_weights': list(host["w"][c]),
+                  'sample_p_global': [p[None] for p in host["pg"][c]],
+                  'sample_p_zones': list(host["pz"][c]),
+                  'sample_p_families': list(pf) if pf is not None else [None] * n,
+                  'last_sample': [], 'chain': c}
+            out.append(st)
+        return out
 
     def _count_operators(self):
         acc, prop = self._operator_counts()

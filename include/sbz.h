@@ -186,8 +186,10 @@ int sbz_memcpy_d2h(sbz_ctx *ctx, void *dst, const void *src, uint64_t bytes);
 /* Bytes of LDS the likelihood kernel needs per workgroup for these dims (0 if unsupported). */
 uint64_t sbz_lik_lds_bytes(const sbz_dims *dims, int source_mode);
 
-/* Diagnostics: the kernels the context's last likelihood launch ran, space-separated (e.g.
- * "repack_source_kernel lik_source_rc_kernel"), "" before the first. */
+/* Diagnostics: the kernels the context's last launch ran, space-separated (a likelihood launch,
+ * e.g. "lik_mixture_kernel" or "lik_source_rc_kernel"; a source-mode sampler launch,
+ * "mh_src_kernel<lds>", "mh_src_kernel<hbm>" or "mh_src_kernel<hbm, tables>"), "" before the
+ * first. */
 const char *sbz_last_kernels(const sbz_ctx *ctx);
 
 /* Diagnostics: n draws of the samplers' gamma generator (LaneRng::gamma, Marsaglia-Tsang on
@@ -346,7 +348,9 @@ typedef struct sbz_trace {            /* per-step trace, [B][n_steps] each, or N
 int sbz_mh_run(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg, uint64_t seed,
                const sbz_tape *tape, sbz_state *io_state, sbz_trace *out_trace);
 
-/* Bytes of LDS the sampler needs per chain for these dims (0 if above the 160 KiB of a CU). */
+/* Bytes of LDS the SAMPLE_SOURCE = false sampler needs per chain for these dims (0 if above the
+ * 160 KiB of a CU), for an operator table without gibbsish_sample_zones: a non-zero weight on it
+ * adds 17 * n_sites bytes of scratch, which sbz_mh_run_device checks (SBZ_EINVAL beyond the 160 KiB). */
 uint64_t sbz_mh_lds_bytes(const sbz_dims *dims);
 
 #ifdef __cplusplus

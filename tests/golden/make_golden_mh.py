@@ -502,6 +502,14 @@ def real_cases():
         run_case(f"src_{tag}_z{z}", data, model, mcmc, steps=100, seed=seed, warmup=False, n_chains=2)
 
 
+def sa_sweep_cases():
+    """South America with K = 2..5 zones (BASELINE configs[3] sweeps K = 1..6; real_cases holds
+    K = 1 and 6): the same capture, 2 chains x 100 steps each."""
+    for z, seed in ((2, 34), (3, 35), (4, 36), (5, 37)):
+        data, model, mcmc = real_data("south_america", z)
+        run_case(f"src_sa_z{z}", data, model, mcmc, steps=100, seed=seed, warmup=False, n_chains=2)
+
+
 def gibbsish_cases():
     """gibbsish_sample_zones (zone_sampling.py:619-702) with a non-zero operator weight.  The
     reference's own operator table gives it weight 0 (mcmc_setup.py:77, 'area' * 0.0), so these
@@ -541,6 +549,9 @@ def main():
         return
     if len(sys.argv) > 1 and sys.argv[1] == "real":
         real_cases()
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "sa_sweep":
+        sa_sweep_cases()
         return
     d = sim_data()
     run_case("cfg1_sim", d, model_cfg(1, False), mcmc_cfg(inheritance=0.0), steps=300, seed=3,

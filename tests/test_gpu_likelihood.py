@@ -1,9 +1,10 @@
 """GPU parity: the HIP likelihood vs the reference's golden values and the oracle.
 
 Tolerance (north_star): log-likelihoods within 1e-9 relative of the reference CPU
-path.  Each table entry is computed in the reference's operation order, so the only
-difference is the reduction (product accumulation + one log per lane + fp64 tree
-sum); in practice the error is ~1e-15 relative.
+path.  Each table entry is computed in the reference's operation order with fused
+multiply-adds (an entry within an ulp of the reference's cell), and the reduction differs
+(product accumulation + one log per lane + fp64 tree sum); in practice the error is
+~1e-15 relative.
 """
 import numpy as np
 import pytest

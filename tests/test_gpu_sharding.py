@@ -36,12 +36,14 @@ def _env(**extra):
     return env
 
 
-def _run(out, ranks, source):
+def _run(out, ranks, source, chains=None):
     settings = {"model": {"N_AREAS": 2, "SAMPLE_SOURCE": source},
                 "mcmc": {"N_STEPS": 3000, "N_SAMPLES": 30, "N_CHAINS": 5,
                          "WARM_UP": {"N_WARM_UP_STEPS": 600, "N_WARM_UP_CHAINS": 7}},
                 "results": {"RESULTS_PATH": str(out)}}
     args = ["-m", "contact_zones_amd", CFG, "--seed", "11", "--name", "x", "--set", json.dumps(settings)]
+    if chains is not None:
+        args += ["--chains", str(chains)]
     if ranks == 1:
         cmd = [sys.executable] + args
         env = _env()
@@ -64,6 +66,31 @@ def test_two_ranks_match_one_rank(gpu_available, tmp_path, source):
     assert f1 == f2
     for f in f1:
         assert filecmp.cmp(one / f, two / f, shallow=False), f"{f} differs between 1 and 2 ranks"
+
+
+@pytest.mark.parametrize("source", [False, True])
+def test_independent_chains_gathered_to_rank0(gpu_available, tmp_path, source):
+    """--chains 4 (independent main-run chains, MC3 off): every chain's samples gathered to rank 0
+    at the end of the run (parallel.gather_rows) and written as results files of their own.  As 2
+    ranks (two chains each) the files equal the 1-rank run's byte for byte, and chain 0's files
+    equal a 1-chain run's (Philox streams keyed by the global chain id)."""
+    one, two, single = tmp_path / "r1", tmp_path / "r2", tmp_path / "s"
+    f1 = _run(one, 1, source, chains=4)
+    f2 = _run(two, 2, source, chains=4)
+    assert f1 == f2
+    for c in (1, 2, 3):
+        assert any(f.endswith(f"_chain{c}.txt") and "stats_" in f for f in f1), f1
+        assert any(f.endswith(f"_chain{c}.txt") and "areas_" in f for f in f1), f1
+    for f in f1:
+        assert filecmp.cmp(one / f, two / f, shallow=False), f"{f} differs between 1 and 2 ranks"
+    fs = _run(single, 1, source)
+    assert fs and all(f in f1 for f in fs)
+    for f in fs:
+        assert filecmp.cmp(one / f, single / f, shallow=False), f"{f}: chain 0 differs from a 1-chain run"
+    # the chains are independent: their samples differ
+    a = (one / [f for f in f1 if f.endswith("_chain1.txt") and "stats_" in f][0]).read_text()
+    b = (one / [f for f in f1 if f.endswith("_chain2.txt") and "stats_" in f][0]).read_text()
+    assert a != b
 
 
 def _rccl_worker():

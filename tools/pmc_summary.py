@@ -72,6 +72,13 @@ for k, s in summary.items():
     print(k, json.dumps(e))
 # the profiled bench run's workload (its JSON line in the pass logs), so bench.py can match it
 meta = {"command": "bash tools/pmc.sh (rocprofv3 --pmc <pass> --kernel-trace -- python3 bench.py ...)"}
+# the kernel sources the counters were measured on (bench.py uses the counters only for the same sources)
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+try:
+    import bench
+    meta["source_hash"] = bench.kernel_source_hash()
+except Exception as e:  # pragma: no cover
+    meta["source_hash_error"] = repr(e)
 for log in sorted(glob.glob(os.path.join(out, "p*.log"))):
     for line in open(log):
         if line.startswith("{"):

@@ -1,6 +1,6 @@
 """Stage cycles of the source sampler's table passes (an SBZ_TB_STAMP=1 build of libsbz, selected with
-SBZ_LIB_PATH): zone moves only at the cfg5 shape, the per-stage shader cycles per pass phase (wave 0
-and the last wave), from the first 16 ll-trace entries the stamp build writes.  Diagnostic only.
+SBZ_LIB_PATH): zone moves only at the cfg5 shape, the per-stage shader cycles per feature of a wave
+(wave 0 and the last wave), from the first 16 ll-trace entries the stamp build writes.  Diagnostic only.
 """
 import json
 import os
@@ -11,7 +11,7 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 import bench  # noqa: E402
 
-STAGES = ["C cells", "D counts out", "B table", "W+A weights/column", "memory ops", "barrier"]
+STAGES = ["column + weights", "table", "cells", "counts out"]
 
 
 def main():
@@ -31,11 +31,11 @@ def main():
     r = bench.source_sampler_leg(shape, 256, steps, 0, seed=3)
     ll = cap["ll"]
     passes = steps + 1  # one count pass per launch + one resample pass per zone move (most steps)
-    phases = passes * (shape["features"] + 4)
-    w0 = ll[:, :8].mean(0) / phases
-    w7 = ll[:, 8:16].mean(0) / phases
-    out = {"us_per_step": r["us_per_step"], "cycles_per_phase_wave0": dict(zip(STAGES, w0.round(1).tolist())),
-           "cycles_per_phase_lastwave": dict(zip(STAGES, w7.round(1).tolist())),
+    feats = passes * (shape["features"] / 8)  # features per wave and pass (8 waves)
+    w0 = ll[:, :4].mean(0) / feats
+    w7 = ll[:, 8:12].mean(0) / feats
+    out = {"us_per_step": r["us_per_step"], "cycles_per_feature_wave0": dict(zip(STAGES, w0.round(1).tolist())),
+           "cycles_per_feature_lastwave": dict(zip(STAGES, w7.round(1).tolist())),
            "total_wave0": float(w0.sum()), "total_lastwave": float(w7.sum())}
     print(json.dumps(out))
 
