@@ -98,6 +98,7 @@ SIGNATURES = {
     "sbz_source_layout_device": (_I, [_P, _I, _P, _P, ctypes.c_int32]),
     "sbz_check_indices_device_pm": (_I, [_P, _I, _P, _P]),
     "sbz_loglik_batch": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "sbz_loglik_batch_pm": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P]),
     "sbz_loglik_batch_device": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P]),
     "sbz_check_indices_device": (_I, [_P, _I, _P, _P]),
     "sbz_device_alloc": (_I, [_P, ctypes.c_uint64, ctypes.POINTER(_P)]),

@@ -373,9 +373,10 @@ int sbz_check_indices_device_pm(sbz_ctx *ctx, int B, const uint8_t *zone_of_site
     return check_indices(ctx, B, zone_of_site, source_pm, true);
 }
 
-int sbz_loglik_batch(sbz_ctx *ctx, int B, const uint8_t *zone_of_site, const double *w,
-                     const double *p_global, const double *p_zones, const double *p_fam,
-                     const uint8_t *source, double *out_ll) {
+namespace {
+int loglik_host(sbz_ctx *ctx, int B, const uint8_t *zone_of_site, const double *w, const double *p_global,
+                const double *p_zones, const double *p_fam, const uint8_t *source, bool source_pm,
+                double *out_ll) {
     if (!ctx) return SBZ_EINVAL;
     if (B < 0 || !zone_of_site || !w || !p_global || !out_ll ||
         (ctx->d.n_zones > 0 && !p_zones))
@@ -391,12 +392,17 @@ int sbz_loglik_batch(sbz_ctx *ctx, int B, const uint8_t *zone_of_site, const dou
     for (size_t i = 0; i < (size_t)B * N; i++)
         if (zone_of_site[i] != SBZ_NONE && zone_of_site[i] >= Z)
             return fail(ctx, SBZ_EINVAL, "zone_of_site holds an index >= n_zones");
-    if (source)
+    const size_t Np = ctx->Np;
+    if (source && !source_pm)
         for (size_t i = 0; i < (size_t)B * N * F; i++)
             if (source[i] >= C) return fail(ctx, SBZ_EINVAL, "source holds a component index >= C");
+    if (source && source_pm)  // rows of Np bytes; columns >= N are padding, not checked
+        for (size_t r = 0; r < (size_t)B * F; r++)
+            for (size_t p = 0; p < N; p++)
+                if (source[r * Np + p] >= C) return fail(ctx, SBZ_EINVAL, "source holds a component index >= C");
 
     const size_t bz = B * N, bw = B * F * C * 8, bg = B * F * S * 8, bpz = B * Z * F * S * 8,
-                 bpf = inh ? B * Fam * F * S * 8 : 0, bs = source ? B * N * F : 0;
+                 bpf = inh ? B * Fam * F * S * 8 : 0, bs = source ? B * F * (source_pm ? Np : N) : 0;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t o_w = 0, o_g = o_w + al(bw), o_z = o_g + al(bg), o_f = o_z + al(bpz),
                  o_zone = o_f + al(bpf), o_src = o_zone + al(bz), total = o_src + al(bs);
@@ -417,13 +423,27 @@ int sbz_loglik_batch(sbz_ctx *ctx, int B, const uint8_t *zone_of_site, const dou
                        reinterpret_cast<double *>(base + o_w), reinterpret_cast<double *>(base + o_g),
                        reinterpret_cast<double *>(base + o_z),
                        inh ? reinterpret_cast<double *>(base + o_f) : nullptr,
-                       source ? reinterpret_cast<uint8_t *>(base + o_src) : nullptr, false,
+                       source ? reinterpret_cast<uint8_t *>(base + o_src) : nullptr, source_pm,
                        static_cast<double *>(ctx->out.ptr));
     if (rc) return rc;
     e = hipMemcpyAsync(out_ll, ctx->out.ptr, (size_t)B * 8, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) return hip_fail(ctx, e, "likelihood D2H");
     return SBZ_OK;
+}
+}  // namespace
+
+int sbz_loglik_batch(sbz_ctx *ctx, int B, const uint8_t *zone_of_site, const double *w,
+                     const double *p_global, const double *p_zones, const double *p_fam,
+                     const uint8_t *source, double *out_ll) {
+    return loglik_host(ctx, B, zone_of_site, w, p_global, p_zones, p_fam, source, false, out_ll);
+}
+
+int sbz_loglik_batch_pm(sbz_ctx *ctx, int B, const uint8_t *zone_of_site, const double *w,
+                        const double *p_global, const double *p_zones, const double *p_fam,
+                        const uint8_t *source_pm, double *out_ll) {
+    if (ctx && !source_pm) return fail(ctx, SBZ_EINVAL, "source_pm is required");
+    return loglik_host(ctx, B, zone_of_site, w, p_global, p_zones, p_fam, source_pm, true, out_ll);
 }
 
 int sbz_set_network(sbz_ctx *ctx, const uint8_t *applicable, int32_t nnz, const int32_t *adj_indptr,

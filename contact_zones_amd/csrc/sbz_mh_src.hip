@@ -1314,7 +1314,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         bool gtent = false;
         int gz = 0, gn = 0, gsize = 0, gdocc = 0;
         // TB zone move: the proposal's q, q_back and the moved sites' mixture delta
-        bool tb_zone = false;
+        bool tb_zone = false, tb_defer = false;
         double tb_q = 0.0, tb_qb = 0.0, tb_ds = 0.0;
 
         if (zone_op) {
@@ -1396,7 +1396,11 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                     dprior = uni(dprior + (geo_new - geo_cur));
                 }
                 if constexpr (TB) {
-                    ll_new = tresample(ct_alt);
+                    // tape: the reference's order (every source redrawn, then the acceptance
+                    // uniform); Philox: the ratio does not depend on the new sources, so they are
+                    // drawn only once the move is accepted
+                    if (rng.tape) ll_new = tresample(ct_alt);
+                    else tb_defer = true;
                     double ds = site_mix_delta(sa, zna, zoa);
                     if (sb >= 0) ds = ds + site_mix_delta(sb, NONE, zna);
                     tb_zone = true;
@@ -1757,10 +1761,14 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             // source landed on a zero-posterior component (ll_new = -inf beside a finite mixture
             // delta; an all-zero moved cell is a 0/0 posterior, NaN in the reference: rejected
             // after the uniform); otherwise the ratio with the sources' terms cancelled
+            // (a Philox draw picks only components with a positive term, so there a new source
+            // never lands on a zero-posterior one)
             if (tb_qb == 0.0 || !(ll > -INFINITY)) accept = false;
-            else if (a.warmup || tb_q == 0.0 || (ll_new == -INFINITY && tb_ds > -INFINITY && tb_ds < INFINITY))
+            else if (a.warmup || tb_q == 0.0 ||
+                     (!tb_defer && ll_new == -INFINITY && tb_ds > -INFINITY && tb_ds < INFINITY))
                 accept = true;
             else accept = flog(rng.real()) < (log(tb_qb) - log(tb_q)) + tb_ds + dprior;
+            if (accept && tb_defer) ll_new = tresample(ct_alt);
         } else if (log_q_back == -INFINITY) accept = false;
         else if (log_q == -INFINITY) accept = true;
         else accept = flog(rng.real()) < ((ll_new - ll) * 1.0) - (log_q - log_q_back) + dprior;

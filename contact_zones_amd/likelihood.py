@@ -127,8 +127,10 @@ class LikelihoodEngine:
                 raise ValueError(f"{name}: expected shape {shape}, got "
                                  f"{None if arr is None else tuple(arr.shape)}")
 
-    def loglik(self, zone_of_site, w, p_global, p_zones, p_fam=None, source=None):
-        """Full log-likelihood of B chains from host arrays; returns float64 (B,)."""
+    def loglik(self, zone_of_site, w, p_global, p_zones, p_fam=None, source=None, source_pm=False):
+        """Full log-likelihood of B chains from host arrays; returns float64 (B,).  source_pm: the
+        sources are [B][F][Np] by position (sbz_loglik_batch_pm: no device transpose), else
+        [B][N][F] by site."""
         zone_of_site = np.ascontiguousarray(zone_of_site, dtype=np.uint8)
         B = zone_of_site.shape[0]
         w = np.ascontiguousarray(w, dtype=np.float64)
@@ -140,9 +142,16 @@ class LikelihoodEngine:
             p_fam = None
         if source is not None:
             source = np.ascontiguousarray(source, dtype=np.uint8)
-        self._check_shapes(B, zone_of_site, w, p_global, p_zones, p_fam, source)
+        if source is not None and source_pm:
+            if source.shape != (B, self.n_features, self.n_positions):
+                raise ValueError(f"source (by position): expected {(B, self.n_features, self.n_positions)}, "
+                                 f"got {source.shape}")
+            self._check_shapes(B, zone_of_site, w, p_global, p_zones, p_fam, None)
+        else:
+            self._check_shapes(B, zone_of_site, w, p_global, p_zones, p_fam, source)
         out = np.empty(B, dtype=np.float64)
-        check(self._lib.sbz_loglik_batch(self.ctx, B, _ptr(zone_of_site), _ptr(w), _ptr(p_global),
+        fn = self._lib.sbz_loglik_batch_pm if (source is not None and source_pm) else self._lib.sbz_loglik_batch
+        check(fn(self.ctx, B, _ptr(zone_of_site), _ptr(w), _ptr(p_global),
                                          _ptr(p_zones), _ptr(p_fam), _ptr(source), _ptr(out)),
               self.ctx)
         return out

@@ -146,6 +146,13 @@ int sbz_loglik_batch(sbz_ctx *ctx, int B, const uint8_t *zone_of_site, const dou
                      const double *p_global, const double *p_zones, const double *p_fam,
                      const uint8_t *source, double *out_ll);
 
+/* Same, with the (host) sources by position (source_pm [B][F][Np], see Layouts; padding columns
+ * are not read): the copy is the likelihood's input as is, with no by-site -> by-position
+ * transpose on the device.  Replaces the same model.py:177-184 call as sbz_loglik_batch. */
+int sbz_loglik_batch_pm(sbz_ctx *ctx, int B, const uint8_t *zone_of_site, const double *w,
+                        const double *p_global, const double *p_zones, const double *p_fam,
+                        const uint8_t *source_pm, double *out_ll);
+
 /* Same, all pointers on the device (out_ll: double[B] device); asynchronous on ctx's stream.
  * The device entry points (this one and sbz_mh_run_device) TRUST their index bytes: they do
  * not re-check zone_of_site < n_zones (or SBZ_NONE) and source < C, which sbz_loglik_batch

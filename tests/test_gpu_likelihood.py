@@ -26,8 +26,13 @@ def _engine(d, device=0, options=None):
 
 
 def _loglik(eng, kernel, zos, w, pg, pz, pf, src):
-    """Host entry (sbz_loglik_batch, sources by site), or for kernel 'pm' the device entry with the
-    sources by position (sbz_loglik_batch_device_pm: the layout the sampler keeps, read in place)."""
+    """Host entry (sbz_loglik_batch, sources by site), for kernel 'hpm' the host entry with the
+    sources by position (sbz_loglik_batch_pm: no transpose), or for kernel 'pm' the device entry with
+    the sources by position (sbz_loglik_batch_device_pm: the layout the sampler keeps, read in place)."""
+    if kernel == "hpm" and src is not None:
+        out = eng.loglik(zos, w, pg, pz, pf, eng.sources_to_positions(src), source_pm=True)
+        assert eng.last_kernels() in ("lik_source_rc_kernel", "lik_source_generic_kernel")
+        return out
     if kernel != "pm" or src is None:
         return eng.loglik(zos, w, pg, pz, pf, src)
     import torch
@@ -60,7 +65,7 @@ def _assert_close(got, ref, tol=REL_TOL):
 # to positions first) and by position (read in place, 'pm'), and on the generic per-cell kernel
 # (option src_table = 0, the path of shapes the table kernel does not take).
 MODES = [("mixture", "dense"), ("mixture", "packed"), ("source", "rc"), ("source", "pm"),
-         ("source", "generic")]
+         ("source", "hpm"), ("source", "generic")]
 
 
 def _options(kernel):

@@ -307,3 +307,74 @@ def test_concurrent_contexts_match_sequential(gpu_available):
     for a, b in zip(seq, con):
         for k in a:
             np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+
+
+def test_source_sampler_cfg5_philox_invariants(gpu_available):
+    """The bench shape (cfg5: 2000 sites x 500 features x 10 states, 8 zones, 4 families, 256
+    chains) on the default path — sources in HBM, per-feature table passes, per-chain count tables
+    (eng.last_kernels() names it) — under the default SAMPLE_SOURCE = true operator mix with Philox
+    draws: every source a component its site allows, zone sizes within [MIN_M, MAX_M], parameters
+    normalised, the tracked ll equal to a fresh evaluation within 1e-9, and the run reproducible
+    bit for bit from its seed."""
+    import torch
+    from scipy.spatial import Delaunay
+
+    from contact_zones_amd.likelihood import LikelihoodEngine
+    from contact_zones_amd.sampler import ChainState, Sampler, precisions
+    rng = np.random.default_rng(55)
+    N, F, S, Z, Fam, B = 2000, 500, 10, 8, 4, 256
+    min_m, max_m = 3, 50
+    obs = rng.integers(0, S, size=(N, F)).astype(np.int8)
+    obs[rng.random((N, F)) < 0.02] = -1
+    fam = rng.integers(0, Fam, size=N).astype(np.uint8)
+    fam[rng.random(N) < 0.2] = 255
+    states = np.ones((F, S), bool)
+    indptr, indices = Delaunay(rng.random((N, 2))).vertex_neighbor_vertices
+    eng = LikelihoodEngine(obs, fam, S, Z, Fam, True)
+    ops = {"shrink_zone": 0.016, "grow_zone": 0.016, "swap_zone": 0.008, "gibbs_sample_weights": 0.4,
+           "gibbs_sample_p_global": 0.05, "gibbs_sample_p_zones": 0.4, "gibbs_sample_p_families": 0.11}
+    prec = precisions({"weights": 15, "universal": 40, "contact": 20, "inheritance": 20})
+
+    def make():
+        zos = np.full((B, N), 255, np.uint8)
+        r = np.random.default_rng(56)
+        for b in range(B):  # 8 disjoint zones of 5 random sites each
+            p = r.permutation(N)[:5 * Z]
+            for z in range(Z):
+                zos[b, p[5 * z:5 * z + 5]] = z
+        w = np.broadcast_to(r.dirichlet(np.ones(3), size=F), (B, F, 3)).copy()
+        pg = np.broadcast_to(r.dirichlet(np.ones(S), size=F), (B, F, S)).copy()
+        pz = r.dirichlet(np.ones(S), size=(B, Z, F))
+        pf = np.broadcast_to(r.dirichlet(np.ones(S), size=(Fam, F)), (B, Fam, F, S)).copy()
+        st = ChainState(eng, zos, w, pg, pz, pf, source=np.zeros((B, N, F), np.uint8))
+        Sampler(eng, states, indptr, indices, {"gibbs_sample_sources": 1.0}, prec, min_m,
+                sample_source=True).run(st, 1, np.full(B, max_m), np.full(B, 0.85), seed=11)
+        smp = Sampler(eng, states, indptr, indices, ops, prec, min_m, sample_source=True)
+        out = smp.run(st, 600, np.full(B, max_m), np.full(B, 0.85), seed=12, trace=True)
+        torch.cuda.synchronize()
+        return st, out
+
+    st, out = make()
+    assert "tables" in eng.last_kernels()
+    assert out["status"].cpu().numpy().tolist() == [0] * B
+    s = st.to_numpy()
+    src = s["source"]
+    assert src.max() <= 2
+    zs = s["zone_of_site"]
+    assert not np.any((src == 1) & (zs == 255)[:, :, None])
+    assert not np.any((src == 2) & (fam == 255)[None, :, None])
+    sizes = np.stack([(zs == z).sum(1) for z in range(Z)], 1)
+    assert sizes.min() >= min_m and sizes.max() <= max_m
+    for name in ("w", "p_global", "p_zones", "p_fam"):
+        np.testing.assert_allclose(s[name].sum(-1), 1.0, rtol=1e-12)
+    fresh = st.refresh_ll().cpu().numpy()
+    assert np.all(np.isfinite(fresh))
+    assert np.max(np.abs(s["ll"] - fresh) / np.abs(fresh)) <= REL_TOL
+    acc = out["accept"].cpu().numpy()
+    op = out["op"].cpu().numpy()
+    assert acc.mean() > 0.05 and len(np.unique(op)) >= 6
+    ll_trace = out["ll"].cpu().numpy()
+    st2, out2 = make()
+    np.testing.assert_array_equal(out2["ll"].cpu().numpy(), ll_trace)
+    np.testing.assert_array_equal(st2.source.cpu().numpy(), src)
+    np.testing.assert_array_equal(st2.zone_of_site.cpu().numpy(), zs)
