@@ -407,6 +407,12 @@ struct LaneRng {
     }
 };
 
+// Gamma draws of the source sampler's Gibbs redraws (Philox mode, sbz_mh_src.hip gamma_fill):
+// integer alpha = n <= GB_NMAX as -log(u_1 ... u_n), exactly Gamma(n, 1) (a sum of n exponentials,
+// no rejection), with 32-bit uniforms (w + 1/2) 2^-32; others by Marsaglia-Tsang.
+constexpr int GB_NMAX = 16;
+__device__ __forceinline__ double u32o(uint32_t w) { return ((double)w + 0.5) * 0x1p-32; }
+
 __device__ __forceinline__ void Rng::dirichlet2(double a0, double a1, double &x0, double &x1) {
     if (tape) {
         x0 = tape_item();

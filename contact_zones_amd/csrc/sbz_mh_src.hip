@@ -193,6 +193,13 @@ size_t mh_src_const_bytes(const sbz_dims &d, int C, bool alg, bool alf, bool gcg
 #ifndef SBZ_SRC_UNR
 #define SBZ_SRC_UNR 1
 #endif
+// Philox Gibbs draws per thread at once (gamma_batch): p_* redraws, weights
+#ifndef SBZ_RB_REDRAW
+#define SBZ_RB_REDRAW 4
+#endif
+#ifndef SBZ_RB_WEIGHTS
+#define SBZ_RB_WEIGHTS 2
+#endif
 
 namespace {
 
@@ -275,6 +282,131 @@ struct TbLogAcc {
     int e = 0;
     __device__ __forceinline__ double value() const { return flog(m) + (double)e * LN2; }
 };
+
+// The Philox Gibbs gammas of a redraw, a function of its own so that its loops get their own
+// registers (inlined, the sampler kernel's live state spilled around them).  buf[t] holds item t's
+// alpha (< 0: no draw, 0 returned) on entry and its gamma on exit, t < n; thread tid takes the
+// items t = tid + i NT.  Item t is the Philox stream (key; block j0 + b, counter word, chain, c3):
+// mode 0 (p_* redraws): item (f, j) = (t / S, t % S), counter ctr0 + frank[f], c3 tag lane j, j0 0;
+// mode 1 (weights): counter ctr0, tag 0xFFF, j0 = t << 8.
+// - integer alpha = m <= GB_NMAX: -log(u_1 ... u_m), the u's four per block from block j0 (K items
+//   at a time);
+// - otherwise Marsaglia-Tsang (boosted by u^(1/alpha) below 1, block j0 + 255), round r of an item
+//   on block j0 + 16 + r (a 53-bit and a 32-bit uniform for the Box-Muller normal, a 32-bit
+//   acceptance uniform), at most 64 rounds (then d, as LaneRng::gamma).  Each thread keeps K items
+//   in flight (their dependent f64 chains overlap) and refills a slot from its own queue as soon
+//   as the slot's item accepts, so a wave runs about (its items / K) x 1.03 rounds plus the tail
+//   of its slowest lane, not the slowest lane's rounds for every batch.
+// A draw depends only on its item's stream: not on K, NT or the order the slots take the items.
+template <int K, int NT>
+__device__ __noinline__ void gamma_fill(lds_ptr<double> bufp, int n, int S, lds_ptr<const int> frankp, uint32_t key0,
+                                        uint32_t key1, uint32_t chain, uint64_t ctr0, int mode) {
+    double *buf = (double *)bufp;
+    const int *frank = (const int *)frankp;
+    const int tid = (int)threadIdx.x;
+    auto stream = [&](int t, uint32_t &j0, uint32_t &bs, uint32_t &c3) {
+        if (mode == 0) {
+            const int f = t / S, j = t - f * S;
+            const uint64_t cr = ctr0 + (uint64_t)frank[f];
+            j0 = 0;
+            bs = (uint32_t)cr;
+            c3 = (uint32_t)(cr >> 32) ^ ((uint32_t)(j + 1) << 24);
+        } else {
+            j0 = (uint32_t)t << 8;
+            bs = (uint32_t)ctr0;
+            c3 = (uint32_t)(ctr0 >> 32) ^ (0xFFFu << 20);
+        }
+    };
+    for (int c0 = 0; c0 < n; c0 += 64 * NT) {  // chunks of at most 64 items per thread
+        const int cn = min(n - c0, 64 * NT);
+        uint64_t mt = 0;  // the thread's Marsaglia-Tsang items of the chunk: bit i <-> c0 + tid + i NT
+        // 1. the product form, K items at a time
+        for (int i0 = 0; i0 * NT < cn; i0 += K) {
+            double prod[K];
+            int m[K], nb[K];
+            uint32_t j0[K], bs[K], c3[K];
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                const int i = i0 + k, t = c0 + tid + i * NT;
+                const bool valid = i * NT + tid < cn;
+                const double al = valid ? buf[t] : -1.0;
+                const bool pm = al >= 1.0 && al <= (double)GB_NMAX && al == floor(al);
+                if (valid && al >= 0.0 && !pm) mt |= 1ull << i;
+                if (valid && al < 0.0) buf[t] = 0.0;
+                m[k] = pm ? (int)al : 0;
+                nb[k] = (m[k] + 3) >> 2;
+                prod[k] = 1.0;
+                stream(valid ? t : c0, j0[k], bs[k], c3[k]);
+            }
+            for (int b = 0; b < GB_NMAX / 4; b++) {
+                bool more = false;
+#pragma unroll
+                for (int k = 0; k < K; k++) more = more || b < nb[k];
+                if (!__any(more)) break;
+#pragma unroll
+                for (int k = 0; k < K; k++) {
+                    if (!__any(b < nb[k])) continue;
+                    uint32_t p[4] = {j0[k] + (uint32_t)b, bs[k], chain, c3[k]};
+                    philox4x32_10(p, key0, key1);
+#pragma unroll
+                    for (int q = 0; q < 4; q++) prod[k] *= 4 * b + q < m[k] ? u32o(p[q]) : 1.0;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < K; k++)
+                if (m[k]) buf[c0 + tid + (i0 + k) * NT] = -flog(prod[k]);
+        }
+        // 2. Marsaglia-Tsang, K slots refilled from the thread's queue `mt`
+        int ts[K], rd[K];
+        double dk[K], ck[K], bo[K];
+        uint32_t j0[K], bs[K], c3[K];
+        auto take = [&](int k) {
+            ts[k] = -1;
+            if (mt == 0) return;
+            const int i = __builtin_ctzll(mt);
+            mt &= mt - 1;
+            const int t = c0 + tid + i * NT;
+            const double al = buf[t];
+            const double a = al < 1.0 ? al + 1.0 : al;
+            ts[k] = t;
+            rd[k] = 0;
+            dk[k] = a - 1.0 / 3.0;
+            ck[k] = 1.0 / sqrt(9.0 * dk[k]);
+            stream(t, j0[k], bs[k], c3[k]);
+            bo[k] = 1.0;
+            if (al < 1.0) {
+                uint32_t p[4] = {j0[k] + 255u, bs[k], chain, c3[k]};
+                philox4x32_10(p, key0, key1);
+                bo[k] = pow(u53(p[0], p[1]), 1.0 / al);
+            }
+        };
+#pragma unroll
+        for (int k = 0; k < K; k++) take(k);
+        for (;;) {
+            bool live = false;
+#pragma unroll
+            for (int k = 0; k < K; k++) live = live || ts[k] >= 0;
+            if (!__any(live)) break;
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                if (!__any(ts[k] >= 0)) continue;
+                uint32_t p[4] = {j0[k] + 16u + (uint32_t)rd[k], bs[k], chain, c3[k]};
+                philox4x32_10(p, key0, key1);
+                const double u1 = u53(p[0], p[1]), u2 = u32o(p[2]), w = u32o(p[3]);
+                const double x = sqrt(-2.0 * flog(1.0 - u1)) * cospi(2.0 * u2);
+                const double v = 1.0 + ck[k] * x;
+                const double v3 = v * v * v, x2 = x * x;
+                const bool ok = v > 0.0 && (w < 1.0 - 0.0331 * x2 * x2 ||
+                                            flog(w) < 0.5 * x2 + dk[k] * (1.0 - v3 + flog(v3 > 0.0 ? v3 : 1.0)));
+                rd[k]++;
+                if (ts[k] >= 0 && (ok || rd[k] >= 64)) {
+                    buf[ts[k]] = dk[k] * (ok ? v3 : 1.0) * bo[k];
+                    take(k);
+                }
+            }
+        }
+    }
+}
 
 // MODE 0 / 2 resample: every source is redrawn from the current sample's posterior into `dst`
 // (gibbs_sample_sources), with Philox uniforms (0) or the tape's (2); MODE 1 reads the sources
@@ -1044,7 +1176,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     int *ct_cur = TB ? a.ctab + (size_t)b * F * td.CTP : nullptr;
     int *ct_alt = TB ? a.ctab + a.ct_half + (size_t)b * F * td.CTP : nullptr;
     // One pass over every observation (tb_pass), the generator advanced as the pass drew
-    uint64_t tbst[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t tbst[16] = {};
     auto tpass = [&](auto mode_c, const uint8_t *sv, uint8_t *dst, int *ct) -> double {
         constexpr int MODE = decltype(mode_c)::value;
         TbPassArgs pa;
@@ -1077,6 +1209,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         pa.chain = rng.chain;
         pa.ctr = rng.ctr;
         pa.stamps = SBZ_TB_STAMP ? tbst : nullptr;
+        if (SBZ_TB_STAMP) tbst[4]++;  // passes
         const TbPassOut o = tb_pass<C, NW, MODE>(pa);
         if (o.err && !err) {
             err = o.err;
@@ -1162,28 +1295,38 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             }
         }
         sync();
+        uint64_t rst = SBZ_TB_STAMP ? __builtin_amdgcn_s_memtime() : 0;
+        auto rstamp = [&](int k) {  // SBZ_TB_STAMP: scan / alphas / gammas / rows
+            if (SBZ_TB_STAMP) {
+                const uint64_t t = __builtin_amdgcn_s_memtime();
+                tbst[k] += t - rst;
+                rst = t;
+            }
+        };
+        rstamp(8);
         const int tot_n = uni(misc_i[0]), tot_r = uni(misc_i[1]);
         const int64_t pos0 = pos;
         const uint64_t ctr0 = ctr;
         const bool have = !tape || pos0 + tot_n <= len;
-        for (int t = tid; t < FS; t += NT) {
-            const int f = t / S, j = t - f * S;
-            const bool act = sub[f] && j < app_cnt(f);
-            double g = 0.0;
-            if (act) {
-                if (tape) {
-                    g = have ? tape[pos0 + fpre[f] + j] : 0.0;
-                } else {
-                    const int x = app_list(f, j);
-                    LaneRng lr;
-                    lr.initk(key0, key1, chain, ctr0 + (uint64_t)frank[f], j);
-                    const double alpha = gcv(comp, row, f * S + x) + (double)cnt[f * S + x];
-                    g = lr.gamma(alpha);
-                }
+        if (tape) {
+            for (int t = tid; t < FS; t += NT) {
+                const int f = t / S, j = t - f * S;
+                const bool act = sub[f] && j < app_cnt(f);
+                gbuf[t] = act && have ? tape[pos0 + fpre[f] + j] : 0.0;
             }
-            gbuf[t] = g;
+        } else {
+            // Philox: item (f, j)'s alpha, then the gammas (gamma_fill, the same thread's items)
+            for (int t = tid; t < FS; t += NT) {
+                const int f = t / S, j = t - f * S;
+                const bool act = sub[f] && j < app_cnt(f);
+                gbuf[t] = act ? gcv(comp, row, f * S + app_list(f, j)) + (double)cnt[f * S + app_list(f, j)] : -1.0;
+            }
+            rstamp(9);
+            gamma_fill<SBZ_RB_REDRAW, NT>((lds_ptr<double>)gbuf, FS, S, (lds_ptr<const int>)frank, key0, key1,
+                                          (uint32_t)chain, ctr0, 0);
         }
         sync();
+        rstamp(10);
         double dp = 0.0, dl = 0.0;
         int zfl = 0;
         const bool al = has_al(comp);
@@ -1219,6 +1362,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             dll = bsum(dl);
             dzf = bor(zfl);
         }
+        rstamp(11);
         bad = have ? 0 : 1;
         pos = uni64(pos0 + (tape ? tot_n : 0));
         ctr = (uint64_t)uni64((int64_t)(ctr0 + (tape ? 0 : (uint64_t)tot_r)));
@@ -1606,12 +1750,15 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             if (!rng.tape) {
                 // Philox: the 2F gammas in parallel, thread t -> feature t / 2, gamma t % 2 (C == 2:
                 // g0 / g1 of Dirichlet(1 + counts); C == 3: ga / gb of the Beta ratio), into gbuf
+                // (gamma_fill: item t's alpha, then the gammas; stream of counter ctr, tag 0xFFF)
                 for (int t = tid; t < 2 * F; t += NT) {
                     const int f = t >> 1, k = t & 1;
                     const int cc = C == 2 ? cnt[f * C + k]
                                           : (k == 0 ? cnt[f * C + (fixed == 0 ? 1 : 2)] : cnt[f * C]);
-                    gbuf[t] = lr.gamma(1.0 + cc);
+                    gbuf[t] = 1.0 + cc;
                 }
+                gamma_fill<SBZ_RB_WEIGHTS, NT>((lds_ptr<double>)gbuf, 2 * F, 1, (lds_ptr<const int>)nullptr,
+                                               rng.key0, rng.key1, (uint32_t)rng.chain, rng.ctr, 1);
                 sync();
             }
             double wdl = 0.0;  // TB: the log-likelihood change from the class counters
@@ -1695,6 +1842,15 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             }
         } else {
             // ---- gibbs_sample_p_global / p_zones / p_families
+            // (SBZ_TB_STAMP builds: cycles of the subset + counts, redraw_rows and the ll update)
+            uint64_t gst = SBZ_TB_STAMP ? __builtin_amdgcn_s_memtime() : 0;
+            auto gstamp = [&](int k) {
+                if (SBZ_TB_STAMP) {
+                    const uint64_t t = __builtin_amdgcn_s_memtime();
+                    tbst[k] += t - gst;
+                    gst = t;
+                }
+            };
             int row = 0;
             if (op == G_P_ZONES) row = rng.below(Z);        // np.random.randint(0, n_zones)
             if (op == G_P_FAMILIES) row = rng.below(Fam);   // np.random.randint(0, n_families)
@@ -1735,8 +1891,10 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             double *lbase = comp == 0 ? lpg : (comp == 1 ? lpz + (size_t)row * F * S : lpf + (size_t)row * F * S);
             double dll = 0.0;
             int dzf = 0;
+            gstamp(5);
             dprior = redraw_rows(base, lbase, comp, row, rng.tape, rng.len, rng.key0, rng.key1, rng.chain,
                                  rpos, rctr, rbad, TB, dll, dzf);
+            gstamp(6);
             rng.pos = rpos;
             rng.ctr = rctr;
             if (rbad) rng.bad = 1;
@@ -1748,6 +1906,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                 ll_new = (dzf || !(ll > -INFINITY && ll < INFINITY))
                              ? tpass(std::integral_constant<int, 1>(), src, nullptr, ct_alt)
                              : uni(ll + dll);
+                gstamp(7);
             } else {
                 ll_new = pass_ll(src);
             }
@@ -1862,8 +2021,8 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             for (int c = tid; c < NF; c += NT) gsrc[c] = src[c];
         }
     }
-    if (SBZ_TB_STAMP && ch.trace_ll && a.n_steps >= 16 && (tid == 0 || tid == NT - 64)) {
-        for (int k = 0; k < 8; k++) ch.trace_ll[(size_t)b * a.n_steps + (tid ? 8 : 0) + k] = (double)tbst[k];
+    if (SBZ_TB_STAMP && ch.trace_ll && a.n_steps >= 32 && (tid == 0 || tid == NT - 64)) {
+        for (int k = 0; k < 16; k++) ch.trace_ll[(size_t)b * a.n_steps + (tid ? 16 : 0) + k] = (double)tbst[k];
     }
     if (tid == 0) {
         ch.ll[b] = ll;

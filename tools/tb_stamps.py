@@ -16,9 +16,12 @@ STAGES = ["column + weights", "table", "cells", "counts out"]
 
 def main():
     shape = {"sites": 2000, "features": 500, "states": 10, "zones": 8, "families": 4}
-    ops = {"shrink_zone": 0.4, "grow_zone": 0.4, "swap_zone": 0.2}
-    bench.src_operators = lambda inh=True: dict(ops)
+    sets = {"zone_moves": {"shrink_zone": 0.4, "grow_zone": 0.4, "swap_zone": 0.2},
+            "p_zones": {"gibbs_sample_p_zones": 1.0}, "p_global": {"gibbs_sample_p_global": 1.0},
+            "weights": {"gibbs_sample_weights": 1.0}, "sources": {"gibbs_sample_sources": 1.0}}
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 40
+    ops = sets[sys.argv[2] if len(sys.argv) > 2 else "zone_moves"]
+    bench.src_operators = lambda inh=True: dict(ops)
     cap = {}
     orig = bench.logged_ess if hasattr(bench, "logged_ess") else None
     import contact_zones_amd.diagnostics as dg
@@ -26,17 +29,23 @@ def main():
 
     def grab(ll):
         cap["ll"] = np.array(ll)
-        return real(np.nan_to_num(ll[:, 16:], nan=0.0, posinf=0.0, neginf=0.0))
+        return real(np.nan_to_num(ll[:, 32:], nan=0.0, posinf=0.0, neginf=0.0))
     dg.logged_ess = grab
-    r = bench.source_sampler_leg(shape, 256, steps, 0, seed=3)
+    r = bench.source_sampler_leg(shape, 256, steps, 0, seed=3, gpu_init=True)
     ll = cap["ll"]
-    passes = steps + 1  # one count pass per launch + one resample pass per zone move (most steps)
+    passes = ll[:, 4].mean()  # table passes run by the timed launch (slot 4 of the stamp build)
     feats = passes * (shape["features"] / 8)  # features per wave and pass (8 waves)
     w0 = ll[:, :4].mean(0) / feats
-    w7 = ll[:, 8:12].mean(0) / feats
-    out = {"us_per_step": r["us_per_step"], "cycles_per_feature_wave0": dict(zip(STAGES, w0.round(1).tolist())),
+    w7 = ll[:, 16:20].mean(0) / feats
+    gib = ll[:, 5:8].mean(0) / steps  # Gibbs p_* steps: subset + counts, redraw_rows, ll update
+    rdr = ll[:, 8:12].mean(0) / steps  # inside redraw_rows: scan, alphas, gammas, rows + delta
+    out = {"set": sys.argv[2] if len(sys.argv) > 2 else "zone_moves", "us_per_step": r["us_per_step"],
+           "passes": float(passes), "cycles_per_feature_wave0": dict(zip(STAGES, w0.round(1).tolist())),
            "cycles_per_feature_lastwave": dict(zip(STAGES, w7.round(1).tolist())),
-           "total_wave0": float(w0.sum()), "total_lastwave": float(w7.sum())}
+           "total_wave0": float(w0.sum()), "total_lastwave": float(w7.sum()),
+           "p_step_cycles_per_step": dict(zip(["subset + counts", "redraw_rows", "ll update"],
+                                              gib.round(0).tolist())),
+           "redraw_cycles_per_step": dict(zip(["scan", "alphas", "gammas", "rows + delta"], rdr.round(0).tolist()))}
     print(json.dumps(out))
 
 
