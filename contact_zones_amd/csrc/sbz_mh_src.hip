@@ -146,7 +146,7 @@ __host__ __device__ inline bool tb_fits(const TbDims &t, int Np) {
 
 // LDS bytes of the redraw scratch (redraw_rows / weight gammas: draws [F][max(S, 2)] doubles,
 // per-feature tape offsets and counter ranks [F] ints, two totals)
-static inline size_t redraw_bytes(size_t F, size_t S) { return F * (S > 2 ? S : 2) * 8 + 2 * F * 4 + 8; }
+__host__ __device__ inline size_t redraw_bytes(size_t F, size_t S) { return F * (S > 2 ? S : 2) * 8 + 2 * F * 4 + 8; }
 
 size_t mh_src_lds_bytes(const sbz_dims &d, int C, bool hbm_sources, bool geo, bool stage, bool tb, int Np, int nw) {
     const size_t N = d.n_sites, F = d.n_features, S = d.n_states, Z = d.n_zones;
@@ -798,7 +798,10 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     bool stg_ok = false;
     // a.cstage: the constant tables, after the staged parameters (16-B aligned)
     const bool cst = a.cstage != 0;
-    const size_t cst_off = (stg_off + ((size_t)F * 12 + (size_t)(1 + Z + Fam) * F * S) * 8 + (size_t)NF + N + 15) & ~(size_t)15;
+    // (TB: after the region of the redraw scratch / pass buffers, as mh_src_lds_bytes counts it)
+    const size_t cst_off =
+        TB ? (uni_off + max(tb_layout(tb_dims(S, Z, Fam, C), a.Np, NW).end, redraw_bytes(F, S)) + 15) & ~(size_t)15
+           : (stg_off + ((size_t)F * 12 + (size_t)(1 + Z + Fam) * F * S) * 8 + (size_t)NF + N + 15) & ~(size_t)15;
     const int FS = F * S;
     // (the global tables are read with ldp, as before staging: a plain LDS load and an atomic
     // global one are never merged into one load through a generic pointer)
@@ -1316,10 +1319,20 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             }
         } else {
             // Philox: item (f, j)'s alpha, then the gammas (gamma_fill, the same thread's items)
-            for (int t = tid; t < FS; t += NT) {
-                const int f = t / S, j = t - f * S;
-                const bool act = sub[f] && j < app_cnt(f);
-                gbuf[t] = act ? gcv(comp, row, f * S + app_list(f, j)) + (double)cnt[f * S + app_list(f, j)] : -1.0;
+            {
+                const int dF = NT / S, dJ = NT - dF * S;
+                int f = tid / S, j = tid - f * S;
+                for (int t = tid; t < FS; t += NT) {
+                    const bool act = sub[f] && j < app_cnt(f);
+                    const int x = app_list(f, j);
+                    gbuf[t] = act ? gcv(comp, row, f * S + x) + (double)cnt[f * S + x] : -1.0;
+                    f += dF;
+                    j += dJ;
+                    if (j >= S) {
+                        j -= S;
+                        f++;
+                    }
+                }
             }
             rstamp(9);
             gamma_fill<SBZ_RB_REDRAW, NT>((lds_ptr<double>)gbuf, FS, S, (lds_ptr<const int>)frank, key0, key1,
@@ -1330,31 +1343,67 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         double dp = 0.0, dl = 0.0;
         int zfl = 0;
         const bool al = has_al(comp);
-        for (int t = tid; t < FS; t += NT) {
-            const int f = t / S, j = t - f * S;
-            const int n = app_cnt(f);
-            if (!(sub[f] && j < n)) continue;
-            double g = gbuf[t];
-            if (!tape) {
+        // Philox: each feature's total of its draws, once (over fpre / frank, no longer needed)
+        double *ftot = reinterpret_cast<double *>(fpre);
+        if (!tape) {
+            for (int f = tid; f < F; f += NT) {
+                const int n = app_cnt(f);
                 double tot = 0.0;
                 for (int i = 0; i < n; i++) tot += gbuf[f * S + i];
-                g = g / tot;
+                ftot[f] = tot;
             }
-            const int x = app_list(f, j);
-            double *prow = base + (size_t)f * S;
-            // the current value: the staged copy once staged (an exact copy), else the global row
-            const double old = stg_ok ? lds_rd(lbase + (size_t)f * S + x) : ldp(prow + x);
-            stp(prow + x, g);
-            if (stg) lbase[(size_t)f * S + x] = g;  // the staged copy follows
-            if (al) {
-                const double am1 = alv(comp, row, f * S + x) - 1.0;
-                dp += xlogy(am1, g) - xlogy(am1, old);
+            sync();
+        }
+        // four items per thread at a time: their loads (the old values from L2) first; item
+        // t = t0 + u NT is (f, j) = (t / S, t % S), walked by (NT / S, NT % S) steps
+        const int dF = NT / S, dJ = NT - dF * S;
+        for (int t0 = tid; t0 < FS; t0 += 4 * NT) {
+            int ns[4], xs[4], fs[4], js[4];
+            double olds[4];
+            {
+                int f = t0 / S, j = t0 - f * S;
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    fs[u] = min(f, F - 1);
+                    js[u] = f < F ? j : 0;
+                    f += dF;
+                    j += dJ;
+                    if (j >= S) {
+                        j -= S;
+                        f++;
+                    }
+                }
             }
-            if (want_dl) {
-                const int c = cnt[f * S + x];
-                if (c > 0) {
-                    if (g > 0.0 && old > 0.0 && g < INFINITY && old < INFINITY) dl += (double)c * (flog(g) - flog(old));
-                    else zfl = 1;
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int f = fs[u], j = js[u];
+                ns[u] = app_cnt(f);
+                xs[u] = app_list(f, j);  // (entries past the count are 0)
+                // the current value: the staged copy once staged (an exact copy), else the global row
+                olds[u] = stg_ok ? lds_rd(lbase + (size_t)f * S + xs[u]) : ldp(base + (size_t)f * S + xs[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int t = t0 + u * NT;
+                if (t >= FS) break;
+                const int f = fs[u], j = js[u], n = ns[u], x = xs[u];
+                if (!(sub[f] && j < n)) continue;
+                double g = gbuf[t];
+                if (!tape) g = g / ftot[f];
+                const double old = olds[u];
+                stp(base + (size_t)f * S + x, g);
+                if (stg) lbase[(size_t)f * S + x] = g;  // the staged copy follows
+                if (al) {
+                    const double am1 = alv(comp, row, f * S + x) - 1.0;
+                    dp += xlogy(am1, g) - xlogy(am1, old);
+                }
+                if (want_dl) {
+                    const int c = cnt[f * S + x];
+                    if (c > 0) {
+                        // (one log of the ratio)
+                        if (g > 0.0 && old > 0.0 && g < INFINITY && old < INFINITY) dl += (double)c * flog(g / old);
+                        else zfl = 1;
+                    }
                 }
             }
         }
@@ -1430,6 +1479,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
     bool broken = false;
     for (int step = 0; step < a.n_steps; step++) {
         if (rng.bad || broken) break;
+        const uint64_t sst = SBZ_TB_STAMP ? __builtin_amdgcn_s_memtime() : 0;  // step start (stamp builds)
         // rng.op with the CDF in LDS: numpy choice(p), the number of cdf entries <= u
         int op;
         if (rng.tape) {
@@ -1844,6 +1894,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             // ---- gibbs_sample_p_global / p_zones / p_families
             // (SBZ_TB_STAMP builds: cycles of the subset + counts, redraw_rows and the ll update)
             uint64_t gst = SBZ_TB_STAMP ? __builtin_amdgcn_s_memtime() : 0;
+            if (SBZ_TB_STAMP) tbst[13] += gst - sst;
             auto gstamp = [&](int k) {
                 if (SBZ_TB_STAMP) {
                     const uint64_t t = __builtin_amdgcn_s_memtime();
@@ -1868,10 +1919,20 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             if constexpr (TB) {
                 // the count table's row of this component: p_global [S], p_zones [row][S],
                 // p_families [row][S] per feature (subset features only)
+                // (four items per thread in flight: the loads first, unconditional, then the stores)
                 const int off = comp == 0 ? 0 : (comp == 1 ? S + row * S : S * (1 + Z) + row * S);
-                for (int i = tid; i < FS; i += NT) {
-                    const int f = i / S, x = i - f * S;
-                    cnt[i] = sub[f] ? ldi(ct_cur + (size_t)f * td.CTP + off + x) : 0;
+                for (int i0 = tid; i0 < FS; i0 += 4 * NT) {
+                    int v[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const int i = min(i0 + u * NT, FS - 1), f = i / S, x = i - f * S;
+                        v[u] = ldi(ct_cur + (size_t)f * td.CTP + off + x);
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const int i = i0 + u * NT;
+                        if (i < FS) cnt[i] = sub[i / S] ? v[u] : 0;
+                    }
                 }
             } else {
                 clear_cnt();
@@ -2000,6 +2061,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             for (int s = tid; s < N; s += NT) tz[s] = zos[s];
         }
         if (bor(err)) break;  // an out-of-range index (reported below)
+        if (SBZ_TB_STAMP && op >= G_P_GLOBAL && op <= G_P_FAMILIES) tbst[12] += __builtin_amdgcn_s_memtime() - sst;
     }
 
     sync();
@@ -2069,10 +2131,10 @@ int launch_mh_source(sbz_ctx *ctx, int B, const MhArgs &a0) {
     // parameters staged in LDS when they fit too (SBZ_OPT_SRC_STAGE 0: off; not with the table passes)
     a.stage = !tb && ctx->src_stage && mh_src_lds_bytes(d, ctx->C, gs, geo, true) + gib <= LDS_MAX ? 1 : 0;
     size_t lds = mh_src_lds_bytes(d, ctx->C, gs, geo, a.stage != 0, tb, ctx->Np, nw);
-    // the constant tables too, when they fit beside the staged parameters
+    // the constant tables too, when they fit beside the staged parameters or the table-pass region
     const size_t cst = mh_src_const_bytes(d, ctx->C, a.alpha_g != nullptr, a.alpha_f != nullptr,
                                           a.gc_g != nullptr, a.gc_f != nullptr);
-    a.cstage = a.stage && d.n_states <= 255 && lds + cst + gib <= LDS_MAX ? 1 : 0;
+    a.cstage = (a.stage || tb) && d.n_states <= 255 && lds + cst + gib <= LDS_MAX ? 1 : 0;
     if (a.cstage) lds += cst;
     if (a.gib) {  // gibbsish_sample_zones scratch at the end (16-B aligned)
         lds = (lds + 15) & ~(size_t)15;

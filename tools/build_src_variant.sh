@@ -9,6 +9,6 @@ name=$1; shift
 TORCH_LIB=$(python -c 'import os,torch;print(os.path.join(os.path.dirname(torch.__file__),"lib"))')
 mkdir -p build_$name
 make -s build/sbz_api.o build/sbz_lik.o build/sbz_mh.o
-/opt/rocm/bin/hipcc ${OPT:--O3} -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off "$@" -c sbz_mh_src.hip -o build_$name/sbz_mh_src.o
+/opt/rocm/bin/hipcc ${OPT:--O3} -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -mllvm -disable-machine-licm "$@" -c sbz_mh_src.hip -o build_$name/sbz_mh_src.o
 g++ -shared -o ../libsbz_$name.so build/sbz_api.o build/sbz_lik.o build/sbz_mh.o build_$name/sbz_mh_src.o \
     -L$TORCH_LIB -lamdhip64 -Wl,--disable-new-dtags,-rpath,$TORCH_LIB -Wl,--no-undefined

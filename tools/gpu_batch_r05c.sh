@@ -2,3 +2,5 @@ set -o pipefail
 : > gpurun_out/r05_tb_stamps6.txt
 for set in p_zones p_global; do SBZ_LIB_PATH=$PWD/contact_zones_amd/libsbz_stamp.so timeout -k 10 300 python -u tools/tb_stamps.py 100 $set 2>&1 | grep -v amdgpu.ids >> gpurun_out/r05_tb_stamps6.txt || exit 1; done
 cat gpurun_out/r05_tb_stamps6.txt
+timeout -k 10 300 python -u -m pytest tests/test_gpu_source.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r05_src_tests.log 2>&1; rc=$?; tail -2 gpurun_out/r05_src_tests.log; [ $rc -eq 0 ] || exit $rc
+VARIANTS="default" SETS=default,zone_moves bash tools/ab_src_sets.sh 2>&1

@@ -45,7 +45,9 @@ def main():
            "total_wave0": float(w0.sum()), "total_lastwave": float(w7.sum()),
            "p_step_cycles_per_step": dict(zip(["subset + counts", "redraw_rows", "ll update"],
                                               gib.round(0).tolist())),
-           "redraw_cycles_per_step": dict(zip(["scan", "alphas", "gammas", "rows + delta"], rdr.round(0).tolist()))}
+           "redraw_cycles_per_step": dict(zip(["scan", "alphas", "gammas", "rows + delta"], rdr.round(0).tolist())),
+           "p_step_total_cycles_per_step": float(ll[:, 12].mean() / steps),
+           "p_step_head_cycles_per_step": float(ll[:, 13].mean() / steps)}
     print(json.dumps(out))
 
 
