@@ -118,7 +118,10 @@ if __name__ == "__main__":
     refenv.setup()
     if len(sys.argv) > 1 and sys.argv[1] == "cfg5":
         sys.path.insert(0, ROOT)
-        print(json.dumps(run_cfg5(), indent=1), flush=True)
+        import contextlib
+        with contextlib.redirect_stdout(sys.stderr):  # the reference's own progress prints
+            res = run_cfg5()
+        print(json.dumps(res, indent=1), flush=True)
     else:
         for name, z, steps in (("balkan", 3, 2000), ("south_america", 6, 1000)):
             print(json.dumps(run(name, z, steps)), flush=True)
