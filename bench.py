@@ -210,6 +210,39 @@ def pmc_kernel_traffic(args, B, prefix):
     return None, None
 
 
+def pmc_source_sampler():
+    """PMC counters of the source-mode sampler kernel per chain-step, from the newest committed
+    profiles/r*_pmc_src*.json (tools/pmc_src.sh: the cfg5 shape, 256 chains, default operators)
+    measured on these kernel sources; a note naming the newest stale one otherwise."""
+    import glob
+    stale = None
+    for fn in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_src*.json")), reverse=True):
+        try:
+            d = json.load(open(fn))
+        except (OSError, ValueError):
+            continue
+        m = d.get("_meta", {})
+        rel = os.path.relpath(fn, ROOT)
+        if m.get("source_hash") != kernel_source_hash():
+            stale = stale or rel
+            continue
+        for k, e in d.get("_per_kernel", {}).items():
+            if not k.startswith("mh_src_kernel") or "traffic_bytes" not in e:
+                continue
+            steps, n, chains = m["src_steps_total"], e["dispatches"], m["src_chains"]
+            per = n / steps  # dispatch means -> per step
+            return {"source": rel, "kernel": k, "set": m.get("src_set"),
+                    "hbm_bytes_per_chain_step": e["traffic_bytes"] * per / chains,
+                    "valu_insts_per_wave_step": e["valu_insts_per_wave"] * per if "valu_insts_per_wave" in e else None,
+                    "lds_insts_per_wave_step": e["lds_insts_per_wave"] * per if "lds_insts_per_wave" in e else None,
+                    "wait_any_frac": e.get("wait_any_frac"), "active_inst_any_frac": e.get("active_inst_any_frac"),
+                    "lds_bank_conflict_frac": e.get("lds_bank_conflict_frac"), "l2_hit_rate": e.get("l2_hit_rate"),
+                    "correction": "FETCH_SIZE x2 (gfx950), WRITE_SIZE x1; averaged over the profile's "
+                                  "dispatches and divided by its steps"}
+    return {"note": f"no PMC profile of these kernel sources; the newest of an earlier build is {stale}"
+            if stale else "no PMC profile"}
+
+
 def pmc_secondary(args, B):
     """The binding on-chip resources of the dominant kernel, from the same committed PMC summary
     as `traffic` (its average counters per launch; these kernel sources only): the LDS array's busy
@@ -1053,6 +1086,8 @@ def main():
         shape = {k: getattr(args, k) for k in ("sites", "features", "states", "zones", "families")}
         sampler_src = source_sampler_leg(shape, B, args.src_sampler_steps, args.src_sampler_burnin, args.seed,
                                          rank, world, local_rank, gpu_init=True)
+        if sampler_src is not None:
+            sampler_src["pmc"] = pmc_source_sampler()
     other = None
     if args.other_steps > 0 and not src_mode:
         other = other_configs_leg(args, dev, stream, rank, world, local_rank)

@@ -18,10 +18,10 @@ rm -rf gpurun_out/prof5
 run timeout -k 10 500 rocprofv3 --kernel-trace --stats -d gpurun_out/prof5 -o run --output-format csv -- python3 bench.py --steps 200 --warmup 20 --cpu-seconds 0 --cpu-sampler-seconds 0 > gpurun_out/prof5.log 2>&1
 find gpurun_out/prof5 -name "*kernel_stats.csv" -exec head -12 {} \;
 rm -rf gpurun_out/pmc5
-PMC_OUT=gpurun_out/pmc5 run timeout -k 10 900 bash tools/pmc.sh --mh-steps 0 --src-steps 0 --other-steps 0 > gpurun_out/pmc5.log 2>&1
+PMC_OUT=gpurun_out/pmc5 run timeout -k 10 900 bash tools/pmc.sh --mh-steps 0 --src-steps 0 --other-steps 0 --cpu-sampler-seconds 0 --src-sampler-steps 0 > gpurun_out/pmc5.log 2>&1
 tail -8 gpurun_out/pmc5.log
 rm -rf gpurun_out/pmc5_src
-PMC_OUT=gpurun_out/pmc5_src run timeout -k 10 900 bash tools/pmc_src.sh default 200 > gpurun_out/pmc5_src.log 2>&1
+PMC_OUT=gpurun_out/pmc5_src run timeout -k 10 900 bash tools/pmc_src.sh default 2000 > gpurun_out/pmc5_src.log 2>&1
 tail -8 gpurun_out/pmc5_src.log
 SBZ_DIST_BACKEND=gloo run timeout -k 10 400 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29631 bench.py --gpus 2 --steps 50 --warmup 5 --cpu-seconds 0 --cpu-sampler-seconds 0 --src-sampler-steps 200 --src-sampler-burnin 50 --mh-steps 2000 --mh-burnin 2000 --src-steps 200 --src-burnin 200 > gpurun_out/bench_2rank.json 2> gpurun_out/bench_2rank.err
 tail -c 300 gpurun_out/bench_2rank.json

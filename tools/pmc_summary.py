@@ -31,6 +31,7 @@ for k, d in vals.items():
     for c, v in sorted(d.items()):
         m = sum(v) / len(v)
         summary[k][c] = m
+        summary[k]["_dispatches"] = len(v)
         print(f"  {c:28s} mean {m:.6g}  (n={len(v)})")
 mix = [k for k in summary if "mixture_kernel" in k or "zoned_kernel" in k]
 if mix:
@@ -52,7 +53,7 @@ summary["_per_kernel"] = {}
 for k, s in summary.items():
     if k.startswith("_") or not isinstance(s, dict):
         continue
-    e = {}
+    e = {"dispatches": s.get("_dispatches")}
     if "FETCH_SIZE" in s or "WRITE_SIZE" in s:
         e["fetch_bytes"] = s.get("FETCH_SIZE", 0.0) * 1024 * 2
         e["write_bytes"] = s.get("WRITE_SIZE", 0.0) * 1024
@@ -88,5 +89,7 @@ for log in sorted(glob.glob(os.path.join(out, "p*.log"))):
                 meta["workload"] = cfg.get("workload")
             except (ValueError, KeyError):
                 pass
+if os.environ.get("PMC_META"):  # extra _meta fields of the caller (tools/pmc_src.sh)
+    meta.update(json.loads(os.environ["PMC_META"]))
 summary["_meta"] = meta
 json.dump(summary, open(os.path.join(out, "pmc.json"), "w"), indent=1)
