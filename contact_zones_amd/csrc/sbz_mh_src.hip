@@ -265,17 +265,19 @@ struct TbPassOut {
 };
 // the per-cell uniforms of a Philox resample pass: xoroshiro128+ seeded per thread and pass from
 // one Philox block keyed (seed; thread, counter, chain, 0xFD tag) — a stream no LaneRng / site
-// stream shares; its top 52 bits make the uniform (1 + r 2^-52 - 1)
+// stream shares; each 64-bit output gives two cells their uniforms, its high and its low 32 bits
+// (w 2^-32: a 3-way categorical draw needs no finer grid)
 struct Xoro {
     uint64_t s0, s1;
-    __device__ __forceinline__ double u() {
+    __device__ __forceinline__ uint64_t next() {
         const uint64_t r = s0 + s1;
         const uint64_t t = s1 ^ s0;
         s0 = ((s0 << 24) | (s0 >> 40)) ^ t ^ (t << 16);
         s1 = (t << 37) | (t >> 27);
-        return __longlong_as_double((long long)(0x3FF0000000000000ull | (r >> 12))) - 1.0;
+        return r;
     }
 };
+__device__ __forceinline__ double u32u(uint32_t w) { return (double)w * 0x1p-32; }
 // per-thread sum of logs as one log: mantissas multiplied, exponents added (exact for any factor)
 struct TbLogAcc {
     double m = 1.0;
@@ -458,14 +460,18 @@ __device__ __noinline__ TbPassOut tb_pass(TbPassArgs pa) {
         }
     };
 
-    // per-position class words: table row base | zone class << 16 | family class << 24
+    // per-position class words: table row base | the zone counters' row << 16 | the family
+    // counters' row << 24 (the count table's p_zones [zc] / p_families [fc - 1] rows; 255: none, the
+    // site is in no zone / no family; CTP <= 192)
     for (int p = tid; p < Np; p += NT) {
-        uint32_t pw = 0;
+        uint32_t pw = 0xffff0000u;
         if (p < N) {
             const int z0 = zos[perm[p]];
             const int zc = z0 < Z ? z0 : Z;
             const int fc = C == 3 ? (int)famc[p] : 0;
-            pw = (uint32_t)((zc * FamC + fc) * (S + 1)) | ((uint32_t)zc << 16) | ((uint32_t)fc << 24);
+            const uint32_t b1 = zc < Z ? (uint32_t)(S + zc * S) : 255u;
+            const uint32_t b2 = fc > 0 ? (uint32_t)(FX + (fc - 1) * S) : 255u;
+            pw = (uint32_t)((zc * FamC + fc) * (S + 1)) | (b1 << 16) | (b2 << 24);
         }
         pinfo[p] = pw;
     }
@@ -597,6 +603,11 @@ __device__ __noinline__ TbPassOut tb_pass(TbPassArgs pa) {
             const uint4 pin = *reinterpret_cast<const uint4 *>(pinfo + min(p0, Np - 4));
             const uint32_t pis[4] = {pin.x, pin.y, pin.z, pin.w};
             uint32_t outw = 0;
+            uint64_t rr[2] = {0, 0};  // MODE 0: the four cells' uniforms
+            if (MODE == 0) {
+                rr[0] = xr.next();
+                rr[1] = xr.next();
+            }
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 // (selects, no branches: every lane runs the same instructions)
@@ -617,7 +628,8 @@ __device__ __noinline__ TbPassOut tb_pass(TbPassArgs pa) {
                         const int k12 = u < c1 ? 1 : ((C == 3 && u < c2) ? 2 : 0);
                         k = u < q0 ? 0 : k12;
                     } else {
-                        const double us = ((ABL & 8) ? 0.5 : xr.u()) * sum;
+                        const uint32_t w32 = (j & 1) ? (uint32_t)rr[j >> 1] : (uint32_t)(rr[j >> 1] >> 32);
+                        const double us = ((ABL & 8) ? 0.5 : u32u(w32)) * sum;
                         const int k12 = us < t0 + t1 ? 1 : ((C == 3 && us < sum) ? 2 : 0);
                         k = us < t0 ? 0 : k12;
                     }
@@ -636,15 +648,14 @@ __device__ __noinline__ TbPassOut tb_pass(TbPassArgs pa) {
                     acc.m *= __builtin_amdgcn_frexp_mant(t);
                     acc.e += __builtin_amdgcn_frexp_exp(t);
                 }
-                const int zc = (pis[j] >> 16) & 255, fc = (int)(pis[j] >> 24);
-                const bool hz = zc < Z, hf = fc > 0;
+                const uint32_t b1 = (pis[j] >> 16) & 255u, b2 = pis[j] >> 24;
+                const bool hz = b1 != 255u, hf = b2 != 255u;
                 if (!(ABL & 1)) {
                     // the component row's counter: p_global [x], p_zones [zc][x], p_families [fc - 1][x]
-                    const int row = k == 0 ? 0 : (k == 1 ? S + zc * S : FX + (fc - 1) * S);
-                    const bool cnt_it = val && x < S && (k == 0 || (k == 1 && hz) || (k == 2 && hf));
-                    if (cnt_it) atomicAdd(&kc[row + x], 1);
+                    const uint32_t row = k == 0 ? 0u : (k == 1 ? b1 : b2);
+                    if (val && x < S && row != 255u) atomicAdd(&kc[row + x], 1);
                 }
-                const uint32_t inc = val ? 1u << (8 * ((hz ? 1 : 0) | (hf ? 2 : 0))) : 0u;
+                const uint32_t inc = val ? 1u << ((hz ? 8 : 0) + (hf ? 16 : 0)) : 0u;
                 R[0] += k == 0 ? inc : 0u;
                 R[1] += k == 1 ? inc : 0u;
                 R[2] += k == 2 ? inc : 0u;
@@ -1782,7 +1793,14 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                 for (int f = tid; f < F; f += NT) {
                     const int *wc = ct_cur + (size_t)f * td.CTP + td.WOFF;
                     const int h1 = (C == 2 || fixed == 0) ? 1 : 2;
-                    for (int k = 0; k < C; k++) cnt[f * C + k] = ldi(wc + h1 * 3 + k) + ldi(wc + 9 + k);
+                    int a3[3], b3[3];
+#pragma unroll
+                    for (int k = 0; k < 3; k++) {
+                        a3[k] = ldi(wc + h1 * 3 + k);
+                        b3[k] = ldi(wc + 9 + k);
+                    }
+#pragma unroll
+                    for (int k = 0; k < C; k++) cnt[f * C + k] = a3[k] + b3[k];
                 }
             } else {
                 clear_cnt();
@@ -1853,7 +1871,11 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                 }
                 if constexpr (TB) {
                     // sum over classes h and components k of count * (log w_norm new - log w_norm old)
+                    // (the 12 counters loaded at once)
                     const int *wc = ct_cur + (size_t)f * td.CTP + td.WOFF;
+                    int wcv[12];
+#pragma unroll
+                    for (int i = 0; i < 12; i++) wcv[i] = ldi(wc + i);
 #pragma unroll
                     for (int h = 0; h < 4; h++) {
                         const double on1 = o[1] * ((h & 1) ? 1.0 : 0.0), nn1 = n[1] * ((h & 1) ? 1.0 : 0.0);
@@ -1865,8 +1887,9 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                             sn = sn + nn2;
                         }
                         const double ov[3] = {o[0] * 1.0, on1, on2}, nv[3] = {n[0] * 1.0, nn1, nn2};
+#pragma unroll
                         for (int k = 0; k < C; k++) {
-                            const int c = ldi(wc + h * 3 + k);
+                            const int c = wcv[h * 3 + k];
                             if (c <= 0) continue;
                             const double wo = ov[k] / so, wn = nv[k] / sn;
                             if (wo > 0.0 && wn > 0.0 && wo < INFINITY && wn < INFINITY) wdl += (double)c * (flog(wn) - flog(wo));
