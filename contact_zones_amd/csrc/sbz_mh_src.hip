@@ -1283,8 +1283,21 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
         // every (feature, state) draw at once: thread t <-> (f, j) = (t / S, t % S).  Feature f's
         // draws are its tape values pos + fpre[f] + j, or the gammas of lane stream j at counter
         // ctr + frank[f] (LaneRng, as one wave per feature drew them), fpre / frank the exclusive
-        // scans over the subset features (wave 0, 64 features at a time).
-        if (wv == 0) {
+        // scans over the subset features (wave 0, 64 features at a time).  Philox needs only frank:
+        // every wave counts the subset blocks by ballots and writes the ranks of its own blocks.
+        if (!tape) {
+            int cr = 0;
+            for (int f0 = 0; f0 < F; f0 += WAVE) {
+                const int f = f0 + lane;
+                const uint64_t m = __ballot(f < F && sub[f]);
+                if ((f0 / WAVE) % NW == wv && f < F) frank[f] = cr + lane_prefix(m);
+                cr += __popcll(m);
+            }
+            if (tid == 0) {
+                misc_i[0] = 0;
+                misc_i[1] = cr;
+            }
+        } else if (wv == 0) {
             int cn = 0, cr = 0;
             for (int f0 = 0; f0 < F; f0 += WAVE) {
                 const int f = f0 + lane;
@@ -1892,7 +1905,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                             const int c = wcv[h * 3 + k];
                             if (c <= 0) continue;
                             const double wo = ov[k] / so, wn = nv[k] / sn;
-                            if (wo > 0.0 && wn > 0.0 && wo < INFINITY && wn < INFINITY) wdl += (double)c * (flog(wn) - flog(wo));
+                            if (wo > 0.0 && wn > 0.0 && wo < INFINITY && wn < INFINITY) wdl += (double)c * flog(wn / wo);
                             else wzf = 1;
                         }
                     }
