@@ -378,3 +378,57 @@ def test_source_sampler_cfg5_philox_invariants(gpu_available):
     np.testing.assert_array_equal(out2["ll"].cpu().numpy(), ll_trace)
     np.testing.assert_array_equal(st2.source.cpu().numpy(), src)
     np.testing.assert_array_equal(st2.zone_of_site.cpu().numpy(), zs)
+
+
+def test_source_sampler_gibbsish_scratch_at_lds_boundary(gpu_available):
+    """the gibbsish_sample_zones scratch (21 N bytes) counts in the placement of
+    the sources.  At the largest feature count whose sources still fit LDS without it (found by
+    bisection on the kernel the context reports), a run with a non-zero gibbsish weight must not
+    fail: the sampler moves the sources to HBM and keeps every invariant."""
+    import torch
+    from scipy.spatial import Delaunay
+
+    from contact_zones_amd.likelihood import LikelihoodEngine
+    from contact_zones_amd.sampler import ChainState, Sampler, precisions
+    rng = np.random.default_rng(8)
+    N, S, Z, Fam, B = 240, 3, 2, 2, 4
+    indptr, indices = Delaunay(rng.random((N, 2))).vertex_neighbor_vertices
+    fam = rng.integers(0, Fam, size=N).astype(np.uint8)
+    fam[rng.random(N) < 0.3] = 255
+    prec = precisions({"weights": 15, "universal": 40, "contact": 20, "inheritance": 20})
+    base_ops = {"shrink_zone": 0.1, "grow_zone": 0.1, "swap_zone": 0.05, "gibbs_sample_weights": 0.25,
+                "gibbs_sample_p_global": 0.1, "gibbs_sample_p_zones": 0.25, "gibbs_sample_p_families": 0.15}
+
+    def run(F, gib_weight, steps=1, seed=3):
+        r = np.random.default_rng(F)
+        obs = r.integers(0, S, size=(N, F)).astype(np.int8)
+        eng = LikelihoodEngine(obs, fam, S, Z, Fam, True)
+        ops = dict(base_ops, gibbsish_sample_zones=gib_weight)
+        smp = Sampler(eng, np.ones((F, S), bool), indptr, indices, ops, prec, 3, sample_source=True)
+        zos = np.full((B, N), 255, np.uint8)
+        for b in range(B):
+            p = r.permutation(N)
+            zos[b, p[:8]], zos[b, p[8:16]] = 0, 1
+        st = ChainState(eng, zos, r.dirichlet(np.ones(3), size=(B, F)), r.dirichlet(np.ones(S), size=(B, F)),
+                        r.dirichlet(np.ones(S), size=(B, Z, F)), r.dirichlet(np.ones(S), size=(B, Fam, F)),
+                        source=np.zeros((B, N, F), np.uint8))
+        out = smp.run(st, steps, np.full(B, 50), np.full(B, 0.85), seed=seed)
+        torch.cuda.synchronize()
+        return eng, st, out
+
+    lo, hi = 20, 400  # sources in LDS at lo, in HBM at hi (without the gibbsish scratch)
+    assert "<lds>" in run(lo, 0.0)[0].last_kernels() and "<hbm" in run(hi, 0.0)[0].last_kernels()
+    while hi - lo > 1:
+        mid = (lo + hi) // 2
+        if "<lds>" in run(mid, 0.0)[0].last_kernels():
+            lo = mid
+        else:
+            hi = mid
+    eng, st, out = run(lo, 0.3, steps=200)
+    assert out["status"].cpu().numpy().tolist() == [0] * B
+    assert "<hbm" in eng.last_kernels()
+    s = st.to_numpy()
+    assert not np.any((s["source"] == 1) & (s["zone_of_site"] == 255)[:, :, None])
+    assert not np.any((s["source"] == 2) & (fam == 255)[None, :, None])
+    fresh = st.refresh_ll().cpu().numpy()
+    assert np.max(np.abs(s["ll"] - fresh) / np.abs(fresh)) <= REL_TOL
