@@ -193,7 +193,7 @@ size_t mh_src_const_bytes(const sbz_dims &d, int C, bool alg, bool alf, bool gcg
 #ifndef SBZ_SRC_UNR
 #define SBZ_SRC_UNR 1
 #endif
-// Philox Gibbs draws per thread at once (gamma_batch): p_* redraws, weights
+// Philox Gibbs draws in flight per thread (gamma_fill slots): p_* redraws, weights
 #ifndef SBZ_RB_REDRAW
 #define SBZ_RB_REDRAW 4
 #endif
@@ -1794,6 +1794,8 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             }
             new_sources = true;
         } else if (op == G_WEIGHTS) {
+            // (SBZ_TB_STAMP builds: cycles of the counts + gammas [14], of the whole operator [15])
+            const uint64_t wst = SBZ_TB_STAMP ? __builtin_amdgcn_s_memtime() : 0;
             // source counts per feature over the sites of a zone (or of a family)
             const int fixed = C == 3 ? rng.below(2) : 0;  // random.choice(['inheritance', 'contact'])
             if (fixed < 0 || fixed > 1) {
@@ -1823,8 +1825,6 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                 });
             }
             sync();
-            LaneRng lr;
-            lr.initw(rng, tid);
             const int64_t pos0 = rng.pos;
             const int64_t need = 2LL * F;  // C == 2: F pairs; C == 3: F beta draws + F uniforms
             const bool have = !rng.tape || pos0 + need <= rng.len;
@@ -1841,12 +1841,20 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                 gamma_fill<SBZ_RB_WEIGHTS, NT>((lds_ptr<double>)gbuf, 2 * F, 1, (lds_ptr<const int>)nullptr,
                                                rng.key0, rng.key1, (uint32_t)rng.chain, rng.ctr, 1);
                 sync();
+                if (SBZ_TB_STAMP) tbst[14] += __builtin_amdgcn_s_memtime() - wst;
             }
             double wdl = 0.0;  // TB: the log-likelihood change from the class counters
             int wzf = 0;
             for (int f = tid; f < F; f += NT) {
                 double *wf = w + (size_t)f * C;
                 double o[3] = {ldp(wf), ldp(wf + 1), C == 3 ? ldp(wf + 2) : 0.0}, n[3] = {0.0, 0.0, 0.0};
+                // TB: the feature's 12 class counters, loaded with the old weights
+                int wcv[12];
+                if constexpr (TB) {
+                    const int *wc = ct_cur + (size_t)f * td.CTP + td.WOFF;
+#pragma unroll
+                    for (int i = 0; i < 12; i++) wcv[i] = ldi(wc + i);
+                }
                 if (C == 2) {
                     double d0, d1;
                     if (rng.tape) {
@@ -1884,11 +1892,14 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                 }
                 if constexpr (TB) {
                     // sum over classes h and components k of count * (log w_norm new - log w_norm old)
-                    // (the 12 counters loaded at once)
-                    const int *wc = ct_cur + (size_t)f * td.CTP + td.WOFF;
-                    int wcv[12];
+                    // log(wn / wo) = log(n_k / o_k) + log(so_h / sn_h): 3 + 4 logs per feature
+                    double lk[3];
+                    bool okk[3];
 #pragma unroll
-                    for (int i = 0; i < 12; i++) wcv[i] = ldi(wc + i);
+                    for (int k = 0; k < 3; k++) {
+                        okk[k] = k < C && o[k] > 0.0 && n[k] > 0.0 && o[k] < INFINITY && n[k] < INFINITY;
+                        lk[k] = okk[k] ? flog(n[k] / o[k]) : 0.0;
+                    }
 #pragma unroll
                     for (int h = 0; h < 4; h++) {
                         const double on1 = o[1] * ((h & 1) ? 1.0 : 0.0), nn1 = n[1] * ((h & 1) ? 1.0 : 0.0);
@@ -1899,13 +1910,14 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                             so = so + on2;
                             sn = sn + nn2;
                         }
-                        const double ov[3] = {o[0] * 1.0, on1, on2}, nv[3] = {n[0] * 1.0, nn1, nn2};
+                        const bool oks = so > 0.0 && sn > 0.0 && so < INFINITY && sn < INFINITY;
+                        const double lh = oks ? flog(so / sn) : 0.0;
 #pragma unroll
                         for (int k = 0; k < C; k++) {
                             const int c = wcv[h * 3 + k];
                             if (c <= 0) continue;
-                            const double wo = ov[k] / so, wn = nv[k] / sn;
-                            if (wo > 0.0 && wn > 0.0 && wo < INFINITY && wn < INFINITY) wdl += (double)c * flog(wn / wo);
+                            const bool present = k == 0 || (k == 1 ? (h & 1) != 0 : (h & 2) != 0);
+                            if (present && okk[k] && oks) wdl += (double)c * (lk[k] + lh);
                             else wzf = 1;
                         }
                     }
@@ -1923,6 +1935,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                 ll_new = (bor(wzf) || !(ll > -INFINITY && ll < INFINITY))
                              ? tpass(std::integral_constant<int, 1>(), src, nullptr, ct_alt)
                              : uni(ll + d);
+                if (SBZ_TB_STAMP) tbst[15] += __builtin_amdgcn_s_memtime() - wst;
             } else {
                 ll_new = pass_ll(src);
             }

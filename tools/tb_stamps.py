@@ -18,7 +18,8 @@ def main():
     shape = {"sites": 2000, "features": 500, "states": 10, "zones": 8, "families": 4}
     sets = {"zone_moves": {"shrink_zone": 0.4, "grow_zone": 0.4, "swap_zone": 0.2},
             "p_zones": {"gibbs_sample_p_zones": 1.0}, "p_global": {"gibbs_sample_p_global": 1.0},
-            "weights": {"gibbs_sample_weights": 1.0}, "sources": {"gibbs_sample_sources": 1.0}}
+            "weights": {"gibbs_sample_weights": 1.0}, "sources": {"gibbs_sample_sources": 1.0},
+            "p_families": {"gibbs_sample_p_families": 1.0}}
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 40
     ops = sets[sys.argv[2] if len(sys.argv) > 2 else "zone_moves"]
     bench.src_operators = lambda inh=True: dict(ops)
@@ -47,7 +48,9 @@ def main():
                                               gib.round(0).tolist())),
            "redraw_cycles_per_step": dict(zip(["scan", "alphas", "gammas", "rows + delta"], rdr.round(0).tolist())),
            "p_step_total_cycles_per_step": float(ll[:, 12].mean() / steps),
-           "p_step_head_cycles_per_step": float(ll[:, 13].mean() / steps)}
+           "p_step_head_cycles_per_step": float(ll[:, 13].mean() / steps),
+           "weights_counts_gammas_cycles_per_step": float(ll[:, 14].mean() / steps),
+           "weights_op_cycles_per_step": float(ll[:, 15].mean() / steps)}
     print(json.dumps(out))
 
 
