@@ -2003,7 +2003,7 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
             int dzf = 0;
             gstamp(5);
             dprior = redraw_rows(base, lbase, comp, row, rng.tape, rng.len, rng.key0, rng.key1, rng.chain,
-                                 rpos, rctr, rbad, TB, dll, dzf);
+                                 rpos, rctr, rbad, true, dll, dzf);
             gstamp(6);
             rng.pos = rpos;
             rng.ctr = rctr;
@@ -2018,7 +2018,8 @@ __global__ __launch_bounds__(NW * WAVE) void mh_src_kernel(MhArgs a) {
                              : uni(ll + dll);
                 gstamp(7);
             } else {
-                ll_new = pass_ll(src);
+                // the change from the row's source counts (cnt, as the table kernel's count table)
+                ll_new = (dzf || !(ll > -INFINITY && ll < INFINITY)) ? pass_ll(src) : uni(ll + dll);
             }
         }
 

@@ -16,13 +16,19 @@ STAGES = ["column + weights", "table", "cells", "counts out"]
 
 def main():
     shape = {"sites": 2000, "features": 500, "states": 10, "zones": 8, "families": 4}
+    if os.environ.get("TB_SHAPE"):  # e.g. TB_SHAPE=28,47,3,3,5 (the Balkan shape)
+        shape = dict(zip(["sites", "features", "states", "zones", "families"],
+                         [int(v) for v in os.environ["TB_SHAPE"].split(",")]))
+    chains = int(os.environ.get("TB_CHAINS", "256"))
     sets = {"zone_moves": {"shrink_zone": 0.4, "grow_zone": 0.4, "swap_zone": 0.2},
             "p_zones": {"gibbs_sample_p_zones": 1.0}, "p_global": {"gibbs_sample_p_global": 1.0},
             "weights": {"gibbs_sample_weights": 1.0}, "sources": {"gibbs_sample_sources": 1.0},
             "p_families": {"gibbs_sample_p_families": 1.0}}
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 40
-    ops = sets[sys.argv[2] if len(sys.argv) > 2 else "zone_moves"]
-    bench.src_operators = lambda inh=True: dict(ops)
+    name = sys.argv[2] if len(sys.argv) > 2 else "zone_moves"
+    if name != "default":  # default: bench.src_operators, the reference's STEPS
+        ops = sets[name]
+        bench.src_operators = lambda inh=True: dict(ops)
     cap = {}
     orig = bench.logged_ess if hasattr(bench, "logged_ess") else None
     import contact_zones_amd.diagnostics as dg
@@ -32,7 +38,7 @@ def main():
         cap["ll"] = np.array(ll)
         return real(np.nan_to_num(ll[:, 32:], nan=0.0, posinf=0.0, neginf=0.0))
     dg.logged_ess = grab
-    r = bench.source_sampler_leg(shape, 256, steps, 0, seed=3, gpu_init=True)
+    r = bench.source_sampler_leg(shape, chains, steps, 0, seed=3, gpu_init=True)
     ll = cap["ll"]
     passes = ll[:, 4].mean()  # table passes run by the timed launch (slot 4 of the stamp build)
     feats = passes * (shape["features"] / 8)  # features per wave and pass (8 waves)
