@@ -1088,6 +1088,16 @@ def main():
                                          rank, world, local_rank, gpu_init=True)
         if sampler_src is not None:
             sampler_src["pmc"] = pmc_source_sampler()
+            try:  # the reference's own source-mode sampler, timed in the build container (it never
+                # travels to the GPU box): a reported figure beside the leg, not a box measurement
+                with open(os.path.join(ROOT, "profiles", "r05_cpu_reference_source_sampler.json")) as f:
+                    r = json.load(f)
+                sampler_src["reference_cpu_container"] = {
+                    "steps_per_sec_per_core": r["reference_steps_per_sec_per_core"], "cores": 1,
+                    "kind": "reference", "where": r["where"],
+                    "source": "profiles/r05_cpu_reference_source_sampler.json"}
+            except (OSError, ValueError, KeyError):
+                pass
     other = None
     if args.other_steps > 0 and not src_mode:
         other = other_configs_leg(args, dev, stream, rank, world, local_rank)
