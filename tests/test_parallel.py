@@ -108,3 +108,38 @@ def test_bench_cpu_baseline_processes():
     r = bench.cpu_baseline(args, 0.5)
     assert r["cores"] == 2 and r["kind"] == "port" and r["host_cpu_count"] == os.cpu_count()
     assert r["value"] > 0 and abs(r["per_core"] * 2 - r["value"]) < 1e-9 * r["value"]
+
+
+def test_bench_cpu_sampler_baseline_processes():
+    """The sampler's CPU baseline runs the restated MH step loop
+    (oracle/mh_numpy.step) in one child process per core, all reaped when it returns, and reports
+    measured steps/s per core and all-core, and the ESS of their traces."""
+    import argparse
+    import bench
+    args = argparse.Namespace(sites=200, features=40, states=5, zones=2, families=2, zone_size=20,
+                              seed=3, cpu_procs=2)
+    r = bench.cpu_baseline_sampler(args, 0.5)
+    assert r["cores"] == 2 and r["kind"] == "port" and r["unit"] == "MH steps/s"
+    assert r["value"] > 0 and len(r["steps_per_process"]) == 2 and min(r["steps_per_process"]) > 0
+
+
+def test_bench_source_sampler_pmc_needs_the_same_kernel_sources(tmp_path, monkeypatch):
+    """The source-mode leg reports PMC counters per chain-step only from a committed profile measured
+    on the current kernel sources (its _meta.source_hash); an older build's profile is named, not
+    used."""
+    import json
+    import bench
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    d = {"_meta": {"source_hash": "abc", "src_steps_total": 101, "src_chains": 256, "src_set": "default"},
+         "_per_kernel": {"mh_src_kernel<3, true, 8, true>": {"dispatches": 2, "traffic_bytes": 101 * 256 * 1000.0,
+                                                               "valu_insts_per_wave": 101 * 500.0}}}
+    (prof / "r09_pmc_src.json").write_text(json.dumps(d))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    monkeypatch.setattr(bench, "kernel_source_hash", lambda: "abc")
+    r = bench.pmc_source_sampler()
+    assert r["source"] == "profiles/r09_pmc_src.json"
+    assert abs(r["hbm_bytes_per_chain_step"] - 2000.0) < 1e-9 and abs(r["valu_insts_per_wave_step"] - 1000.0) < 1e-9
+    monkeypatch.setattr(bench, "kernel_source_hash", lambda: "other")
+    r = bench.pmc_source_sampler()
+    assert "source" not in r and "r09_pmc_src.json" in r["note"]
