@@ -48,6 +48,8 @@ def parse():
                    help="bounded CPU-baseline sample (0 disables)")
     p.add_argument("--cpu-sampler-seconds", type=float, default=12.0,
                    help="sampler CPU baseline: seconds per worker process (0 disables)")
+    p.add_argument("--cpu-src-sampler-seconds", type=float, default=12.0,
+                   help="SAMPLE_SOURCE = true sampler CPU baseline: seconds per worker process (0 disables)")
     p.add_argument("--cpu-procs", type=int, default=0,
                    help="CPU baseline: worker processes, one per core (0: the cores this process "
                         "may run on, at most 16 = a one-GPU box's CPU share)")
@@ -341,7 +343,65 @@ def _cpu_sampler_worker(shape, seconds, seed):
     return {"n": len(lls), "seconds": el, "ll": [float(v) for v in lls]}
 
 
-CPU_WORKERS = {"lik": _cpu_worker, "sampler": _cpu_sampler_worker}
+def _cpu_src_sampler_worker(shape, seconds, seed):
+    """One CPU-baseline process of the SAMPLE_SOURCE = true sampler: the numpy restatement of the
+    MH step loop (oracle/mh_numpy.step with the zone moves' source resampling and the Gibbs
+    operators, every candidate's log-likelihood a full lik_numpy evaluation of the selected
+    components), decisions drawn from a numpy Generator (DrawTape: operator by probability, the
+    Gibbs operators' beta / Dirichlet draws of the source counts, as the reference), on one chain of
+    the source-mode leg's workload (source_sampler_leg's data, network, initial sample and initial
+    sources), run for `seconds`: steps and the log-likelihood trace."""
+    import random
+    import numpy as np
+    from scipy.spatial import Delaunay
+    from contact_zones_amd import packing
+    from contact_zones_amd.mcmc import InitialSamples
+    from contact_zones_amd.sources import draw_sources, source_posterior
+    from oracle import mh_numpy
+    N, F, S, Z, Fam = (shape[k] for k in ("sites", "features", "states", "zones", "families"))
+    inh = Fam > 0
+    rng = np.random.default_rng(shape["seed"])  # source_sampler_leg's data and network
+    obs = rng.integers(0, S, size=(N, F)).astype(np.int8)
+    obs[rng.random((N, F)) < 0.02] = -1
+    fam = rng.integers(0, max(Fam, 1), size=N).astype(np.uint8)
+    fam[rng.random(N) < 0.2] = 255
+    if not inh:
+        fam[:] = 255
+    indptr, indices = Delaunay(rng.random((N, 2))).vertex_neighbor_vertices
+    states = np.ones((F, S), bool)
+    init = InitialSamples(packing.obs_to_features(obs, S), states, indptr, indices,
+                          packing.index_to_groups(fam, Fam) if inh else np.zeros((0, N), bool), Z,
+                          MH_M_INITIAL, inh, None, random.Random(seed * 1000003))
+    zones = init.zones()
+    st = {"zos": packing.zones_to_zone_of_site(zones, N), "w": init.weights(), "pg": init.p_global()[0],
+          "pz": init.p_zones(zones)}
+    if inh:
+        st["pf"] = init.p_families()
+    st["src"] = draw_sources(source_posterior(obs, fam, st["zos"], st["w"], st["pg"], st["pz"], st.get("pf"), inh),
+                             np.random.default_rng(seed + 31).random)
+    ops = src_operators(inh)
+    prec = [MH_PRECISION[k] for k in ("weights", "universal", "contact", "inheritance")]
+    fx = {"obs": obs, "fam_of_site": fam, "states": states, "inheritance": inh, "warmup": False,
+          "min_size": MH_MIN_M, "max_size": np.array([MH_MAX_M]), "p_grow_connected": np.array([MH_P_GROW]),
+          "precision": np.array(prec, np.float64), "adj_indptr": indptr, "adj_indices": indices,
+          "n_zones": Z, "sample_source": True, "gibbs_counts_global": np.ones((F, S)),
+          "gibbs_counts_fam": np.ones((max(Fam, 1), F, S)) if inh else None}
+    m = mh_numpy.Model(fx)
+    probs = [ops.get(k, 0.0) for k in mh_numpy.OPS]
+    tape = mh_numpy.DrawTape(np.random.default_rng(seed), probs)
+    ll, prior = m.loglik(st), m.log_prior(st)
+    lls = []
+    t0 = time.perf_counter()
+    while True:
+        st, ll, prior, _, _ = mh_numpy.step(m, st, ll, prior, 0, tape)
+        lls.append(ll)
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"n": len(lls), "seconds": el, "ll": [float(v) for v in lls]}
+
+
+CPU_WORKERS = {"lik": _cpu_worker, "sampler": _cpu_sampler_worker, "src_sampler": _cpu_src_sampler_worker}
 
 
 def _cgroup_cpus():
@@ -458,6 +518,42 @@ def cpu_baseline_sampler(args, seconds):
                     "reference_equivalent_value": out["value"] / r["restatement_over_reference"],
                     "ratio_source": "profiles/r05_cpu_reference_sampler_ratio.json "
                                     "(tools/time_reference_sampler.py cfg5)"})
+    except (OSError, ValueError, KeyError):
+        pass
+    return out
+
+
+def cpu_baseline_src_sampler(args, seconds):
+    """The SAMPLE_SOURCE = true sampler's CPU baseline on the GPU box: one process per usable core,
+    each running the numpy restatement of the source-mode MH step loop (_cpu_src_sampler_worker) on
+    its own chain of the sampler_source_mode leg's cfg5 workload for `seconds`: steps/s per core and
+    all-core, ESS/s of the log-likelihood traces.  The reference's own source-mode ZoneMCMC on the
+    same shape, timed in the build container (the reference never travels to the box), gives the
+    restatement / reference ratio (profiles/r05_cpu_reference_source_sampler.json)."""
+    import numpy as np
+    from contact_zones_amd.diagnostics import ess
+    procs, avail, quota, usable = _cpu_procs(args)
+    shape = {k: getattr(args, k) for k in ("sites", "features", "states", "zones", "families", "seed")}
+    res = _run_cpu_workers("src_sampler", shape, seconds, [args.seed * 6151 + i for i in range(procs)])
+    rates = [r["n"] / r["seconds"] for r in res]
+    e = [float(ess(np.asarray(r["ll"])[None, :], max_lag=None)[0]) if r["n"] > 3 else 0.0 for r in res]
+    wall = max(r["seconds"] for r in res)
+    out = {"value": float(sum(rates)), "unit": "MH steps/s", "cores": procs, "kind": "port",
+           "per_core": float(sum(rates) / procs), "per_core_min": float(min(rates)),
+           "ess_per_sec": float(sum(e) / wall), "steps_per_process": [r["n"] for r in res],
+           "host_cpu_count": os.cpu_count(), "cores_available": avail, "cgroup_cpu_quota": quota,
+           "sample": f"numpy restatement of MCMCGenerative.step + ZoneMCMC operators with SAMPLE_SOURCE = "
+                     f"true (oracle/mh_numpy.step: zone moves resample every source, Gibbs weights / p_* "
+                     f"draws from the source counts), one chain of the source-mode leg's workload per "
+                     f"process, {procs} processes x {seconds:.0f} s, 1 thread each"}
+    try:
+        with open(os.path.join(ROOT, "profiles", "r06_cpu_source_sampler_ratio.json")) as f:
+            r = json.load(f)
+        out.update({"restatement_over_reference": r["restatement_over_reference"],
+                    "reference_equivalent_value": out["value"] / r["restatement_over_reference"],
+                    "ratio_source": "profiles/r06_cpu_source_sampler_ratio.json (restatement and the "
+                                    "reference's ZoneMCMC, SAMPLE_SOURCE = true, cfg5, both timed in the "
+                                    "build container, 1 thread)"})
     except (OSError, ValueError, KeyError):
         pass
     return out
@@ -948,6 +1044,33 @@ def other_configs_leg(args, dev, stream, rank, world, local_rank):
     return res
 
 
+def reap_children():
+    """End and reap every process this one started that is still alive (the CPU-baseline workers
+    are waited for where they run; this is the check that nothing else was left behind).  Returns
+    what it found: [{"pid", "name", "cmdline"}]."""
+    try:
+        import psutil
+    except ImportError:  # pragma: no cover
+        return []
+    me = psutil.Process()
+    kids = me.children(recursive=True)
+    found = []
+    for k in kids:
+        try:
+            found.append({"pid": k.pid, "name": k.name(), "cmdline": " ".join(k.cmdline())[:200]})
+            k.terminate()
+        except psutil.Error:
+            pass
+    _, alive = psutil.wait_procs(kids, timeout=5)
+    for k in alive:
+        try:
+            k.kill()
+        except psutil.Error:
+            pass
+    psutil.wait_procs(alive, timeout=5)
+    return found
+
+
 def _free_port():
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
@@ -998,8 +1121,12 @@ def main():
     import torch.distributed as dist
 
     # one rank per GPU; a rehearsal with more ranks than GPUs (SBZ_DIST_BACKEND=gloo: RCCL
-    # refuses two ranks on one device) shares the GPUs round-robin
-    local_rank = local_rank % max(1, torch.cuda.device_count())
+    # refuses two ranks on one device) shares the GPUs round-robin and is marked as such in the
+    # line (n_gpus = the distinct devices, "rehearsal": true), never reported as N GPUs
+    n_dev = max(1, torch.cuda.device_count())
+    devices_used = min(world, n_dev)
+    rehearsal = world > n_dev
+    local_rank = local_rank % n_dev
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
@@ -1115,7 +1242,10 @@ def main():
             "metric": METRIC,
             "value": value,
             "unit": "likelihood-evals/s",
-            "n_gpus": world,
+            "n_gpus": devices_used,
+            **({"rehearsal": True, "ranks": world,
+                "rehearsal_note": f"{world} ranks on {devices_used} GPU(s): a test of the N > 1 path, "
+                                  f"not an N-GPU measurement"} if rehearsal else {}),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": wall_max / args.steps * 1e3,
@@ -1134,7 +1264,8 @@ def main():
                 "pool_batches": args.pool,
                 "zone_size": args.zone_size,
                 "workload_key": workload_key(args, B),
-                "parallelism": f"chains sharded over {world} GPU(s)",
+                "parallelism": (f"chains sharded over {world} ranks on {devices_used} GPU(s) (rehearsal)"
+                                if rehearsal else f"chains sharded over {world} GPU(s)"),
             },
             "roofline": {
                 "bound": "hbm",
@@ -1172,9 +1303,17 @@ def main():
             if sampler is not None and args.cpu_sampler_seconds > 0:
                 sampler["cpu_baseline"] = cpu_baseline_sampler(args, args.cpu_sampler_seconds)
                 sampler["speedup_vs_cpu_steps"] = sampler["mh_steps_per_sec"] / sampler["cpu_baseline"]["value"]
+            if sampler_src is not None and args.cpu_src_sampler_seconds > 0:
+                sampler_src["cpu_baseline"] = cpu_baseline_src_sampler(args, args.cpu_src_sampler_seconds)
+                sampler_src["speedup_vs_cpu_steps"] = (sampler_src["mh_steps_per_sec"] /
+                                                       sampler_src["cpu_baseline"]["value"])
+        line["processes_at_exit"] = reap_children()
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    left = reap_children()
+    if left:
+        print(f"bench: ended child processes at exit: {left}", file=sys.stderr, flush=True)
 
 
 if __name__ == "__main__":

@@ -296,6 +296,10 @@ int sbz_set_option(sbz_ctx *ctx, int32_t option, int64_t value) {
             if (value < 1 || value > 24) return fail(ctx, SBZ_EINVAL, "sampler lookahead must be in 1..24");
             ctx->mh_la = (int)value;
             return SBZ_OK;
+        case SBZ_OPT_MH_GROUP:
+            if (value < 1 || value > 4) return fail(ctx, SBZ_EINVAL, "sampler move groups must be in 1..4");
+            ctx->mh_group = (int)value;
+            return SBZ_OK;
         default: return fail(ctx, SBZ_EINVAL, "unknown option " + std::to_string(option));
     }
 }
@@ -311,6 +315,7 @@ int sbz_get_option(const sbz_ctx *ctx, int32_t option, int64_t *value) {
         case SBZ_OPT_SRC_WAVES: *value = ctx->src_waves; return SBZ_OK;
         case SBZ_OPT_MH_LOOKAHEAD: *value = ctx->mh_la; return SBZ_OK;
         case SBZ_OPT_SRC_PASS_TABLES: *value = ctx->src_pass_tables; return SBZ_OK;
+        case SBZ_OPT_MH_GROUP: *value = ctx->mh_group; return SBZ_OK;
         default: return SBZ_EINVAL;
     }
 }

@@ -79,11 +79,11 @@ struct Plans {
 // c (CH = NT * KT sites per chunk, nsc chunks); zos / nb / lst are padded to NpS = nsc * CH.
 struct MhLayout {
     int KT, CH, nsc, NpS, nent, ncol;
-    uint32_t col, zsize, red, nb, zos, selc, lst, tabo, tabn, nw, rowp, ipos, plans, plcol,
+    uint32_t col, zsize, red, nb, zos, selc, lst, wtab, wnw, tdl, gdl, rowp, ipos, plans, plcol,
         plnw, geo, gib;
     size_t total;
     __host__ __device__ MhLayout(int N, int Np, int S, int Z, int Fam, int C, int FamC, int NT,
-                                 bool with_geo = false, int la = 1, bool with_gib = false) {
+                                 bool with_geo = false, int la = 1, bool with_gib = false, int ntab = 1) {
         KT = Np / NT;
         KT = KT < 4 ? 4 : (KT > 32 ? 32 : KT);
         CH = NT * KT;
@@ -104,9 +104,14 @@ struct MhLayout {
         zos = take((size_t)NpS);
         selc = take((size_t)nsc * 16 * 4);  // per chunk: selected sites per wave of the last scan
         lst = take((size_t)NpS * 2);
-        tabo = take((size_t)nent * 8);
-        tabn = take((size_t)nent * 8);
-        nw = take(32 * 8);
+        // a parameter move's cell tables, one pair per table slot (old cells, new cells; 1 where
+        // the move changes nothing; ntab slots, one per wave of a group), its normalised weights
+        // [NWV][2][4][4], the entries decomposed once (tdl), and the grouped moves' deltas (two
+        // slots of 8)
+        wtab = take((size_t)ntab * 2 * nent * 8);
+        wnw = take((size_t)(NT / 64) * 32 * 8);
+        tdl = take((size_t)nent * 4);
+        gdl = take(16 * 8);
         rowp = take((size_t)Np * 4);
         ipos = take((size_t)N * 2);
         // geo prior scratch (geo_zone_prior): key [N] doubles, mem [N] u16, cnt + redd / redi [16]
@@ -142,7 +147,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
     const int N = a.N, F = a.F, S = a.S, Z = a.Z, Fam = (C == 3) ? a.Fam : 0;
     const sbz_chains &ch = a.ch;
 
-    const MhLayout L(N, a.Np, S, Z, a.Fam, C, a.FamC, NT, a.geo_cost != nullptr, a.la, a.gib != 0);
+    const MhLayout L(N, a.Np, S, Z, a.Fam, C, a.FamC, NT, a.geo_cost != nullptr, a.la, a.gib != 0, a.ntab);
     const int KT = L.KT, CH = L.CH, nsc = L.nsc, ncol = L.ncol;
     double *col = reinterpret_cast<double *>(lds + L.col);  // staged parameter column
     int *zsize = reinterpret_cast<int *>(lds + L.zsize);     // [Z]
@@ -157,9 +162,10 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
     // class * FamC + family class, one neutral row (cls = ncls) for padding positions.
     const int S1 = S + 1, FamC = a.FamC, ncls = (Z + 1) * FamC, row_bytes = S1 * 8;
     const int nent = L.nent;
-    double *tabo = reinterpret_cast<double *>(lds + L.tabo);     // [nent] old cells (1 if unchanged)
-    double *tabn = reinterpret_cast<double *>(lds + L.tabn);     // [nent] new cells (1 if unchanged)
-    double *nw = reinterpret_cast<double *>(lds + L.nw);         // [2][4][4] normalised weights
+    double *wtab = reinterpret_cast<double *>(lds + L.wtab);     // [NWV][2][nent] cells old / new
+    double *wnw = reinterpret_cast<double *>(lds + L.wnw);       // [NWV][2][4][4] normalised weights
+    uint32_t *tdl = reinterpret_cast<uint32_t *>(lds + L.tdl);   // [nent] decomposed entries
+    double *gdl = reinterpret_cast<double *>(lds + L.gdl);       // [2][8] grouped moves' deltas
     uint32_t *rowp = reinterpret_cast<uint32_t *>(lds + L.rowp); // [Np] table row (bytes) by position
     uint16_t *ipos = reinterpret_cast<uint16_t *>(lds + L.ipos); // [N] position of each site
     double *plcol = reinterpret_cast<double *>(lds + L.plcol);  // [la][ncol] planned steps' columns
@@ -484,28 +490,6 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
         for (int i = tid + NT * NCV; i < ncol; i += NT) col[i] = ldp(col_src(f, i));
         bsync();
     };
-    // Observation words of feature f: chunk k = 256 positions (4 per lane); wave wv gathers
-    // chunks wv, wv + NWV, ...  OB of them are loaded ahead (clamped: unconditional loads, so
-    // they all issue back to back).
-    constexpr int OB = 4;
-    const int nch = a.Np / 256;
-    const uint32_t *obs32 = reinterpret_cast<const uint32_t *>(a.obs_fm);
-    auto obs_load = [&](int f, int i0, uint32_t (&o)[OB]) {
-        const size_t fo = (size_t)MH_IDX(f, F, 13) * (size_t)(a.Np / 4);
-#pragma unroll
-        for (int i = 0; i < OB; i++)
-            o[i] = obs32[fo + (size_t)min(wv + NWV * (i0 + i), nch - 1) * WAVE + lane];
-    };
-    // delta of a parameter move on feature f: component comp (0 global, 1 zone, 2 family,
-    // 3 weights), row (zone / family), the two altered entries ia, ib with new values va, vb.
-    // A cell's value depends only on (zone class, family class, x), so the block builds two
-    // tables for feature f — the reference cell before and after the move for every (class, x)
-    // whose value the move changes, 1.0 for every other entry — and each site then multiplies one
-    // factor from each (its row offset in rowp, its observation byte), with no per-site tests.
-    // The changed entries are exactly the cells the reference recomputes: every cell for the
-    // weights, state ia / ib of the component's rows otherwise (NA cells do not change).
-    // `o` holds the wave's first OB observation chunks (obs_load, issued early).  Returns this
-    // thread's part of the delta (block_sum).
     // normalize_weights (model.py:436-452) of class h (bit 0: has a zone, bit 1: has a family) for
     // feature weights wc, after the move when nu (weights move: entries ia / ib become va / vb);
     // one division per weight, as the reference
@@ -534,36 +518,51 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
         const int zcl = real ? cls / FamC : 0, fc = real ? cls - (cls / FamC) * FamC : 0;
         return (uint32_t)x | ((uint32_t)zcl << 8) | ((uint32_t)fc << 16) | ((real ? 1u : 0u) << 24);
     };
-    const uint32_t tdec[2] = {tdecomp(min(tid, nent - 1)), tdecomp(min(tid + NT, nent - 1))};
-    // `cl` is feature f's column in LDS (the staged col, or a planned step's column) and `nwp` its
-    // normalised weights before (nwp[0..15]) and after (nwp[16..31]) the move, or null: computed
-    // here into nw.
+    for (int e = tid; e < nent; e += NT) tdl[e] = tdecomp(e);
+    bsync();
+    // Delta of a parameter move, computed by ONE wave (the calling wave; every lane of it gets the
+    // value).  Parameter moves on different features change disjoint cells, so up to NWV planned
+    // moves of a batch get their deltas at once, one per wave (the step loop's grouped path), and
+    // an unplanned move is computed the same way by wave 0: the value of a move's delta does not
+    // depend on how the steps were grouped or planned.  `cl` is feature f's column in LDS (the
+    // staged col, or a planned step's column) and `nwp` its normalised weights before
+    // (nwp[0..15]) and after (nwp[16..31]) the move, or null: computed here into the wave's wnw.
+    // A cell's value depends only on (zone class, family class, x), so the wave builds two tables
+    // for feature f in its own LDS slice — the reference cell before and after the move for every
+    // (class, x) whose value the move changes, 1.0 for every other entry — and each position then
+    // multiplies one factor from each (its row offset in rowp, its observation byte), with no
+    // per-site tests.  The changed entries are exactly the cells the reference recomputes: every
+    // cell for the weights, state ia / ib of the component's rows otherwise (NA cells do not change).
+    constexpr int OBW = 8;  // observation words (chunks of 256 positions) in flight per lane
+    const int nch = a.Np / 256;
+    const uint32_t *obs32 = reinterpret_cast<const uint32_t *>(a.obs_fm);
     auto delta_param = [&](const double *cl, const double *nwp, int f, int comp, int row, int ia, int ib,
-                           double va, double vb, uint32_t (&o)[OB]) {
+                           double va, double vb) -> double {
+        const int wvu = uni(wv);
+        double *tabo = wtab + (size_t)wvu * 2 * nent, *tabn = tabo + nent;
+        // the feature's observation words, all in flight during the table build
+        const size_t fo = (size_t)MH_IDX(f, F, 13) * (size_t)(a.Np / 4);
+        uint32_t o[OBW];
+#pragma unroll
+        for (int i = 0; i < OBW; i++) o[i] = obs32[fo + (size_t)min(i, nch - 1) * WAVE + lane];
         if (!nwp) {
-            if (tid < 8) norm_w(cl + (1 + Z + Fam) * S, comp, ia, ib, va, vb, tid & 3, tid >> 2, nw + tid * 4);
-            bsync();
-            nwp = nw;
+            double *own = wnw + wvu * 32;
+            if (lane < 8) norm_w(cl + (1 + Z + Fam) * S, comp, ia, ib, va, vb, lane & 3, lane >> 2, own + lane * 4);
+            wsync();
+            nwp = own;
         }
-        // the class rows of the wave's first two chunks, read before the tables are built (they
-        // do not depend on them), so the gathers start one LDS round trip earlier
-        const int nci0 = (nch - wv + NWV - 1) / NWV;
-        const uint4 ra0 = *reinterpret_cast<const uint4 *>(rowp + min(wv, nch - 1) * 256 + 4 * lane);
-        const uint4 rb0 = *reinterpret_cast<const uint4 *>(rowp + min(wv + NWV * (nci0 > 1 ? 1 : 0), nch - 1) * 256 + 4 * lane);
         // tables: entry e = cls * S1 + x (zone class cls / FamC, family class cls % FamC; the
-        // neutral row cls = ncls).  Thread tid takes e = tid + NT u, two entries at a time with the
-        // LDS reads of both in flight (unconditional, valid indices; selects discard).
+        // neutral row cls = ncls); lane takes e = lane + 64 u, two entries at a time with the LDS
+        // reads of both in flight (unconditional, valid indices; selects discard)
         int wide = 0;
-        int it = 0;
-        for (int e0 = tid; e0 < nent; e0 += 2 * NT, it++) {
+        for (int e0 = lane; e0 < nent; e0 += 2 * WAVE) {
             double to[2], tn[2];
+            uint32_t dcs[2];
+#pragma unroll
+            for (int u = 0; u < 2; u++) dcs[u] = tdl[min(e0 + u * WAVE, nent - 1)];
 #pragma unroll
             for (int u = 0; u < 2; u++) {
-                const int e = min(e0 + u * NT, nent - 1);
-                // the first pass's entries were decomposed once (tdec); later ones divide here
-                uint32_t dc;
-                if (it == 0) dc = tdec[u];
-                else dc = tdecomp(e);
+                const uint32_t dc = dcs[u];
                 const int x = (int)(dc & 0xffu), zcl = (int)((dc >> 8) & 0xffu), fc = (int)((dc >> 16) & 0xffu);
                 const bool real = (dc >> 24) != 0;
                 const bool na = x == S, hz = zcl > 0, hf = fc > 0;
@@ -589,55 +588,62 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             }
 #pragma unroll
             for (int u = 0; u < 2; u++)
-                if (e0 + u * NT < nent) {
-                    tabo[e0 + u * NT] = to[u];
-                    tabn[e0 + u * NT] = tn[u];
+                if (e0 + u * WAVE < nent) {
+                    tabo[e0 + u * WAVE] = to[u];
+                    tabn[e0 + u * WAVE] = tn[u];
                 }
         }
-        const bool wid = block_sum_i(wide) != 0;  // (its barrier publishes the tables)
-        // gathers: position p = 256 k + 4 lane + j of the wave's chunks k = wv + NWV * i, two
-        // chunks (8 positions per lane) at a time, all 16 table reads issued together.  Safe tables
-        // (every factor 0 or within 2^+-120): the 8 factors multiply as a tree, one renormalisation
-        // per pair of chunks; otherwise renormalise after every factor.
+        const bool wid = __ballot(wide != 0) != 0;
+        wsync();  // the wave's table writes are visible to its gathers
+        // gathers: position p = 256 k + 4 lane + j of chunk k, two chunks (8 positions per lane)
+        // at a time, all 16 table reads issued together.  Safe tables (every factor 0 or within
+        // 2^+-120): the 8 factors multiply as a tree, one renormalisation per pair of chunks;
+        // otherwise renormalise after every factor.
         double mn = 1.0, mo = 1.0;
         int en = 0, eo = 0;
-        const int nci = nci0;  // this wave's chunks
         const unsigned char *tbo = reinterpret_cast<const unsigned char *>(tabo);
         const unsigned char *tbn = reinterpret_cast<const unsigned char *>(tabn);
         const uint32_t xsh = a.xs8 ? 0u : 3u;
-        for (int i0 = 0; i0 < nci; i0 += 2) {
-            if (i0 > 0 && (i0 & (OB - 1)) == 0) obs_load(f, i0, o);
-            const bool two = i0 + 1 < nci;
-            const int ka = wv + NWV * i0, kb = wv + NWV * (two ? i0 + 1 : i0);
-            const uint4 ra = i0 == 0 ? ra0 : *reinterpret_cast<const uint4 *>(rowp + ka * 256 + 4 * lane);
-            const uint4 rb = i0 == 0 ? rb0 : *reinterpret_cast<const uint4 *>(rowp + kb * 256 + 4 * lane);
-            const uint32_t oa = (i0 & 2) ? o[2] : o[0], ob = (i0 & 2) ? o[3] : o[1];
-            const uint32_t r8[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
-            double vo[8], vn[8];
+        for (int b0 = 0; b0 < nch; b0 += OBW) {
+            if (b0 > 0) {
 #pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const uint32_t xb = ((j < 4 ? oa : ob) >> (8 * (j & 3))) & 0xffu;
-                const uint32_t ad = r8[j] + (xb << xsh);
-                vo[j] = *reinterpret_cast<const double *>(tbo + ad);
-                vn[j] = *reinterpret_cast<const double *>(tbn + ad);
+                for (int i = 0; i < OBW; i++) o[i] = obs32[fo + (size_t)min(b0 + i, nch - 1) * WAVE + lane];
             }
-            if (!two) {
 #pragma unroll
-                for (int j = 4; j < 8; j++) vo[j] = vn[j] = 1.0;
-            }
-            if (wid) {
+            for (int j = 0; j < OBW; j += 2) {
+                const int i0 = b0 + j;
+                if (i0 >= nch) break;  // uniform
+                const bool two = i0 + 1 < nch;
+                const uint4 ra = *reinterpret_cast<const uint4 *>(rowp + i0 * 256 + 4 * lane);
+                const uint4 rb = *reinterpret_cast<const uint4 *>(rowp + (two ? i0 + 1 : i0) * 256 + 4 * lane);
+                const uint32_t oa = o[j], ob = o[j + 1];
+                const uint32_t r8[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
+                double vo[8], vn[8];
 #pragma unroll
-                for (int j = 0; j < 8; j++) {
-                    mo *= vo[j];
+                for (int q = 0; q < 8; q++) {
+                    const uint32_t xb = ((q < 4 ? oa : ob) >> (8 * (q & 3))) & 0xffu;
+                    const uint32_t ad = r8[q] + (xb << xsh);
+                    vo[q] = *reinterpret_cast<const double *>(tbo + ad);
+                    vn[q] = *reinterpret_cast<const double *>(tbn + ad);
+                }
+                if (!two) {
+#pragma unroll
+                    for (int q = 4; q < 8; q++) vo[q] = vn[q] = 1.0;
+                }
+                if (wid) {
+#pragma unroll
+                    for (int q = 0; q < 8; q++) {
+                        mo *= vo[q];
+                        renorm(mo, eo);
+                        mn *= vn[q];
+                        renorm(mn, en);
+                    }
+                } else {
+                    mo *= ((vo[0] * vo[1]) * (vo[2] * vo[3])) * ((vo[4] * vo[5]) * (vo[6] * vo[7]));
+                    mn *= ((vn[0] * vn[1]) * (vn[2] * vn[3])) * ((vn[4] * vn[5]) * (vn[6] * vn[7]));
                     renorm(mo, eo);
-                    mn *= vn[j];
                     renorm(mn, en);
                 }
-            } else {
-                mo *= ((vo[0] * vo[1]) * (vo[2] * vo[3])) * ((vo[4] * vo[5]) * (vo[6] * vo[7]));
-                mn *= ((vn[0] * vn[1]) * (vn[2] * vn[3])) * ((vn[4] * vn[5]) * (vn[6] * vn[7]));
-                renorm(mo, eo);
-                renorm(mn, en);
             }
         }
 #if SBZ_MH_DLOG
@@ -645,7 +651,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
 #else
         const double r = log(mn / mo) + (double)(en - eo) * LN2;
 #endif
-        return r;
+        return wave_sum(r);
     };
 
     // One MH step per iteration, in four phases with one call site each (keeps the kernel small):
@@ -873,6 +879,37 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
     };
     // per-operator counts: lane op counts operator op's proposals / acceptances (every wave alike)
     int cnt_prop = 0, cnt_acc = 0;
+    // An accepted parameter move on feature f: later plans of the batch on this feature (`later`:
+    // the plan's mask, made when planned; ~0 for a step that was not planned) take the new values
+    // in their columns (wave 0 writes, a barrier publishes them); a plan whose proposal read the
+    // altered row (same component and row), or whose weights changed, is stale and recomputed when
+    // reached.
+    auto patch_later = [&](int pk_, uint32_t later, int comp_, int row_, int f_, int ia_, int ib_, double nv0_,
+                           double nv1_) {
+        if (later == 0) return;
+        const int k = min(lane, LA - 1);
+        const bool in = lane < LAe && lane > pk_ && ((later >> k) & 1u) && pl->comp[k] >= 0 && pl->f[k] == f_;
+        const int cb = comp_ == 3 ? (1 + Z + Fam) * S : (comp_ == 0 ? 0 : (comp_ == 1 ? (1 + row_) * S : (1 + Z + row_) * S));
+        if (wv == 0 && in) {
+            plcol[k * ncol + cb + ia_] = nv0_;
+            plcol[k * ncol + cb + ib_] = nv1_;
+        }
+        if (in && (comp_ == 3 || (pl->comp[k] == comp_ && pl->row[k] == row_))) okw[k] = 0;
+        if (__ballot(in) != 0) bsync();  // the same ballot in every wave
+    };
+    auto trace_step = [&](int st, int op_, bool acc) {
+        if (ch.trace_op && tid == 0) {
+            const size_t t = (size_t)b * a.n_steps + st;
+            ch.trace_op[t] = (int8_t)op_;
+            ch.trace_accept[t] = acc ? 1 : 0;
+            ch.trace_ll[t] = ll;
+        }
+        if (ch.trace_zos) {
+            uint8_t *tz = ch.trace_zos + ((size_t)b * a.n_steps + st) * N;
+            for (int s = tid; s < N; s += NT) tz[s] = zos[s];
+        }
+    };
+    int gsl = 0;  // gdl slot of the next group
     for (int step = 0; step < a.n_steps; step++) {
         if (rng.bad || broken) break;
         if (philox) rng.ctr = ctr0 + (uint64_t)step * WIN;
@@ -880,35 +917,86 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             fence_params();
             make_plans(step);
         }
-#ifdef SBZ_MH_MARK
-        asm volatile("; PH1_BEGIN");
-#endif
         const int pk = step - plan_t0;  // this step's plan (Philox, LAe > 1)
         // the plan's fields, read in one batch (one LDS round trip)
-        int p_ok = 0, p_op = 0, p_comp = 0, p_row = 0, p_f = 0, p_ia = 0, p_ib = 0, p_off = 0;
-        uint32_t p_fm = 0;
-        double p_nv0 = 0.0, p_nv1 = 0.0, p_lq = 0.0, p_lqb = 0.0, p_dp = 0.0, p_lu = 0.0;
+        int p_ok = 0, p_op = 0, p_comp = -1;
+        double p_lu = 0.0;
+        int nx_ok[MAX_NWV], nx_comp[MAX_NWV];
+        uint32_t nx_fm[MAX_NWV];
         if (philox && LAe > 1) {
             p_ok = okw[pk];
             p_op = pl->op[pk];
             p_comp = pl->comp[pk];
-            p_row = pl->row[pk];
-            p_f = pl->f[pk];
-            p_ia = pl->ia[pk];
-            p_ib = pl->ib[pk];
-            p_off = pl->off[pk];
-            p_fm = pl->fm[pk];
-            p_nv0 = pl->nv0[pk];
-            p_nv1 = pl->nv1[pk];
-            p_lq = pl->lq[pk];
-            p_lqb = pl->lqb[pk];
-            p_dp = pl->dprior[pk];
             p_lu = pl->lu[pk];
+#pragma unroll
+            for (int k = 0; k < NWV; k++) {
+                const int q = min(pk + k, LA - 1);
+                nx_ok[k] = okw[q];
+                nx_comp[k] = pl->comp[q];
+                nx_fm[k] = pl->fm[q];
+            }
         }
-#ifdef SBZ_MH_MARK
-        asm volatile("; PH1_READ");
-#endif
         const bool planned = philox && LAe > 1 && uni(p_ok) != 0;
+        if (planned && uni(p_comp) >= 0) {
+            // ---- grouped planned parameter moves: this step and the next planned, valid parameter
+            // moves of the batch whose features differ pairwise (at most NWV).  Each changes only
+            // its own feature's cells, so their deltas do not depend on each other's outcome: wave k
+            // computes member k's delta, then every wave takes the members' decisions in step order
+            // (the trajectory is the one-step-at-a-time trajectory: test_gpu_sampler.py)
+            int g = 1;
+            uint32_t fmacc = (uint32_t)uni((int)nx_fm[0]);
+#pragma unroll
+            for (int k = 1; k < NWV; k++) {
+                const int q = pk + k;
+                const bool more = g == k && k < a.ntab && step + k < a.n_steps && q < LAe && uni(nx_ok[k]) != 0 &&
+                                  uni(nx_comp[k]) >= 0 && !((fmacc >> q) & 1u);
+                if (more) {
+                    fmacc |= (uint32_t)uni((int)nx_fm[k]);
+                    g++;
+                }
+            }
+            double *gslot = gdl + gsl * 8;
+            gsl ^= 1;  // a slot is rewritten only after every wave passed the next group's barrier
+            const int wvu = uni(wv);
+            if (wvu < g) {
+                const int q = pk + wvu;
+                const double d = delta_param(plcol + q * ncol, plnw + q * 32, uni(pl->f[q]), uni(pl->comp[q]),
+                                             uni(pl->row[q]), uni(pl->ia[q]), uni(pl->ib[q]), uni(pl->nv0[q]),
+                                             uni(pl->nv1[q]));
+                if (lane == 0) gslot[wvu] = d;
+            }
+            bsync();
+            for (int k = 0; k < g; k++) {
+                const int q = pk + k;
+                const int op_k = uni(pl->op[q]), comp_k = uni(pl->comp[q]), row_k = uni(pl->row[q]);
+                const int f_k = uni(pl->f[q]), ia_k = uni(pl->ia[q]), ib_k = uni(pl->ib[q]), off_k = uni(pl->off[q]);
+                const uint32_t fm_k = (uint32_t)uni((int)pl->fm[q]);
+                const double nv0_k = uni(pl->nv0[q]), nv1_k = uni(pl->nv1[q]), lq_k = uni(pl->lq[q]);
+                const double lqb_k = uni(pl->lqb[q]), dp_k = uni(pl->dprior[q]), lu_k = uni(pl->lu[q]);
+                const double delta_k = uni(gslot[k]);
+                // metropolis_hastings_ratio (mcmc_generative.py:331-351), as the sequential path
+                bool acc;
+                if (lqb_k == -INFINITY) acc = false;
+                else if (lq_k == -INFINITY) acc = true;
+                else acc = lu_k < (delta_k * 1.0) - (lq_k - lqb_k) + dp_k;
+                cnt_prop += lane == op_k ? 1 : 0;
+                if (acc) {
+                    cnt_acc += lane == op_k ? 1 : 0;
+                    ll = ll + delta_k;
+                    prior = prior + dp_k;
+                    double *bs = (comp_k == 3 ? w : (comp_k == 0 ? pg : (comp_k == 1 ? pz : pf))) + off_k;
+                    if (tid == 0) {
+                        stp(bs + ia_k, nv0_k);
+                        stp(bs + ib_k, nv1_k);
+                    }
+                    store_pending = true;
+                    patch_later(q, fm_k, comp_k, row_k, f_k, ia_k, ib_k, nv0_k, nv1_k);
+                }
+                trace_step(step + k, op_k, acc);
+            }
+            step += g - 1;
+            continue;
+        }
         const int op = planned ? uni(p_op) : rng.op(a.op_cdf, a.nops);
         if (op < 0 || op > GIBBSISH || (op == P_FAMILIES && (C == 2 || Fam == 0)) ||
             ((op <= SWAP || op == GIBBSISH) && Z == 0) || (op == P_ZONES && Z == 0)) {
@@ -1119,14 +1207,6 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                     }
                 }
             }
-        } else if (planned) {
-            // checked when planned (make_plans stage A; an invalid move is never planned)
-            comp = uni(p_comp);
-            row = uni(p_row);
-            f = uni(p_f);
-            ia = uni(p_ia);
-            ib = uni(p_ib);
-            base = (comp == 3 ? w : (comp == 0 ? pg : (comp == 1 ? pz : pf))) + uni(p_off);
         } else {
             if (op == WEIGHTS) {
                 f = rng.below(F);
@@ -1165,26 +1245,14 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             poff = off;
         }
 
-#ifdef SBZ_MH_MARK
-        asm volatile("; PH1_END");
-#endif
         // ---- 2. Dirichlet proposal of the pair (zone_sampling.py:421-438, :537-569)
-        if (!(planned && comp >= 0)) fence_params();  // planned steps read no parameters from HBM
+        fence_params();  // (planned parameter moves took the grouped path above)
         double nv0 = 0.0, nv1 = 0.0;
         double cv[NCV];
-        uint32_t ow[OB];
-        if (comp >= 0 && planned) {
-            obs_load(f, 0, ow);
-            nv0 = uni(p_nv0);
-            nv1 = uni(p_nv1);
-            log_q = uni(p_lq);
-            log_q_back = uni(p_lqb);
-            dprior = uni(p_dp);
-        } else if (comp >= 0) {
+        if (comp >= 0) {
             const double c0 = uni(ldp(base + ia)), c1 = uni(ldp(base + ib));
-            // the move's column and observations: in flight during the proposal math
+            // the move's column: in flight during the proposal math
             col_load(f, cv);
-            obs_load(f, 0, ow);
             // without inheritance the weight pair is used as is (zone_sampling.py:440-443)
             const bool raw = C == 2 && comp == 3;
             const double sum = raw ? 1.0 : c0 + c1;
@@ -1214,10 +1282,13 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                 part = delta_site(sa, zoa, zna);
                 if (sb >= 0) part = part + delta_site(sb, zna, NONE);
             } else if (comp >= 0) {
-                // a planned step's column and weights are in plcol / plnw; otherwise staged here
-                if (!planned) col_store(f, cv);
-                part = delta_param(planned ? plcol + pk * ncol : col, planned ? plnw + pk * 32 : nullptr, f, comp,
-                                   row, ia, ib, nv0, nv1, ow);
+                // the column staged here; wave 0 computes the delta as a grouped move's wave would,
+                // and the block sum below adds zeros to it (exact)
+                col_store(f, cv);
+                if (uni(wv) == 0) {
+                    const double d = delta_param(col, nullptr, f, comp, row, ia, ib, nv0, nv1);
+                    part = lane == 0 ? d : 0.0;
+                }
             }
             int n_err = 0;
             delta = block_sum_di(part, err != 0 ? 1 : 0, n_err);
@@ -1293,23 +1364,8 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                     stp(base + ib, nv1);
                 }
                 store_pending = true;
-                // later plans of the batch on this feature (p_fm, made when planned; a step that is
-                // not planned compares them here): their columns take the new values (wave 0
-                // writes, a barrier publishes them); a plan whose proposal read the altered row
-                // (same component and row), or whose weights changed, is stale and recomputed when
-                // reached
-                const uint32_t later = !philox || LAe <= 1 ? 0u : planned ? (uint32_t)uni((int)p_fm) : ~0u;
-                if (later != 0) {
-                    const int k = min(lane, LA - 1);
-                    const bool in = lane < LAe && lane > pk && ((later >> k) & 1u) && pl->comp[k] >= 0 && pl->f[k] == f;
-                    const int cb = comp == 3 ? (1 + Z + Fam) * S : (comp == 0 ? 0 : (comp == 1 ? (1 + row) * S : (1 + Z + row) * S));
-                    if (wv == 0 && in) {
-                        plcol[k * ncol + cb + ia] = nv0;
-                        plcol[k * ncol + cb + ib] = nv1;
-                    }
-                    if (in && (comp == 3 || (pl->comp[k] == comp && pl->row[k] == row))) okw[k] = 0;
-                    if (__ballot(in) != 0) bsync();  // the same ballot in every wave
-                }
+                // (a step that was not planned compares every later plan)
+                patch_later(pk, !philox || LAe <= 1 ? 0u : ~0u, comp, row, f, ia, ib, nv0, nv1);
             }
         }
         if (gtent && !accept) {  // restore the assignment the proposal overwrote
@@ -1317,16 +1373,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                 zos[lst[k]] = (gib_fl[k] & 2) ? (uint8_t)gz : (uint8_t)NONE;
             bsync();
         }
-        if (ch.trace_op && tid == 0) {
-            const size_t t = (size_t)b * a.n_steps + step;
-            ch.trace_op[t] = (int8_t)op;
-            ch.trace_accept[t] = accept ? 1 : 0;
-            ch.trace_ll[t] = ll;
-        }
-        if (ch.trace_zos) {
-            uint8_t *tz = ch.trace_zos + ((size_t)b * a.n_steps + step) * N;
-            for (int s = tid; s < N; s += NT) tz[s] = zos[s];
-        }
+        trace_step(step, op, accept);
     }
 
     bsync();
@@ -1473,16 +1520,22 @@ int launch_mh(sbz_ctx *ctx, int B, int n_steps, const sbz_mh_config *cfg, const 
     const bool geo = a.geo_cost != nullptr;
     if (mh_lds_bytes(d, ctx->C, geo, a.gib != 0) > 160 * 1024)
         return fail(ctx, SBZ_EINVAL, "sampler state exceeds the 160 KiB of LDS (too many sites)");
-    // planned steps per batch (Philox only): as many as SBZ_MH_LA asks whose columns fit the LDS
-    auto lds_of = [&](int la) {
+    // planned steps per batch (Philox only): as many as SBZ_MH_LA asks whose columns fit the LDS,
+    // and table slots for grouped parameter moves (one per wave): the most slots that leave room
+    // for min(8, asked) planned steps, then the most planned steps beside them
+    auto lds_of = [&](int la, int nt) {
         return MhLayout(d.n_sites, np_of(d.n_sites), d.n_states, d.n_zones, d.n_families, ctx->C, ctx->FamC,
-                        MH_WAVES * WAVE, geo, la, a.gib != 0).total;
+                        MH_WAVES * WAVE, geo, la, a.gib != 0, nt).total;
     };
     constexpr size_t LDS_MAX = 160 * 1024;
-    int la = a.ch.tape ? 1 : std::min(ctx->mh_la, LA);
-    while (la > 1 && lds_of(la) > LDS_MAX) la--;
+    const int la_ask = a.ch.tape ? 1 : std::min(ctx->mh_la, LA);
+    int ntab = la_ask > 1 ? std::min(MH_WAVES, ctx->mh_group) : 1;  // groups need plans
+    while (ntab > 1 && lds_of(std::min(la_ask, 8), ntab) > LDS_MAX) ntab--;
+    int la = la_ask;
+    while (la > 1 && lds_of(la, ntab) > LDS_MAX) la--;
     a.la = la;
-    const size_t lds = lds_of(la);
+    a.ntab = ntab;
+    const size_t lds = lds_of(la, ntab);
     auto fn = ctx->C == 3 ? mh_kernel<3, MH_WAVES> : mh_kernel<2, MH_WAVES>;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn),

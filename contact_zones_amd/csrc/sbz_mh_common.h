@@ -544,6 +544,8 @@ struct MhArgs {
     int n_steps, nops, min_size, warmup;
     int la;     // mh_kernel, Philox draws: proposals planned ahead per batch (1 = none; <= LA = 24;
                 // the host lowers it until the plan columns fit the 160 KiB of LDS)
+    int ntab;   // mh_kernel: per-wave cell-table slots (1 .. waves): planned parameter moves on
+                // different features computed at once, at most ntab (the host fits it to the LDS)
     int stage;  // mh_src_kernel: parameters and normalised weights staged in LDS for the N*F passes
     int cstage; // mh_src_kernel (with stage): the constant tables (applicable states, Gibbs prior
                 //   counts, 'counts' prior) staged in LDS too

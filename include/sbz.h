@@ -116,7 +116,12 @@ int sbz_synchronize(sbz_ctx *ctx);
  *   SBZ_OPT_SRC_PASS_TABLES   1 (default): the source-mode sampler with its sources in HBM runs its
  *                             passes over the observations on per-feature tables and keeps per-chain
  *                             source counts, so the Gibbs parameter operators need no pass (where the
- *                             tables fit: 4 or 8 waves, Np <= 4 x threads); 0: per-cell passes
+ *                             tables fit: 4 or 8 waves, Np <= 2048, table lines and count-table
+ *                             columns <= 192, and the LDS holds them); 0: per-cell passes
+ *   SBZ_OPT_MH_GROUP          mixture sampler with Philox draws: planned parameter moves on pairwise
+ *                             different features whose deltas are computed at once, one per wave,
+ *                             1..4 (default 4; fewer when the per-wave cell tables do not fit the
+ *                             LDS; trajectories do not depend on it)
  * SBZ_EINVAL for an unknown option or a value out of range. */
 enum sbz_option {
     SBZ_OPT_LIK_TASKS_PER_CU = 1,
@@ -127,6 +132,7 @@ enum sbz_option {
     SBZ_OPT_SRC_STAGE = 6,
     SBZ_OPT_MH_LOOKAHEAD = 7,
     SBZ_OPT_SRC_PASS_TABLES = 8,
+    SBZ_OPT_MH_GROUP = 9,
 };
 int sbz_set_option(sbz_ctx *ctx, int32_t option, int64_t value);
 int sbz_get_option(const sbz_ctx *ctx, int32_t option, int64_t *value);

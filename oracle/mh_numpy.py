@@ -70,12 +70,21 @@ class TapeReader:
         self.pos += n
         return np.asarray(v, np.float64)
 
+    def beta(self, a, b):
+        """stats.beta(a, b).rvs() per entry (the Gibbs weights draw)."""
+        return self.reals(np.size(a))
+
+    def dirichlet_vec(self, alpha):
+        """np.random.dirichlet(alpha) over a feature's applicable states (the Gibbs p_* draws)."""
+        return self.reals(np.size(alpha))
+
 
 class DrawTape(TapeReader):
     """The decisions drawn from a numpy Generator instead of a tape (the reference's distributions:
     np.random.choice of the operator by its probability, uniform ints, random.sample pairs,
     np.random.dirichlet proposals, uniform reals) — the CPU baseline's sampler (bench.py), no
-    replay.  SAMPLE_SOURCE = false operators only."""
+    replay.  In SAMPLE_SOURCE = true mode the Gibbs operators draw from the reference's
+    distributions too (beta / Dirichlet of the source counts)."""
 
     def __init__(self, rng, op_probs):
         self.rng = rng
@@ -99,6 +108,12 @@ class DrawTape(TapeReader):
 
     def reals(self, n):
         return self.rng.random(n)
+
+    def beta(self, a, b):
+        return self.rng.beta(a, b)
+
+    def dirichlet_vec(self, alpha):
+        return self.rng.dirichlet(alpha)
 
 
 def geo_prior_distance(zone, cost, scale):
@@ -469,14 +484,16 @@ def op_gibbs_weights(m, st, c, tape):
     if not m.inheritance:
         counts = _source_counts(m, st, has_area)
         for f in range(F):
-            w_new[f, :] = tape.reals(2)  # np.random.dirichlet(1 + counts[f])
+            w_new[f, :] = tape.dirichlet_vec(1 + counts[f])  # np.random.dirichlet(1 + counts[f])
         return dict(st, w=w_new), -np.inf, 0
-    fixed = ["inheritance", "contact"][tape.int()]
+    fixed = ["inheritance", "contact"][tape.int(2)]
     if fixed == "inheritance":
-        a = tape.reals(F)                # stats.beta(1 + c_contact, 1 + c_univ).rvs()
+        counts = _source_counts(m, st, has_area)
+        a = tape.beta(1 + counts[..., 1], 1 + counts[..., 0])  # stats.beta(1 + c_contact, 1 + c_univ).rvs()
         w_new[..., 1] = a * w[..., 0] / (1 - a)
     else:
-        a = tape.reals(F)                # stats.beta(1 + c_inherit, 1 + c_univ).rvs()
+        counts = _source_counts(m, st, np.any(m.families, axis=0) if m.families is not None else has_area)
+        a = tape.beta(1 + counts[..., 2], 1 + counts[..., 0])  # stats.beta(1 + c_inherit, 1 + c_univ).rvs()
         w_new[..., 2] = a * w[..., 0] / (1 - a)
     w_new = normalize(w_new)
     tape.reals(F)                        # np.random.random(F) < p_accept (overridden)
@@ -490,8 +507,17 @@ def normalize(x, axis=-1):
 def _gibbs_p(tape, p_row, prior_counts, counts, idx):
     """p[idx] = np.random.dirichlet(prior_counts[idx] + counts) (value from the tape)."""
     p_row = p_row.copy()
-    p_row[idx] = tape.reals(idx.size)
+    p_row[idx] = tape.dirichlet_vec(prior_counts[idx] + counts)
     return p_row
+
+
+def _state_counts(m, st, comp, f, idx, sites=None):
+    """np.nansum(features[:, f, idx] where source == comp (and the site in `sites`), axis=0)
+    (zone_sampling.py:341-352, :366-373, :390-401)."""
+    sel = st["src"][:, f] == comp
+    if sites is not None:
+        sel = sel & sites
+    return np.sum(m.features[sel][:, f, idx], axis=0)
 
 
 def op_gibbs_p_global(m, st, c, tape, fraction_of_features=0.4):
@@ -501,29 +527,31 @@ def op_gibbs_p_global(m, st, c, tape, fraction_of_features=0.4):
     pg = st["pg"].copy()
     for f in np.flatnonzero(subset):
         idx = np.flatnonzero(m.states[f])
-        pg[f] = _gibbs_p(tape, pg[f], None, None, idx)
+        pg[f] = _gibbs_p(tape, pg[f], m.gibbs_counts_global[f], _state_counts(m, st, 0, f, idx), idx)
     return dict(st, pg=pg), -np.inf, 0
 
 
 def op_gibbs_p_zones(m, st, c, tape):
     """gibbs_sample_p_zones (zone_sampling.py:359-379)."""
-    z = tape.int()  # np.random.randint(0, n_zones)
+    z = tape.int(m.n_zones)  # np.random.randint(0, n_zones)
     pz = st["pz"].copy()
+    ones = np.ones(m.states.shape[1])
     for f in range(pz.shape[1]):
         idx = np.flatnonzero(m.states[f])
-        pz[z, f] = _gibbs_p(tape, pz[z, f], None, None, idx)
+        pz[z, f] = _gibbs_p(tape, pz[z, f], ones, _state_counts(m, st, 1, f, idx, st["zos"] == z), idx)
     return dict(st, pz=pz), -np.inf, 0
 
 
 def op_gibbs_p_families(m, st, c, tape, fraction_of_features=0.4):
     """gibbs_sample_p_families (zone_sampling.py:381-406)."""
-    fam = tape.int()  # np.random.randint(0, n_families)
+    fam = tape.int(st["pf"].shape[0])  # np.random.randint(0, n_families)
     F = st["pf"].shape[1]
     subset = tape.reals(F) < fraction_of_features
     pf = st["pf"].copy()
     for f in np.flatnonzero(subset):
         idx = np.flatnonzero(m.states[f])
-        pf[fam, f] = _gibbs_p(tape, pf[fam, f], None, None, idx)
+        pf[fam, f] = _gibbs_p(tape, pf[fam, f], m.gibbs_counts_fam[fam, f],
+                              _state_counts(m, st, 2, f, idx, m.fam == fam), idx)
     return dict(st, pf=pf), -np.inf, 0
 
 

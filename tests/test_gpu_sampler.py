@@ -248,14 +248,15 @@ def test_host_form_philox_matches_device_form(gpu_available):
 @pytest.mark.parametrize("case", ["mh_small_priors", "mh_cfg1_sim_inh_z2", "mh_small_bounds"])
 def test_philox_planned_proposals_do_not_change_trajectories(gpu_available, case):
     """Philox mode plans the proposals of the next parameter moves in parallel lanes (option
-    mh_lookahead steps at a time) and recomputes a plan that an accepted move made stale: the
+    mh_lookahead steps at a time), computes the deltas of up to mh_group planned moves on different
+    features at once (one per wave) and recomputes a plan that an accepted move made stale: the
     trajectory (operators, accepts, ll, final state, counters) is bit-identical to the
     one-step-at-a-time path (mh_lookahead = 1), over launches of different lengths."""
     import torch
     fx = load_golden(case)
     runs = []
-    for la in (1, 24, 6):
-        eng, smp, st = _setup(fx, {"mh_lookahead": la})
+    for la, grp in ((1, 4), (24, 4), (6, 4), (24, 1), (24, 2), (6, 3)):
+        eng, smp, st = _setup(fx, {"mh_lookahead": la, "mh_group": grp})
         outs = [smp.run(st, n, fx["max_size"], fx["p_grow_connected"], seed=4242, chain_id0=3, trace=True)
                 for n in (700, 5, 1301)]
         torch.cuda.synchronize()
@@ -274,9 +275,10 @@ def test_philox_planned_proposals_do_not_change_trajectories(gpu_available, case
 
 
 def test_planned_batches_cut_by_lds(gpu_available):
-    """Wide parameter columns (S = 60, Z = 6, Fam = 4: 663 doubles per planned step) leave room
-    in the 160 KiB for fewer than 24 planned steps (about 20 here): the host cuts the batch, and
-    the trajectory stays bit-identical to the one-step-at-a-time path."""
+    """Wide parameter columns (S = 60, Z = 6, Fam = 4: 663 doubles per planned step, 35 KB of cell
+    tables per wave) leave room in the 160 KiB for fewer than 24 planned steps and fewer than 4
+    table slots (2 here): the host cuts both, and the trajectory stays bit-identical to the
+    one-step-at-a-time path."""
     import torch
     runs = []
     for la in (1, 24):

@@ -43,13 +43,14 @@ def main():
     ap.add_argument("--stamps", action="store_true",
                     help="library built with SBZ_MH_STAMP: report mean phase cycles per operator")
     ap.add_argument("--sets", default=",".join(SETS), help="comma-separated operator sets")
+    ap.add_argument("--options", default="{}", help="JSON context options, e.g. {\"mh_group\": 1}")
     a = ap.parse_args()
     N, F, S, Z, Fam, B = a.sites, a.features, a.states, a.zones, a.families, a.chains
     rng = np.random.default_rng(5)
     obs = rng.integers(0, S, size=(N, F)).astype(np.int8)
     obs[rng.random((N, F)) < 0.02] = -1
     fam = rng.integers(0, Fam, size=N).astype(np.uint8)
-    eng = LikelihoodEngine(obs, fam, S, Z, Fam, True, device=0)
+    eng = LikelihoodEngine(obs, fam, S, Z, Fam, True, device=0, options=json.loads(a.options) or None)
     indptr, indices = bench.make_network(N, np.random.default_rng(22))
     states = np.ones((F, S), bool)
     init = InitialSamples(packing.obs_to_features(obs, S), states, indptr, indices,
