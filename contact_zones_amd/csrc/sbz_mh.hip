@@ -79,7 +79,7 @@ struct Plans {
 // c (CH = NT * KT sites per chunk, nsc chunks); zos / nb / lst are padded to NpS = nsc * CH.
 struct MhLayout {
     int KT, CH, nsc, NpS, nent, ncol;
-    uint32_t col, zsize, red, nb, zos, selc, lst, wtab, wnw, tdl, gdl, rowp, ipos, plans, plcol,
+    uint32_t col, zsize, red, nb, zos, selc, lst, wtab, wnw, tdl, gdl, fpr, rowp, ipos, plans, plcol,
         plnw, geo, gib;
     size_t total;
     __host__ __device__ MhLayout(int N, int Np, int S, int Z, int Fam, int C, int FamC, int NT,
@@ -104,14 +104,15 @@ struct MhLayout {
         zos = take((size_t)NpS);
         selc = take((size_t)nsc * 16 * 4);  // per chunk: selected sites per wave of the last scan
         lst = take((size_t)NpS * 2);
-        // a parameter move's cell tables, one pair per table slot (old cells, new cells; 1 where
-        // the move changes nothing; ntab slots, one per wave of a group), its normalised weights
-        // [NWV][2][4][4], the entries decomposed once (tdl), and the grouped moves' deltas (two
-        // slots of 8)
+        // a parameter move's cell-ratio tables, per table slot (ntab, one per wave of a group) a
+        // dense one (weights moves) and a sparse one (1.0 but the changed entries), its normalised
+        // weights [NWV][2][4][4], the entries decomposed once (tdl), the grouped moves' deltas
+        // (two slots of 8), each family class's position range [FamC][2]
         wtab = take((size_t)ntab * 2 * nent * 8);
         wnw = take((size_t)(NT / 64) * 32 * 8);
         tdl = take((size_t)nent * 4);
         gdl = take(16 * 8);
+        fpr = take((size_t)FamC * 8);
         rowp = take((size_t)Np * 4);
         ipos = take((size_t)N * 2);
         // geo prior scratch (geo_zone_prior): key [N] doubles, mem [N] u16, cnt + redd / redi [16]
@@ -166,6 +167,7 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
     double *wnw = reinterpret_cast<double *>(lds + L.wnw);       // [NWV][2][4][4] normalised weights
     uint32_t *tdl = reinterpret_cast<uint32_t *>(lds + L.tdl);   // [nent] decomposed entries
     double *gdl = reinterpret_cast<double *>(lds + L.gdl);       // [2][8] grouped moves' deltas
+    int *fpr = reinterpret_cast<int *>(lds + L.fpr);             // [FamC][2] positions of each family class
     uint32_t *rowp = reinterpret_cast<uint32_t *>(lds + L.rowp); // [Np] table row (bytes) by position
     uint16_t *ipos = reinterpret_cast<uint16_t *>(lds + L.ipos); // [N] position of each site
     double *plcol = reinterpret_cast<double *>(lds + L.plcol);  // [la][ncol] planned steps' columns
@@ -519,47 +521,91 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
         return (uint32_t)x | ((uint32_t)zcl << 8) | ((uint32_t)fc << 16) | ((real ? 1u : 0u) << 24);
     };
     for (int e = tid; e < nent; e += NT) tdl[e] = tdecomp(e);
+    for (int e = tid; e < a.ntab * nent; e += NT) wtab[(e / nent) * 2 * nent + nent + e % nent] = 1.0;  // sparse
+    for (int c = tid; c < 2 * FamC; c += NT) fpr[c] = 0;
+    bsync();
+    // family class c occupies positions [fpr[2c], fpr[2c + 1]) (sites sorted by class, sbz_open)
+    for (int p = tid; p < N; p += NT) {
+        const int c = C == 3 ? (int)a.famc[p] : 0;
+        if (p == 0 || (C == 3 && (int)a.famc[p - 1] != c)) fpr[2 * c] = p;
+        if (p == N - 1 || (C == 3 && (int)a.famc[p + 1] != c)) fpr[2 * c + 1] = p + 1;
+    }
     bsync();
     // Delta of a parameter move, computed by ONE wave (the calling wave; every lane of it gets the
-    // value).  Parameter moves on different features change disjoint cells, so up to NWV planned
+    // value).  Parameter moves on different features change disjoint cells, so up to ntab planned
     // moves of a batch get their deltas at once, one per wave (the step loop's grouped path), and
     // an unplanned move is computed the same way by wave 0: the value of a move's delta does not
     // depend on how the steps were grouped or planned.  `cl` is feature f's column in LDS (the
     // staged col, or a planned step's column) and `nwp` its normalised weights before
     // (nwp[0..15]) and after (nwp[16..31]) the move, or null: computed here into the wave's wnw.
-    // A cell's value depends only on (zone class, family class, x), so the wave builds two tables
-    // for feature f in its own LDS slice — the reference cell before and after the move for every
-    // (class, x) whose value the move changes, 1.0 for every other entry — and each position then
-    // multiplies one factor from each (its row offset in rowp, its observation byte), with no
-    // per-site tests.  The changed entries are exactly the cells the reference recomputes: every
-    // cell for the weights, state ia / ib of the component's rows otherwise (NA cells do not change).
+    // A cell's value depends only on (zone class, family class, x), so the wave writes one table
+    // for feature f in its own LDS slot — new cell / old cell for every (class, x) whose value the
+    // move changes (the reference's cells, model.py:436-452, 174-176), 1.0 for every other entry —
+    // and each position multiplies the entry of its class row (rowp) and observation byte.  The
+    // changed entries are exactly the cells the reference recomputes: every cell for the weights
+    // (the slot's dense table, rewritten whole), states ia / ib of the component's rows otherwise
+    // (the slot's sparse table, 1.0 everywhere else: only the 2 x rows changed entries are written,
+    // and reset to 1.0 after the gathers).  A sparse move reads only the positions its entries can
+    // apply to (state ia / ib; the zone's rows for p_zones; the family's position range for
+    // p_families, families being contiguous in the position order); the others multiply 1.
+#ifdef SBZ_MH_STAMP
+    double stamp_dp = 0.0;  // phase cycles of the last delta_param (SBZ_MH_STAMP 4 / 5 / 6)
+#endif
     constexpr int OBW = 8;  // observation words (chunks of 256 positions) in flight per lane
     const int nch = a.Np / 256;
     const uint32_t *obs32 = reinterpret_cast<const uint32_t *>(a.obs_fm);
     auto delta_param = [&](const double *cl, const double *nwp, int f, int comp, int row, int ia, int ib,
                            double va, double vb) -> double {
+#ifdef SBZ_MH_STAMP
+        const long long dt_start = clock64();
+#endif
         const int wvu = uni(wv);
-        double *tabo = wtab + (size_t)wvu * 2 * nent, *tabn = tabo + nent;
+        const bool dense = comp == 3;
+        double *tab = wtab + (size_t)wvu * 2 * nent + (dense ? 0 : nent);
+        // positions the move's entries can apply to: [p_lo, p_hi) (a family's range for p_families)
+        // and class rows [c_lo, c_lo + c_span) (bytes; the zone's rows for p_zones)
+        int p_lo = 0, p_hi = a.Np;
+        uint32_t c_lo = 0, c_span = (uint32_t)(ncls * row_bytes);
+        if (comp == 2) {
+            p_lo = uni(fpr[2 * (row + 1)]);
+            p_hi = uni(fpr[2 * (row + 1) + 1]);
+        } else if (comp == 1) {
+            c_lo = (uint32_t)((row + 1) * FamC * row_bytes);
+            c_span = (uint32_t)(FamC * row_bytes);
+        }
+        const int k_lo = p_lo / 256, k_hi = p_hi > p_lo ? (p_hi + 255) / 256 : k_lo;  // chunks
         // the feature's observation words, all in flight during the table build
         const size_t fo = (size_t)MH_IDX(f, F, 13) * (size_t)(a.Np / 4);
         uint32_t o[OBW];
 #pragma unroll
-        for (int i = 0; i < OBW; i++) o[i] = obs32[fo + (size_t)min(i, nch - 1) * WAVE + lane];
+        for (int i = 0; i < OBW; i++) o[i] = obs32[fo + (size_t)min(k_lo + i, nch - 1) * WAVE + lane];
         if (!nwp) {
             double *own = wnw + wvu * 32;
             if (lane < 8) norm_w(cl + (1 + Z + Fam) * S, comp, ia, ib, va, vb, lane & 3, lane >> 2, own + lane * 4);
             wsync();
             nwp = own;
         }
-        // tables: entry e = cls * S1 + x (zone class cls / FamC, family class cls % FamC; the
-        // neutral row cls = ncls); lane takes e = lane + 64 u, two entries at a time with the LDS
-        // reads of both in flight (unconditional, valid indices; selects discard)
+        // the changed entries: dense, every entry e; sparse, entry i of the move's list (state ia /
+        // ib of every class row (p_global), of the zone's rows (p_zones), of the family's rows
+        // (p_families)); lane takes i = lane + 64 u, two at a time with the LDS reads of both in
+        // flight (unconditional, valid indices; selects discard)
+        const int n_chg = dense ? nent : (comp == 0 ? 2 * ncls : (comp == 1 ? 2 * FamC : 2 * (Z + 1)));
+        auto entry_of = [&](int i) -> int {
+            if (dense) return i;
+            const int x = (i & 1) ? ib : ia, j = i >> 1;
+            const int cls = comp == 0 ? j : (comp == 1 ? (row + 1) * FamC + j : j * FamC + row + 1);
+            return cls * S1 + x;
+        };
         int wide = 0;
-        for (int e0 = lane; e0 < nent; e0 += 2 * WAVE) {
-            double to[2], tn[2];
+        for (int i0 = lane; i0 < n_chg; i0 += 2 * WAVE) {
+            double rt[2];
+            int es[2];
             uint32_t dcs[2];
 #pragma unroll
-            for (int u = 0; u < 2; u++) dcs[u] = tdl[min(e0 + u * WAVE, nent - 1)];
+            for (int u = 0; u < 2; u++) {
+                es[u] = entry_of(min(i0 + u * WAVE, n_chg - 1));
+                dcs[u] = tdl[es[u]];
+            }
 #pragma unroll
             for (int u = 0; u < 2; u++) {
                 const uint32_t dc = dcs[u];
@@ -582,76 +628,91 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                 const double wold[3] = {wo[0], wo[1], wo[2]}, wnew[3] = {wn[0], wn[1], wn[2]};
                 const double vo = cell_nw<C>(wold, hz, hf, na, l0, l1, l2);
                 const double vn = cell_nw<C>(wnew, hz, hf, na, n0, n1, n2);
-                to[u] = changed ? vo : 1.0;
-                tn[u] = changed ? vn : 1.0;
-                wide |= !(safe_cell(to[u]) && safe_cell(tn[u])) ? 1 : 0;
+                rt[u] = changed ? vn / vo : 1.0;
+                wide |= !(rt[u] >= 0x1p-120 && rt[u] <= 0x1p120) ? 1 : 0;  // (NaN: wide)
             }
 #pragma unroll
             for (int u = 0; u < 2; u++)
-                if (e0 + u * WAVE < nent) {
-                    tabo[e0 + u * WAVE] = to[u];
-                    tabn[e0 + u * WAVE] = tn[u];
-                }
+                if (i0 + u * WAVE < n_chg) tab[es[u]] = rt[u];
         }
         const bool wid = __ballot(wide != 0) != 0;
         wsync();  // the wave's table writes are visible to its gathers
+#ifdef SBZ_MH_STAMP
+        const long long dt_tb = clock64();
+#endif
         // gathers: position p = 256 k + 4 lane + j of chunk k, two chunks (8 positions per lane)
-        // at a time, all 16 table reads issued together.  Safe tables (every factor 0 or within
-        // 2^+-120): the 8 factors multiply as a tree, one renormalisation per pair of chunks;
-        // otherwise renormalise after every factor.
-        double mn = 1.0, mo = 1.0;
-        int en = 0, eo = 0;
-        const unsigned char *tbo = reinterpret_cast<const unsigned char *>(tabo);
-        const unsigned char *tbn = reinterpret_cast<const unsigned char *>(tabn);
+        // at a time.  Dense: all 8 table reads issued together; sparse: a read only where the
+        // position's state is ia / ib and its class row / position is the move's (a branch per
+        // position, skipped when no lane needs it).  Safe factors (within 2^+-120): the 8 multiply
+        // as a tree, one renormalisation per pair of chunks; otherwise renormalise after every
+        // factor.
+        double m = 1.0;
+        int e = 0;
+        const unsigned char *tb = reinterpret_cast<const unsigned char *>(tab);
         const uint32_t xsh = a.xs8 ? 0u : 3u;
-        for (int b0 = 0; b0 < nch; b0 += OBW) {
-            if (b0 > 0) {
+        const uint32_t xa = (uint32_t)ia << (3 - xsh), xbv = (uint32_t)ib << (3 - xsh);  // obs byte of ia / ib
+        for (int b0 = k_lo; b0 < k_hi; b0 += OBW) {
+            if (b0 > k_lo) {
 #pragma unroll
                 for (int i = 0; i < OBW; i++) o[i] = obs32[fo + (size_t)min(b0 + i, nch - 1) * WAVE + lane];
             }
 #pragma unroll
             for (int j = 0; j < OBW; j += 2) {
                 const int i0 = b0 + j;
-                if (i0 >= nch) break;  // uniform
-                const bool two = i0 + 1 < nch;
+                if (i0 >= k_hi) break;  // uniform
+                const bool two = i0 + 1 < k_hi;
                 const uint4 ra = *reinterpret_cast<const uint4 *>(rowp + i0 * 256 + 4 * lane);
                 const uint4 rb = *reinterpret_cast<const uint4 *>(rowp + (two ? i0 + 1 : i0) * 256 + 4 * lane);
                 const uint32_t oa = o[j], ob = o[j + 1];
                 const uint32_t r8[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
-                double vo[8], vn[8];
+                double v[8];
+                if (dense) {
 #pragma unroll
-                for (int q = 0; q < 8; q++) {
-                    const uint32_t xb = ((q < 4 ? oa : ob) >> (8 * (q & 3))) & 0xffu;
-                    const uint32_t ad = r8[q] + (xb << xsh);
-                    vo[q] = *reinterpret_cast<const double *>(tbo + ad);
-                    vn[q] = *reinterpret_cast<const double *>(tbn + ad);
+                    for (int q = 0; q < 8; q++) {
+                        const uint32_t xb = ((q < 4 ? oa : ob) >> (8 * (q & 3))) & 0xffu;
+                        v[q] = *reinterpret_cast<const double *>(tb + r8[q] + (xb << xsh));
+                    }
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 8; q++) {
+                        const uint32_t xb = ((q < 4 ? oa : ob) >> (8 * (q & 3))) & 0xffu;
+                        const int pq = (q < 4 ? i0 : i0 + 1) * 256 + 4 * lane + (q & 3);
+                        const bool need = (xb == xa || xb == xbv) && (r8[q] - c_lo) < c_span &&
+                                          (uint32_t)(pq - p_lo) < (uint32_t)(p_hi - p_lo);
+                        v[q] = 1.0;
+                        if (need) v[q] = lds_rd(reinterpret_cast<const double *>(tb + r8[q] + (xb << xsh)));
+                    }
                 }
                 if (!two) {
 #pragma unroll
-                    for (int q = 4; q < 8; q++) vo[q] = vn[q] = 1.0;
+                    for (int q = 4; q < 8; q++) v[q] = 1.0;
                 }
                 if (wid) {
 #pragma unroll
                     for (int q = 0; q < 8; q++) {
-                        mo *= vo[q];
-                        renorm(mo, eo);
-                        mn *= vn[q];
-                        renorm(mn, en);
+                        m *= v[q];
+                        renorm(m, e);
                     }
                 } else {
-                    mo *= ((vo[0] * vo[1]) * (vo[2] * vo[3])) * ((vo[4] * vo[5]) * (vo[6] * vo[7]));
-                    mn *= ((vn[0] * vn[1]) * (vn[2] * vn[3])) * ((vn[4] * vn[5]) * (vn[6] * vn[7]));
-                    renorm(mo, eo);
-                    renorm(mn, en);
+                    m *= ((v[0] * v[1]) * (v[2] * v[3])) * ((v[4] * v[5]) * (v[6] * v[7]));
+                    renorm(m, e);
                 }
             }
         }
-#if SBZ_MH_DLOG
-        const double r = flog(fdiv_pos(mn, mo)) + (double)(en - eo) * LN2;  // mn, mo in [0.5, 1)
+        if (!dense) {  // reset the sparse table's entries (this wave's reads of them come first)
+            for (int i = lane; i < n_chg; i += WAVE) tab[entry_of(i)] = 1.0;
+        }
+#ifdef SBZ_MH_STAMP
+        const long long dt_ga = clock64();
+        const double res = wave_sum(flog_e(m, e));
+        const long long dt_lg = clock64();
+        if (SBZ_MH_STAMP == 4) stamp_dp = (double)(dt_tb - dt_start);
+        if (SBZ_MH_STAMP == 5) stamp_dp = (double)(dt_ga - dt_tb);
+        if (SBZ_MH_STAMP == 6) stamp_dp = (double)(dt_lg - dt_ga);
+        return res;
 #else
-        const double r = log(mn / mo) + (double)(en - eo) * LN2;
+        return wave_sum(flog_e(m, e));  // m in [0.5, 1) (1.0 if no pair), 0, or not finite
 #endif
-        return wave_sum(r);
     };
 
     // One MH step per iteration, in four phases with one call site each (keeps the kernel small):
@@ -897,12 +958,25 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
         if (in && (comp_ == 3 || (pl->comp[k] == comp_ && pl->row[k] == row_))) okw[k] = 0;
         if (__ballot(in) != 0) bsync();  // the same ballot in every wave
     };
+#ifdef SBZ_MH_STAMP
+    // diagnostic builds (tools/build_mh_variant.sh NAME -DSBZ_MH_STAMP=K): the trace's ll column
+    // holds shader-clock cycles per step instead (K = 1: the whole step, make_plans included;
+    // 2: the grouped path's delta phase; 3: make_plans; a group's cycles are split evenly over its
+    // members; 4 / 5 / 6: wave 0's delta_param table build / gathers / log + sum, not split);
+    // tools/mh_optime.py --stamps reads them
+    long long stamp_t0 = 0, stamp_plan = 0, stamp_d0 = 0, stamp_d1 = 0;
+    double stamp_val = 0.0;
+#endif
     auto trace_step = [&](int st, int op_, bool acc) {
         if (ch.trace_op && tid == 0) {
             const size_t t = (size_t)b * a.n_steps + st;
             ch.trace_op[t] = (int8_t)op_;
             ch.trace_accept[t] = acc ? 1 : 0;
+#ifdef SBZ_MH_STAMP
+            ch.trace_ll[t] = stamp_val;
+#else
             ch.trace_ll[t] = ll;
+#endif
         }
         if (ch.trace_zos) {
             uint8_t *tz = ch.trace_zos + ((size_t)b * a.n_steps + st) * N;
@@ -912,10 +986,17 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
     int gsl = 0;  // gdl slot of the next group
     for (int step = 0; step < a.n_steps; step++) {
         if (rng.bad || broken) break;
+#ifdef SBZ_MH_STAMP
+        stamp_t0 = clock64();
+        stamp_plan = 0;
+#endif
         if (philox) rng.ctr = ctr0 + (uint64_t)step * WIN;
         if (philox && LAe > 1 && step >= plan_t0 + LAe) {
             fence_params();
             make_plans(step);
+#ifdef SBZ_MH_STAMP
+            stamp_plan = clock64() - stamp_t0;
+#endif
         }
         const int pk = step - plan_t0;  // this step's plan (Philox, LAe > 1)
         // the plan's fields, read in one batch (one LDS round trip)
@@ -957,6 +1038,9 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             }
             double *gslot = gdl + gsl * 8;
             gsl ^= 1;  // a slot is rewritten only after every wave passed the next group's barrier
+#ifdef SBZ_MH_STAMP
+            stamp_d0 = clock64();
+#endif
             const int wvu = uni(wv);
             if (wvu < g) {
                 const int q = pk + wvu;
@@ -966,6 +1050,9 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                 if (lane == 0) gslot[wvu] = d;
             }
             bsync();
+#ifdef SBZ_MH_STAMP
+            stamp_d1 = clock64();
+#endif
             for (int k = 0; k < g; k++) {
                 const int q = pk + k;
                 const int op_k = uni(pl->op[q]), comp_k = uni(pl->comp[q]), row_k = uni(pl->row[q]);
@@ -992,6 +1079,14 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                     store_pending = true;
                     patch_later(q, fm_k, comp_k, row_k, f_k, ia_k, ib_k, nv0_k, nv1_k);
                 }
+#ifdef SBZ_MH_STAMP
+                {
+                    const long long now = clock64();
+                    stamp_val = SBZ_MH_STAMP == 1 ? (double)(now - stamp_t0) / g
+                              : SBZ_MH_STAMP == 2 ? (double)(stamp_d1 - stamp_d0) / g
+                              : SBZ_MH_STAMP == 3 ? (double)stamp_plan / g : uni(stamp_dp);
+                }
+#endif
                 trace_step(step + k, op_k, acc);
             }
             step += g - 1;
@@ -1373,6 +1468,9 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                 zos[lst[k]] = (gib_fl[k] & 2) ? (uint8_t)gz : (uint8_t)NONE;
             bsync();
         }
+#ifdef SBZ_MH_STAMP
+        stamp_val = SBZ_MH_STAMP == 1 ? (double)(clock64() - stamp_t0) : SBZ_MH_STAMP == 3 ? (double)stamp_plan : 0.0;
+#endif
         trace_step(step, op, accept);
     }
 

@@ -174,6 +174,36 @@ __device__ __forceinline__ double flog(double x) {
 #endif
 }
 
+// log(m 2^k) for a renormalised product m (frexp mantissa, or 0 / not finite) and its exponent k:
+// flog's series with k added to the exponent part (two-part ln 2), so a product of exact 1.0
+// factors gives exactly 0
+__device__ __forceinline__ double flog_e(double x, int k) {
+    double m = __builtin_amdgcn_frexp_mant(x);
+    int e = __builtin_amdgcn_frexp_exp(x);
+    const bool lo = m < 0.70710678118654752440;
+    m = lo ? m * 2.0 : m;
+    e = (lo ? e - 1 : e) + k;
+    const double f = m - 1.0, d = m + 1.0;
+    const double dl = m - (d - 1.0);
+    double r = __builtin_amdgcn_rcp(d);
+    r = fma(fma(-d, r, 1.0), r, r);
+    r = fma(fma(-d, r, 1.0), r, r);
+    const double s0 = f * r;
+    const double sv = fma(r, fma(-s0, d, f) - s0 * dl, s0);
+    const double z = sv * sv;
+    const double z2 = z * z, z4 = z2 * z2, z8 = z4 * z4;
+    const double a0 = fma(2.0 / 5.0, z, 2.0 / 3.0), a1 = fma(2.0 / 9.0, z, 2.0 / 7.0);
+    const double a2 = fma(2.0 / 13.0, z, 2.0 / 11.0), a3 = fma(2.0 / 17.0, z, 2.0 / 15.0);
+    const double a4 = fma(2.0 / 21.0, z, 2.0 / 19.0);
+    const double p = fma(a4, z8, fma(fma(a3, z2, a2), z4, fma(a1, z2, a0)));
+    const double lm = fma(sv * z, p, 2.0 * sv);
+    const double de = (double)e;
+    double v = fma(de, 6.93147180369123816490e-01, fma(de, 1.90821492927058770002e-10, lm));
+    v = x == 0.0 ? -INFINITY : v;
+    v = x == INFINITY ? INFINITY : v;
+    return (x < 0.0 || x != x) ? __builtin_nan("") : v;
+}
+
 // a / b for normal positive a, b away from the range limits (v_rcp_f64, two Newton steps and
 // one residual correction: <= 1 ulp): ~7 dependent operations against the IEEE sequence's
 // div_scale / div_fmas / div_fixup (~310 cycles, profiles/r04_gamma_lat.txt).

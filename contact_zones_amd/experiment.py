@@ -347,21 +347,24 @@ def derive_seeds(seed, run, n_zones):
     return {"host": host, "warmup": warm, "sample": main}
 
 
-def agree_seed(seed=None):
+def agree_seed(seed=None, group=None):
     """The experiment seed every rank uses: `seed` if given, else one drawn from OS entropy on
-    rank 0; broadcast from rank 0 when torch.distributed is initialised, so that all ranks build
-    the same initial samples (the chains are sharded, their initial states are not)."""
+    rank 0; broadcast from rank 0 of `group` when torch.distributed is initialised, so that all
+    ranks build the same initial samples (the chains are sharded, their initial states are not)."""
     from .parallel import broadcast_seed
     if seed is None:
         seed = int(np.random.SeedSequence().entropy) & (2**63 - 1)
-    return broadcast_seed(int(seed))
+    return broadcast_seed(int(seed), group)
 
 
 def run_experiment(config, data, n_zones, run=0, name="experiment", seed=None, device=None,
-                   logger=None, warmup_chains=None):
+                   logger=None, warmup_chains=None, group=None):
     """One run for one number of zones (cli.py:13-27): warm-up, sampling, results files.
     Returns (statistics, paths).  `seed` is the experiment seed (None: fresh entropy, agreed
-    across ranks); the phases draw from independent streams derived from (seed, run, n_zones)."""
+    across the ranks of `group`); the phases draw from independent streams derived from
+    (seed, run, n_zones), so a job's files do not depend on which rank or thread runs it or on
+    what runs beside it.  `group`: the ranks whose GPUs share this job's chains (None: all ranks;
+    a one-rank group when the runner shards the jobs themselves, run_jobs)."""
     from . import io
     from .mcmc import BatchedZoneMCMC, BatchedZoneMCMCWarmup
     from .postprocessing import contribution_per_area, eval_ground_truth, match_areas, rank_areas
@@ -372,13 +375,16 @@ def run_experiment(config, data, n_zones, run=0, name="experiment", seed=None, d
     priors, gibbs = build_priors(cfg, data)
     model = model_spec(cfg, n_zones)
     ops = operators(cfg)
-    seeds = derive_seeds(agree_seed(seed), run, n_zones)
+    seeds = derive_seeds(agree_seed(seed, group), run, n_zones)
     rng = random.Random(seeds["host"])
-    np.random.seed(seeds["host"] % 2**32)  # the initial sources' draws (np.random, as the reference)
+    # the initial sources' draws: the reference's np.random stream seeded per job, as a RandomState
+    # of the job's own (the same draws as np.random.seed + np.random.random)
+    nps = np.random.RandomState(seeds["host"] % 2**32)
     common = dict(model=model, data=data, operators=ops, var_proposal=mc["PROPOSAL_PRECISION"],
                   p_grow_connected=mc["P_GROW_CONNECTED"], initial_size=mc["M_INITIAL"],
                   logger=logger, rng=rng, device=device, priors=priors,
-                  gibbs_counts=gibbs if model.sample_source else None)
+                  gibbs_counts=gibbs if model.sample_source else None, group=group,
+                  np_random=nps.random_sample)
     t0 = time.time()
     warm = BatchedZoneMCMCWarmup(n_chains=warmup_chains or mc["WARM_UP"]["N_WARM_UP_CHAINS"],
                                  seed=seeds["warmup"], **common)
@@ -391,7 +397,8 @@ def run_experiment(config, data, n_zones, run=0, name="experiment", seed=None, d
     # gathered to rank 0 at the end of the run (BatchedZoneMCMC.chain_statistics)
     n_main = max(int(mc["N_CHAINS"]), int(mc.get("INDEPENDENT_CHAINS", 1)))
     smp = BatchedZoneMCMC(n_chains=n_main, initial_sample=best, seed=seeds["sample"],
-                          log_all_chains=n_main > 1, **common)
+                          log_all_chains=n_main > 1, chain_params=mc.get("CHAIN_PARAMS"),
+                          log_window=mc.get("LOG_WINDOW"), **common)
     smp.generate_samples(mc["N_STEPS"], mc["N_SAMPLES"])
     if getattr(smp, "rank", 0) != 0:
         # chain_idx[0] (the logged chain) lives on rank 0: the other ranks have nothing to write
@@ -413,23 +420,32 @@ def run_experiment(config, data, n_zones, run=0, name="experiment", seed=None, d
     pth = os.path.join(cfg["results"]["RESULTS_PATH"], name, fi)
     os.makedirs(pth, exist_ok=True)
     out = None
+    truth = None  # eval_ground_truth once per run (its true_* keys copied into every chain's stats)
     for c, chain_stats in enumerate(per_chain):
         # chain 0: the reference's files; chain c > 0: the same files with a _chain<c> suffix
         sfx = "" if c == 0 else f"_chain{c}"
         paths = {"parameters": os.path.join(pth, f"stats_{fi}_{run}{sfx}.txt"),
-                 "areas": os.path.join(pth, f"areas_{fi}_{run}{sfx}.txt"),
-                 "gt": os.path.join(pth, "ground_truth", "stats.txt"),
-                 "gt_areas": os.path.join(pth, "ground_truth", "areas.txt")}
+                 "areas": os.path.join(pth, f"areas_{fi}_{run}{sfx}.txt")}
+        if c == 0:  # the ground-truth files: once per run
+            paths.update({"gt": os.path.join(pth, "ground_truth", "stats.txt"),
+                          "gt_areas": os.path.join(pth, "ground_truth", "areas.txt")})
         main_stats = smp.statistics
         smp.statistics = chain_stats
         try:
-            contribution_per_area(smp)
-            stats = rank_areas(match_areas(smp.statistics))
+            if "sample_weights" in chain_stats:
+                contribution_per_area(smp)
+                stats = rank_areas(match_areas(smp.statistics))
+            else:
+                # a chain logged without its parameters (ChainLog): zones matched, no per-zone
+                # contributions to rank them by, no parameter columns (io.samples2file)
+                stats = match_areas(dict(smp.statistics, acceptance_ratio=main_stats["acceptance_ratio"]))
         finally:
             smp.statistics = main_stats
         if getattr(data, "is_simulated", False):  # MCMC.save_samples (mcmc_setup.py:227-229)
-            eval_ground_truth(smp, data, bool(cfg["model"]["INHERITANCE"]), stats)
-            os.makedirs(os.path.dirname(paths["gt"]), exist_ok=True)
+            if truth is None:
+                truth = eval_ground_truth(smp, data, bool(cfg["model"]["INHERITANCE"]), {})
+                os.makedirs(os.path.dirname(paths["gt"]), exist_ok=True)
+            stats.update(truth)
         io.samples2file(stats, data, cfg, paths)
         if c == 0:
             out = (stats, paths)
@@ -451,6 +467,18 @@ def main(argv=None):
                    help="independent main-run chains (mcmc.INDEPENDENT_CHAINS; MC3 stays off): chain 0 "
                         "writes the reference's results files, chain c > 0 the same files with a _chain<c> "
                         "suffix; the chains are sharded over the ranks and gathered to rank 0 at the end")
+    p.add_argument("--chain-params", default=None,
+                   help="with --chains: the chains (besides chain 0) whose parameters are logged too, "
+                        "'all' or comma-separated global chain ids (mcmc.CHAIN_PARAMS); the others log "
+                        "zones, log-likelihood and log prior only")
+    p.add_argument("--log-window", type=int, default=None, help=argparse.SUPPRESS)
+    p.add_argument("--jobs", choices=["concurrent", "sequential"], default="concurrent",
+                   help="the N_RUNS x N_AREAS jobs: all at once, each on a thread and HIP stream of its own "
+                        "(default), or one after another as the reference's cli.py; the files are the same")
+    p.add_argument("--shard", choices=["auto", "jobs", "chains"], default="auto",
+                   help="under torchrun: give each rank whole jobs ('jobs': job i on rank i %% world) or "
+                        "split every job's chains over the ranks ('chains'); auto: jobs when there are at "
+                        "least as many jobs as ranks")
     p.add_argument("--sim-data", default=None,
                    help="simulation config: the simulated data and its ground truth (.npz, SimulatedData.from_npz)")
     a = p.parse_args(argv)
@@ -460,6 +488,11 @@ def main(argv=None):
     custom = json.loads(a.set) if a.set else {}
     if a.chains is not None:
         custom.setdefault("mcmc", {})["INDEPENDENT_CHAINS"] = a.chains
+    if a.chain_params is not None:
+        custom.setdefault("mcmc", {})["CHAIN_PARAMS"] = (
+            "all" if a.chain_params == "all" else [int(c) for c in a.chain_params.split(",") if c])
+    if a.log_window is not None:
+        custom.setdefault("mcmc", {})["LOG_WINDOW"] = a.log_window
     config, _ = load_config(a.config, custom or None, simulated=a.sim_data is not None)
     name = a.name or time.strftime("%Y%m%d-%H%M%S")
     data = SimulatedData.from_npz(a.sim_data) if a.sim_data else ExperimentData(config)
@@ -472,11 +505,10 @@ def main(argv=None):
                          "(set it with --set '{\"model\": {\"N_AREAS\": 3}}')")
     name = _broadcast_name(name)
     seed = agree_seed(a.seed)
+    jobs = [(run, int(n)) for run in range(config["mcmc"]["N_RUNS"]) for n in sweep]
     try:
-        for run in range(config["mcmc"]["N_RUNS"]):
-            for n in sweep:
-                run_experiment(config, data, int(n), run=run, name=name, seed=seed, device=device,
-                               logger=logger)
+        run_jobs(config, data, jobs, name, seed, device, logger, shard=a.shard,
+                 concurrent=a.jobs == "concurrent")
     except BaseException:
         # no barrier: the other ranks may be waiting in a different collective; leave the group
         # and exit non-zero so the launcher tears the job down
@@ -484,6 +516,63 @@ def main(argv=None):
         raise
     _finish_distributed(ok=True)
     return 0
+
+
+def run_jobs(config, data, jobs, name, seed, device=None, logger=None, shard="auto", concurrent=True):
+    """The (run, n_zones) jobs of an experiment (cli.py:71-84 runs them one after another).
+
+    concurrent: every job of this process at once, each on a thread of its own with its own HIP
+    stream (torch's current stream is per thread, and every launch of a job goes to it), so the
+    jobs' launches share the GPU (one chain per job occupies one CU of 256).  Under torchrun
+    (WORLD_SIZE > 1) with shard 'jobs' (or 'auto' and at least as many jobs as ranks) job i runs
+    whole on rank i % world in a one-rank group (no collective inside a job); with 'chains' every
+    job's chains are split over all ranks (the jobs then run one after another: their collectives
+    must not interleave).  A job's files do not depend on any of this (run_experiment).  Returns
+    this process's results in job order (None for another rank's jobs)."""
+    from .parallel import _dist
+    d = _dist()
+    world = d.get_world_size() if d is not None else 1
+    rank = d.get_rank() if d is not None else 0
+    group = None
+    mine = list(range(len(jobs)))
+    if world > 1 and (shard == "jobs" or (shard == "auto" and len(jobs) >= world)):
+        groups = [d.new_group([r]) for r in range(world)]  # every rank creates every group
+        group = groups[rank]
+        mine = [i for i in range(len(jobs)) if i % world == rank]
+    elif world > 1:
+        concurrent = False
+    results = [None] * len(jobs)
+
+    def job(i):
+        run, n = jobs[i]
+        return run_experiment(config, data, n, run=run, name=name, seed=seed, device=device,
+                              logger=logger, group=group)
+
+    if not concurrent or len(mine) <= 1:
+        for i in mine:
+            results[i] = job(i)
+        return results
+    import threading
+    import torch
+    dev = device if device is not None else torch.cuda.current_device()
+    errors = []
+
+    def work(i):
+        try:
+            with torch.cuda.device(dev), torch.cuda.stream(torch.cuda.Stream(dev)):
+                results[i] = job(i)
+                torch.cuda.current_stream().synchronize()
+        except BaseException as e:  # re-raised in the calling thread
+            errors.append((i, e))
+
+    threads = [threading.Thread(target=work, args=(i,), name=f"sbz-job-{i}") for i in mine]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    if errors:
+        raise errors[0][1]
+    return results
 
 
 def init_distributed(device=None):

@@ -303,10 +303,13 @@ def _fmt(v):
 
 
 def stats_columns(feature_names, state_names, family_names, n_zones, inheritance, simulated,
-                  single_zones):
-    """The column names of collect_row_for_writing (util.py:744-843), in order."""
+                  single_zones, params=True):
+    """The column names of collect_row_for_writing (util.py:744-843), in order (params False: a
+    chain logged without its parameters, the columns before and after the parameter block)."""
     cols = ["Sample", "posterior", "likelihood", "prior"]
     cols += [f"size_a{i}" for i in range(n_zones)]
+    if not params:
+        return cols + (["recall", "precision"] if simulated else [])
     for f in feature_names:
         cols += ["w_universal_" + str(f), "w_contact_" + str(f)]
         if inheritance:
@@ -416,7 +419,7 @@ def samples2file(samples, data, config, paths):
     inheritance = bool(config["model"]["INHERITANCE"])
     family_names = list(ext(data.family_names)) if inheritance else []
     simulated = bool(getattr(data, "is_simulated", False))
-    if simulated:
+    if simulated and "gt" in paths:  # (written once per run: an independent chain c > 0 leaves them out)
         gt, gt_cols = collect_gt_for_writing(samples, data, config)
         with open(paths["gt"], "w", newline="") as fh:
             writer = csv.writer(fh, delimiter="\t")
@@ -429,8 +432,11 @@ def samples2file(samples, data, config, paths):
     steps_per_sample = float(config["mcmc"]["N_STEPS"] / config["mcmc"]["N_SAMPLES"])
     n_zones = int(config["model"]["N_AREAS"])
     single = "sample_lh_single_zones" in samples
+    # a chain logged without its parameters (an independent chain c > 0, mcmc.ChainLog): the
+    # sample, posterior, likelihood, prior and size columns (and recall / precision) only
+    params = "sample_weights" in samples
     cols = stats_columns(feature_names, state_names, family_names, n_zones, inheritance, simulated,
-                         single)
+                         single, params)
     n_f = len(feature_names)
     st_idx = [list(range(len(s))) for s in state_names]
     with open(paths["parameters"], "w", newline="") as fh:
@@ -443,6 +449,11 @@ def samples2file(samples, data, config, paths):
             row = [str(int(s * steps_per_sample)), _fmt(pri + lik), _fmt(lik), _fmt(pri)]
             z = np.asarray(zones[s])
             row += [str(int(np.count_nonzero(a))) for a in z]
+            if not params:
+                if simulated:
+                    row += [_fmt(v) for v in recall_precision(z, samples["true_zones"])]
+                writer.writerow(row)
+                continue
             w = samples["sample_weights"][s]
             for f in range(n_f):
                 row += [_fmt(w[f][0]), _fmt(w[f][1])]

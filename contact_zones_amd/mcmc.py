@@ -117,7 +117,7 @@ class InitialSamples:
     """generate_initial_sample (zone_sampling.py:935-1233) on the host, draw for draw."""
 
     def __init__(self, features, applicable_states, adj_indptr, adj_indices, families, n_zones,
-                 initial_size, inheritance, initial_sample, rng, sample_source=False):
+                 initial_size, inheritance, initial_sample, rng, sample_source=False, np_random=None):
         self.features = features
         self.applicable_states = applicable_states
         self.adj_indptr, self.adj_indices = adj_indptr, adj_indices
@@ -128,6 +128,10 @@ class InitialSamples:
         self.initial_sample = initial_sample if initial_sample is not None else Sample.empty_sample()
         self.rng = rng
         self.sample_source = sample_source
+        # the initial sources' uniforms: np.random.random (the reference's global stream) or a
+        # job's own RandomState(seed).random_sample (the same draws as np.random.seed(seed) then
+        # np.random.random, without sharing the global stream with concurrent jobs)
+        self.np_random = np_random
         self.n_sites, self.n_features = features.shape[:2]
 
     def neighbours(self, zone, already_in_zone):
@@ -257,7 +261,8 @@ class InitialSamples:
             post = source_posterior(self._obs, self._fam, zos, np.asarray(weights, np.float64),
                                     np.asarray(p_global, np.float64)[0], p_zones, p_families,
                                     self.inheritance)
-            sample.source = packing.index_to_source(draw_sources(post), 3 if self.inheritance else 2)
+            draws = draw_sources(post) if self.np_random is None else draw_sources(post, self.np_random)
+            sample.source = packing.index_to_source(draws, 3 if self.inheritance else 2)
         return sample
 
 
@@ -281,7 +286,8 @@ class BatchedZoneMCMC:
                  initial_size, initial_sample=None, mc3=False, swap_period=None, chain_swaps=None,
                  sample_from_prior=False, show_screen_log=False, logger=None, *, seed=None,
                  rng=None, device=None, group=None, refresh_every_launch=True, priors=None,
-                 gibbs_counts=None, log_all_chains=False, **kwargs):
+                 gibbs_counts=None, log_all_chains=False, chain_params=None, log_window=None,
+                 np_random=None, **kwargs):
         if mc3:
             raise NotImplementedError("MC3 chain swaps are not part of the batched sampler")
         if sample_from_prior:
@@ -339,11 +345,15 @@ class BatchedZoneMCMC:
                            'acceptance_ratio': math.nan, 'accepted_steps': 0, 'n_swaps': 0,
                            'accepted_swaps': 0, 'swap_ratio': [],
                            'accept_operator': defaultdict(int), 'reject_operator': defaultdict(int)}
-        # independent-chains runs (the runner's --chains): every chain's samples are logged too,
-        # kept on the device until the run ends and then gathered to rank 0 (chain_statistics)
+        # independent-chains runs (the runner's --chains): every chain's samples are logged too, in
+        # windows gathered to rank 0 as the run goes (ChainLog -> chain_statistics): zones, ll and
+        # prior of every chain; the parameters of chain 0 (the logged chain, `statistics`) and of
+        # the chains in `chain_params` ("all" or global chain ids)
         self.log_all_chains = bool(log_all_chains)
+        self.chain_params = chain_params
+        self.log_window = log_window
         self.chain_statistics = None
-        self._snaps = []
+        self._chain_log = None
         self._ll = np.full(self.n_chains, -np.inf)
         self._prior = np.full(self.n_chains, -np.inf)
         self.t_start = time.time()
@@ -361,7 +371,7 @@ class BatchedZoneMCMC:
         self._init = InitialSamples(self.features, self.applicable_states, self.adj_indptr,
                                     self.adj_indices, self.families, self.n_zones,
                                     self.initial_size, self.inheritance, self.initial_sample,
-                                    self.rng, sample_source=self.sample_source)
+                                    self.rng, sample_source=self.sample_source, np_random=np_random)
 
     # ---- reference API ---------------------------------------------------------------
     def generate_initial_sample(self, c=0):
@@ -599,12 +609,15 @@ class BatchedZoneMCMC:
                                     "(the reference's last-sample test divides by n_steps - 1)")
         events.add(n_steps - 1)
         done = 0  # steps taken so far
+        if self.log_all_chains:
+            self._chain_log = ChainLog(self, len(range(0, n_steps, steps_per_sample)), self.chain_params,
+                                       self.log_window)
         for i_step in sorted(events):
             self._advance(i_step + 1 - done)
             done = i_step + 1
             if i_step % steps_per_sample == 0:
                 if self.log_all_chains:
-                    self._snap(int(i_step / steps_per_sample))
+                    self._chain_log.snap(int(i_step / steps_per_sample))
                 s0 = self._chain0_sample()
                 if self.rank == 0:
                     # the logged sample's prior evaluated in full (the carried value differs by
@@ -626,7 +639,8 @@ class BatchedZoneMCMC:
             self._resolve_alias(st.p_global[0], st.p_zones[0],
                                 st.p_fam[0] if st.p_fam is not None else None)
         if self.log_all_chains:
-            self.chain_statistics = self._gather_chains()
+            self.chain_statistics = self._chain_log.finish()
+            self._chain_log = None
         t_end = time.time()
         self._count_operators()
         self.statistics['sampling_time'] = t_end - t_start
@@ -634,63 +648,6 @@ class BatchedZoneMCMC:
         self.statistics['acceptance_ratio'] = self.statistics['accepted_steps'] / n_steps
         self.statistics['swap_ratio'] = 0
         return None
-
-    def _snap(self, sample_id):
-        """Copy of this rank's chains at a logging point (device tensors, gathered at the end)."""
-        import torch
-        st = self._state
-        if st is None:
-            self._snaps.append(None)
-            return
-        self._snaps.append({"id": sample_id, "zos": st.zone_of_site.clone(), "w": st.w.clone(),
-                            "pg": st.p_global.clone(), "pz": st.p_zones.clone(),
-                            "pf": st.p_fam.clone() if st.p_fam is not None else None,
-                            "ll": st.ll.clone()})
-
-    def _gather_chains(self):
-        """Every chain's logged samples on rank 0: this rank's snapshots stacked per chain
-        ([chains][samples][...]), then one gather of the shards per array over the ranks
-        (parallel.gather_rows: RCCL over xGMI with the nccl backend).  Returns, on rank 0, one
-        statistics dict per global chain with the keys samples2file reads (the logged prior is
-        evaluated in full on the host, as for the logged chain); None on the other ranks.  Chain 0
-        is the logged chain: its dict is `statistics` itself."""
-        import torch
-        from .parallel import gather_rows
-        n, B = len(self._snaps), self.hi - self.lo
-        N, F, S, Z = self.n_sites, self.n_features, self.n_states, self.n_zones
-        C = 3 if self.inheritance else 2
-        Fam = self.n_families if self.inheritance else 0
-        dev = self._state.ll.device if self._state is not None else torch.device("cpu")
-        shapes = {"zos": ((N,), torch.uint8), "w": ((F, C), torch.float64), "pg": ((F, S), torch.float64),
-                  "pz": ((Z, F, S), torch.float64), "ll": ((), torch.float64)}
-        if self.inheritance:
-            shapes["pf"] = ((Fam, F, S), torch.float64)
-        ids = [sn["id"] for sn in self._snaps] if n and self._snaps[0] is not None else list(range(n))
-        full = {}
-        for k, (shp, dt) in shapes.items():
-            loc = (torch.stack([sn[k] for sn in self._snaps], 1) if B and n
-                   else torch.zeros((B, n) + shp, dtype=dt, device=dev))
-            full[k] = gather_rows(loc, self.n_chains, self._group)
-        self._snaps = []
-        if self.rank != 0:
-            return None
-        host = {k: v.cpu().numpy() for k, v in full.items()}
-        out = [self.statistics]
-        for c in range(1, self.n_chains):
-            zos = host["zos"][c]
-            pf = host["pf"][c] if self.inheritance else None
-            prior = self.priors.log_prior(zos, host["pg"][c], pf, self.applicable_states, self.n_zones,
-                                          self.inheritance) if n else np.zeros(0)
-            st = {'sample_id': list(ids), 'sample_likelihood': [float(v) for v in host["ll"][c]],
-                  'sample_prior': [float(v) for v in prior],
-                  'sample_zones': [packing.index_to_groups(z, Z) for z in zos],
-                  'sample_weights': list(host["w"][c]),
-                  'sample_p_global': [p[None] for p in host["pg"][c]],
-                  'sample_p_zones': list(host["pz"][c]),
-                  'sample_p_families': list(pf) if pf is not None else [None] * n,
-                  'last_sample': [], 'chain': c}
-            out.append(st)
-        return out
 
     def _count_operators(self):
         acc, prop = self._operator_counts()
@@ -720,6 +677,161 @@ class BatchedZoneMCMC:
         return Sample(zones=arrays[0], weights=arrays[1], p_global=arrays[2], p_zones=arrays[3],
                       p_families=arrays[4] if self.inheritance else None,
                       source=arrays[k] if self.sample_source else None, chain=best)
+
+
+class ChainLog:
+    """The logged samples of every chain of an independent-chains run (BatchedZoneMCMC with
+    log_all_chains), streamed to rank 0 in windows (mcmc_generative.py:205-218 logs one chain;
+    util.py:846-907 writes it).
+
+    Each logging point copies, on the device, this rank's chains' zone assignments (u8 [N]), carried
+    log-likelihood and carried log prior into slot j of a window of W samples; the parameters
+    (w, p_global, p_zones, p_families) only of the chains in `params` ("all", or global chain ids;
+    chain 0's are logged by the reference path itself).  A full window is gathered to rank 0 (one
+    gather per array, parallel.gather_to_root: RCCL over xGMI with nccl), copied through a pinned
+    host buffer into rank 0's host arrays, and the slot counter starts again: device memory is
+    O(W), never O(N_SAMPLES), and no rank but 0 ever holds other ranks' samples.
+
+    Bytes: per rank and window B (N + 16) W for every chain, plus P (8 F (C + S (1 + Z + Fam))) W
+    for P parameter chains; rank 0's gather output is the same times the ranks; rank 0's host
+    arrays n_chains n_log (N + 16) (+ n_log x the parameter bytes per parameter chain).  At the
+    north-star run (2048 chains over 8 GPUs, N = 2000, cfg5 parameters 534 KB, 1000 samples,
+    W = 64, no parameter chains but chain 0): 33 MB of window per rank, 264 MB of gather output on
+    rank 0, 4.1 GB of host arrays on rank 0."""
+
+    WINDOW_BYTES = 256 << 20  # default window: as many samples as fit this per rank (at most 64)
+
+    def __init__(self, smp, n_log, params=None, window=None):
+        import torch
+        self.smp = smp
+        self.n_log = int(n_log)
+        n, lo, hi = smp.n_chains, smp.lo, smp.hi
+        B = hi - lo
+        N, F, S, Z = smp.n_sites, smp.n_features, smp.n_states, smp.n_zones
+        self.C = 3 if smp.inheritance else 2
+        self.Fam = smp.n_families if smp.inheritance else 0
+        if params == "all":
+            pc = list(range(1, n))
+        else:
+            pc = sorted({int(c) for c in (params or []) if 0 < int(c) < n})
+        self.pc = pc                                        # global ids with parameters (chain 0 aside)
+        self.pc_local = [c - lo for c in pc if lo <= c < hi]
+        from .parallel import shard_range
+        w = smp.world_size
+        self.pc_sizes = [sum(1 for c in pc if shard_range(n, r, w)[0] <= c < shard_range(n, r, w)[1])
+                         for r in range(w)]
+        st = smp._state
+        self.dev = st.ll.device if st is not None else torch.device("cpu")
+        pbytes = 8 * F * (self.C + S * (1 + Z + self.Fam))
+        per_sample = max(1, B * (N + 16) + max(self.pc_sizes) * pbytes)
+        W = int(window) if window else max(1, min(64, self.WINDOW_BYTES // per_sample))
+        self.W = max(1, min(W, max(self.n_log, 1)))
+        W = self.W
+        self.buf = {"zos": torch.empty((B, W, N), dtype=torch.uint8, device=self.dev),
+                    "ll": torch.empty((B, W), dtype=torch.float64, device=self.dev),
+                    "prior": torch.empty((B, W), dtype=torch.float64, device=self.dev)}
+        self.pshape = {"w": (F, self.C), "pg": (F, S), "pz": (Z, F, S)}
+        if self.Fam:
+            self.pshape["pf"] = (self.Fam, F, S)
+        P = len(self.pc_local)
+        self.pbuf = {k: torch.empty((P, W) + shp, dtype=torch.float64, device=self.dev)
+                     for k, shp in self.pshape.items()} if pc else {}
+        self.j = 0          # filled slots of the window
+        self.done = 0       # samples already on rank 0
+        self.ids = []
+        self.host = None
+        if smp.rank == 0:
+            self.host = {"zos": np.empty((n, self.n_log, N), np.uint8),
+                         "ll": np.empty((n, self.n_log)), "prior": np.empty((n, self.n_log))}
+            self.phost = {k: np.empty((len(pc), self.n_log) + shp) for k, shp in self.pshape.items()}
+            self.pin = None
+
+    def window_bytes(self):
+        """Device bytes of this rank's window buffers."""
+        return sum(t.numel() * t.element_size() for t in list(self.buf.values()) + list(self.pbuf.values()))
+
+    def snap(self, sample_id):
+        """Log this rank's chains at a logging point (device copies into the window)."""
+        st, j = self.smp._state, self.j
+        if st is not None:
+            self.buf["zos"][:, j].copy_(st.zone_of_site)
+            self.buf["ll"][:, j].copy_(st.ll)
+            self.buf["prior"][:, j].copy_(st.prior)
+            if self.pc_local:
+                idx = self.pc_local
+                self.pbuf["w"][:, j].copy_(st.w[idx])
+                self.pbuf["pg"][:, j].copy_(st.p_global[idx])
+                self.pbuf["pz"][:, j].copy_(st.p_zones[idx])
+                if "pf" in self.pbuf:
+                    self.pbuf["pf"][:, j].copy_(st.p_fam[idx])
+        self.ids.append(int(sample_id))
+        self.j += 1
+        if self.j == self.W:
+            self.flush()
+
+    def _to_host(self, t, out):
+        """Rank 0: a gathered window (device or host tensor) into the host array slice `out`
+        (through a pinned staging buffer when it is on the GPU)."""
+        import torch
+        if t.device.type == "cpu":
+            out[...] = t.numpy()
+            return
+        nb = t.numel() * t.element_size()
+        if self.pin is None or self.pin.numel() < nb:
+            self.pin = torch.empty(nb, dtype=torch.uint8, pin_memory=True)
+        stage = self.pin[:nb].view(t.dtype).view(t.shape)
+        stage.copy_(t)
+        out[...] = stage.numpy()
+
+    def flush(self):
+        """Gather the filled slots of the window to rank 0 and append them to its host arrays."""
+        from .parallel import gather_to_root
+        n = self.j
+        if n == 0:
+            return
+        smp, s0 = self.smp, self.done
+        for k in ("zos", "ll", "prior"):
+            full = gather_to_root(self.buf[k][:, :n].contiguous(), smp.n_chains, smp._group)
+            if smp.rank == 0:
+                self._to_host(full, self.host[k][:, s0:s0 + n])
+        for k in self.pbuf:
+            full = gather_to_root(self.pbuf[k][:, :n].contiguous(), len(self.pc), smp._group, sizes=self.pc_sizes)
+            if smp.rank == 0:
+                self._to_host(full, self.phost[k][:, s0:s0 + n])
+        self.done += n
+        self.j = 0
+
+    def finish(self):
+        """The last window; on rank 0 one statistics dict per global chain (chain 0: the logged
+        chain's `statistics` itself), None on the other ranks.  Chains without parameters log
+        sample_id, sample_likelihood, sample_prior (the carried log prior) and sample_zones; chains
+        with parameters also the parameter samples and the prior evaluated in full on the host (as
+        the logged chain's)."""
+        self.flush()
+        smp = self.smp
+        if smp.rank != 0:
+            return None
+        h, Z = self.host, smp.n_zones
+        m = self.done
+        out = [smp.statistics]
+        pidx = {c: i for i, c in enumerate(self.pc)}
+        for c in range(1, smp.n_chains):
+            zos = h["zos"][c, :m]
+            st = {'sample_id': list(self.ids[:m]), 'sample_likelihood': [float(v) for v in h["ll"][c, :m]],
+                  'sample_zones': [packing.index_to_groups(z, Z) for z in zos], 'last_sample': [], 'chain': c}
+            if c in pidx:
+                i = pidx[c]
+                pg, pf = self.phost["pg"][i, :m], self.phost["pf"][i, :m] if self.Fam else None
+                prior = smp.priors.log_prior(zos, pg, pf, smp.applicable_states, Z, smp.inheritance) if m else []
+                st.update({'sample_prior': [float(v) for v in prior],
+                           'sample_weights': list(self.phost["w"][i, :m]),
+                           'sample_p_global': [p[None] for p in pg],
+                           'sample_p_zones': list(self.phost["pz"][i, :m]),
+                           'sample_p_families': list(pf) if pf is not None else [None] * m})
+            else:
+                st['sample_prior'] = [float(v) for v in h["prior"][c, :m]]
+            out.append(st)
+        return out
 
 
 class BatchedZoneMCMCWarmup(BatchedZoneMCMC):

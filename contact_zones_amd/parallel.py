@@ -6,7 +6,8 @@ the step loop has no collective.  What crosses ranks:
   * per-operator accept / proposal counters (sum, once per run);
   * the warm-up arg-max of (log posterior, chain id) (mcmc_generative.py:195-200) and the
     broadcast of the winning Sample from its owner;
-  * the end-of-run gather of per-chain results to rank 0 (gather_rows).
+  * the per-window gather of every chain's logged samples to rank 0 (gather_to_root; an
+    independent-chains run, mcmc.ChainLog).
 With the nccl backend (RCCL over xGMI on MI355X) tensors live on the rank's GPU; with gloo (the
 CPU tests) on the host.
 """
@@ -121,21 +122,27 @@ def broadcast_arrays(arrays, src, group=None):
     return out
 
 
-def gather_rows(local, n_total, group=None):
-    """Concatenate every rank's shard (a torch tensor whose first dim is that rank's chains under
-    shard_range) into the full [n_total, ...] tensor on every rank (all_gather of equal-size
-    padded shards: one collective, no host round trip)."""
+def gather_to_root(local, n_total, group=None, sizes=None):
+    """Every rank's shard (first dim = that rank's chains under shard_range, or `sizes[r]` rows of
+    rank r) concatenated into the full tensor on rank 0 (on the shard's device), None on the other
+    ranks: one gather of equal-size padded shards (RCCL over xGMI with the nccl backend), so only
+    rank 0 ever holds the whole."""
     d = _dist()
     if d is None or d.get_world_size(group) == 1:
         return local
     import torch
     w = d.get_world_size(group)
+    rank = d.get_rank(group)
     dev = _device(group)
-    sizes = [shard_range(n_total, r, w) for r in range(w)]
-    m = max(hi - lo for lo, hi in sizes)
+    if sizes is None:
+        sizes = [hi - lo for lo, hi in (shard_range(n_total, r, w) for r in range(w))]
+    m = max(max(sizes), 1)
     pad = torch.zeros((m,) + tuple(local.shape[1:]), dtype=local.dtype, device=dev)
     pad[:local.shape[0]] = local.to(dev)
-    out = torch.empty((w * m,) + tuple(local.shape[1:]), dtype=local.dtype, device=dev)
-    d.all_gather_into_tensor(out, pad, group=group)
-    parts = [out[r * m:r * m + (hi - lo)] for r, (lo, hi) in enumerate(sizes)]
-    return torch.cat(parts, 0).to(local.device)
+    dst = d.get_global_rank(group, 0) if group is not None else 0
+    bufs = [torch.empty_like(pad) for _ in range(w)] if rank == 0 else None
+    d.gather(pad, gather_list=bufs, dst=dst, group=group)
+    if rank != 0:
+        return None
+    parts = [bufs[r][:n] for r, n in enumerate(sizes)]
+    return torch.cat(parts, 0)  # (on the collective's device: rank 0 copies it to the host)

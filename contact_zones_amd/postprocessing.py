@@ -151,10 +151,12 @@ def match_areas(samples):
         matching.append(best)
         s_sum += s[best]
     for key in ("sample_zones", "sample_p_zones"):
-        samples[key] = [samples[key][i][:][m] if key == "sample_zones" else samples[key][i][m]
-                        for i, m in enumerate(matching[:len(samples[key])])]
+        if key in samples:  # (a chain logged without parameters has no p_zones: mcmc.ChainLog)
+            samples[key] = [samples[key][i][:][m] if key == "sample_zones" else samples[key][i][m]
+                            for i, m in enumerate(matching[:len(samples[key])])]
     for key in ("sample_lh_single_zones", "sample_prior_single_zones", "sample_posterior_single_zones"):
-        samples[key] = [[samples[key][i][j] for j in m] for i, m in enumerate(matching[:len(samples[key])])]
+        if key in samples:
+            samples[key] = [[samples[key][i][j] for j in m] for i, m in enumerate(matching[:len(samples[key])])]
     return samples
 
 

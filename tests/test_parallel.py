@@ -10,7 +10,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from contact_zones_amd.parallel import (all_reduce_sum, best_chain, broadcast_arrays,
-                                        broadcast_seed, gather_rows, owner_of, shard_range)
+                                        broadcast_seed, gather_to_root, owner_of, shard_range)
 
 
 def test_shard_range_covers_every_chain_once():
@@ -57,7 +57,11 @@ def _worker(rank, world, port, results):
         got = broadcast_arrays(arrs, owner)
         out["bcast"] = [(a.dtype.str, a.shape, a.tolist()) for a in got]
         local = torch.arange(lo * 10, hi * 10, dtype=torch.float64).reshape(hi - lo, 10)
-        out["gather"] = gather_rows(local, 7).tolist()
+        g = gather_to_root(local, 7)
+        out["gather"] = g.tolist() if g is not None else None
+        # explicit row counts per rank (ChainLog's parameter chains): 1 row on rank 0, none on rank 1
+        g = gather_to_root(torch.full((1 - rank, 2), 7.0), 1, sizes=[1, 0])
+        out["gather_sizes"] = g.tolist() if g is not None else None
         results[rank] = out
     finally:
         dist.destroy_process_group()
@@ -79,7 +83,10 @@ def test_collectives_world_size_2():
         assert o["bcast"][0] == ("<f8", (3, 4), np.arange(12.0).reshape(3, 4).tolist())
         assert o["bcast"][1] == ("|b1", (1, 2), [[True, False]])
         assert o["bcast"][2][1] == (0, 3)
-        assert o["gather"] == np.arange(70, dtype=np.float64).reshape(7, 10).tolist()
+    # only rank 0 receives the gathered rows
+    assert res[0]["gather"] == np.arange(70, dtype=np.float64).reshape(7, 10).tolist()
+    assert res[1]["gather"] is None
+    assert res[0]["gather_sizes"] == [[7.0, 7.0]] and res[1]["gather_sizes"] is None
 
 
 def test_bench_self_launch_two_ranks():
@@ -143,3 +150,83 @@ def test_bench_source_sampler_pmc_needs_the_same_kernel_sources(tmp_path, monkey
     monkeypatch.setattr(bench, "kernel_source_hash", lambda: "other")
     r = bench.pmc_source_sampler()
     assert "source" not in r and "r09_pmc_src.json" in r["note"]
+
+
+class _FakeSampler:
+    """What ChainLog reads of a BatchedZoneMCMC: shapes, shard, state (CPU tensors here)."""
+
+    def __init__(self, rank, world, n, N=11, F=3, S=4, Z=2, Fam=2):
+        import types
+        from contact_zones_amd.priors import PriorSpec
+        self.n_chains, self.rank, self.world_size, self._group = n, rank, world, None
+        self.lo, self.hi = shard_range(n, rank, world)
+        self.n_sites, self.n_features, self.n_states, self.n_zones = N, F, S, Z
+        self.inheritance, self.n_families = True, Fam
+        self.priors, self.applicable_states = PriorSpec(), np.ones((F, S), bool)
+        self.statistics = {"chain0": True}
+        B = self.hi - self.lo
+        self._state = types.SimpleNamespace(
+            zone_of_site=torch.zeros((B, N), dtype=torch.uint8), ll=torch.zeros(B, dtype=torch.float64),
+            prior=torch.zeros(B, dtype=torch.float64), w=torch.zeros((B, F, 3), dtype=torch.float64),
+            p_global=torch.zeros((B, F, S), dtype=torch.float64),
+            p_zones=torch.zeros((B, Z, F, S), dtype=torch.float64),
+            p_fam=torch.zeros((B, Fam, F, S), dtype=torch.float64))
+
+    def set_step(self, t):
+        """Chain c's state at logging point t: recognisable values."""
+        st = self._state
+        for i, c in enumerate(range(self.lo, self.hi)):
+            st.zone_of_site[i] = torch.tensor([(c + t + s) % 3 if (c + t + s) % 3 < 2 else 255
+                                               for s in range(self.n_sites)], dtype=torch.uint8)
+            st.ll[i] = -1000.0 * c - t
+            st.prior[i] = -c - 0.5 * t
+            st.w[i] = 100 * c + t
+            st.p_global[i] = 100 * c + t + 0.25
+            st.p_zones[i] = 100 * c + t + 0.5
+            st.p_fam[i] = 100 * c + t + 0.75
+
+
+def _chainlog_worker(rank, world, port, results):
+    from contact_zones_amd.mcmc import ChainLog
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        smp = _FakeSampler(rank, world, 5)
+        log = ChainLog(smp, 7, params=[2, 4], window=3)   # windows of 3, 3, 1 samples
+        for t in range(7):
+            smp.set_step(t)
+            log.snap(10 + t)
+        out = log.finish()
+        results[rank] = None if out is None else [
+            {k: (np.asarray(v).tolist() if k != "chain0" else v) for k, v in d.items() if k != "last_sample"}
+            for d in out]
+    finally:
+        dist.destroy_process_group()
+
+
+def test_chain_log_windows_gathered_to_rank0():
+    """mcmc.ChainLog over 2 gloo ranks: every chain's zones, ll and carried prior at 7 logging
+    points in windows of 3 (the last partial), parameters of chains 2 and 4 only; everything on
+    rank 0, nothing on rank 1, each value the chain's own."""
+    port = _free_port()
+    with mp.Manager() as m:
+        results = m.dict()
+        mp.spawn(_chainlog_worker, args=(2, port, results), nprocs=2, join=True)
+        res = dict(results)
+    assert res[1] is None
+    out = res[0]
+    assert len(out) == 5 and out[0] == {"chain0": True}
+    for c in range(1, 5):
+        d = out[c]
+        assert d["chain"] == c and d["sample_id"] == list(range(10, 17))
+        assert d["sample_likelihood"] == [-1000.0 * c - t for t in range(7)]
+        for t in range(7):
+            zos = [(c + t + s) % 3 for s in range(11)]
+            want = [[z == k for z in zos] for k in range(2)]
+            assert d["sample_zones"][t] == want
+        if c in (2, 4):
+            assert d["sample_weights"] == [np.full((3, 3), 100.0 * c + t).tolist() for t in range(7)]
+            assert d["sample_p_families"][6] == np.full((2, 3, 4), 100.0 * c + 6.75).tolist()
+            assert d["sample_prior"] == [0.0] * 7   # zero priors, evaluated in full on the host
+        else:
+            assert "sample_weights" not in d
+            assert d["sample_prior"] == [-c - 0.5 * t for t in range(7)]  # the carried prior
