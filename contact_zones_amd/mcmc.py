@@ -90,7 +90,9 @@ def adjacency_csr(adj_mat, n_sites):
     """The network's adjacency (scipy sparse or dense, data['network']['adj_mat']) as sorted CSR
     int32 arrays; the neighbour relation is 'adj.dot(zone) != 0' (util.py:152-155)."""
     import scipy.sparse as sp
-    a = sp.csr_matrix(adj_mat)
+    # a copy: csr_matrix of a CSR matrix shares its arrays, and sorting them in place would race
+    # with another job's sampler reading the same data (experiment.run_jobs runs jobs in threads)
+    a = sp.csr_matrix(adj_mat, copy=True)
     a.eliminate_zeros()
     a.sort_indices()
     if a.shape != (n_sites, n_sites):
