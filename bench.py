@@ -962,9 +962,41 @@ def source_lik_leg(args, eng, gen, dev, stream, rank, world):
     secs = float(t[0])
     P, D, per_launch = algorithmic_bytes(a, B, True)
     launch_s = secs / K
-    del pool
+    # the by-site entry (the reference's Sample.source order, [B][N][F]): the same launches with
+    # the sources by site, transposed to positions on the device by the entry (source_to_pm_kernel)
+    c0 = pool[0]
+    src_site = torch.empty(B, args.sites, args.features, dtype=torch.uint8, device=dev)
+    eng.source_layout_device(B, c0["src_pm"].data_ptr(), src_site.data_ptr(), False)
+
+    def step_site():
+        eng.loglik_device(B, c0["zos"].data_ptr(), c0["w"].data_ptr(), c0["pg"].data_ptr(),
+                          c0["pz"].data_ptr(), c0["pf"].data_ptr() if c0["pf"] is not None else 0,
+                          src_site.data_ptr(), out[1].data_ptr(), validate=False, source_pm=False)
+    step_site()
+    torch.cuda.synchronize()
+    ref = out[1].clone()
+    step(0)
+    torch.cuda.synchronize()
+    if not torch.equal(out[0], ref):
+        raise SystemExit("source branch: by-site and by-position launches disagree")
+    ev0.record(stream)
+    for i in range(K):
+        step_site()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    t = torch.tensor([ev0.elapsed_time(ev1) / 1e3], dtype=torch.float64, device=dev)
+    if world > 1:
+        _all_reduce(t, dist.ReduceOp.MAX)
+    site_launch_s = float(t[0]) / K
+    site_kernels = eng.last_kernels()
+    del pool, src_site
     traffic, traffic_src = pmc_kernel_traffic(args, B, "lik_source_rc_kernel")
     return {"evals_per_sec": B * K * world / secs, "launch_us": launch_s * 1e6,
+            "by_site": {"launch_us": site_launch_s * 1e6, "kernels": site_kernels,
+                        "transpose_us_est": (site_launch_s - launch_s) * 1e6,
+                        "how": "the same launches with the sources by site ([B][N][F], the reference's "
+                               "order): sbz_loglik_batch_device transposes them to positions first; "
+                               "transpose_us_est = by-site launch - by-position launch"},
             "bytes_per_eval": P + D / B, "bytes_per_launch": per_launch,
             "achieved_GBs": per_launch / launch_s / 1e9,
             "frac": per_launch / launch_s / 1e9 / HBM_PEAK_GBS, "steps": K,

@@ -1168,6 +1168,83 @@ __global__ __launch_bounds__(256) void source_transpose_kernel(int N, int F, int
     }
 }
 
+// By-site sources [B][N][F] -> by-position [B][F][Np] (F a multiple of 4), the by-site entry's
+// transpose: one workgroup moves a tile of TR_P positions x 128 features (whole 128-B segments of
+// the site rows) through LDS laid out position-major, tile[p][fw] (row stride 33 words):
+// - read: 8 consecutive lanes take one site row's 128 B (16 B each, as 4 dwords), so a wave
+//   instruction reads 8 whole row segments; the writes tile[r][4 c + k] of a half-wave (rows
+//   r0 .. r0 + 3, chunks c = 0..7) fall on banks r + 4 c + k: 32 distinct;
+// - write: TR_P / 4 lanes per feature word; lane l reads the words of positions 4 l .. 4 l + 3,
+//   transposes the 4 x 4 bytes in registers (v_perm_b32) and stores one dword per feature row:
+//   each store is a coalesced TR_P-byte row segment.
+// A tile (x, y) and its neighbour (x, y + 1) share the boundary lines of unaligned site rows; their
+// linear block ids differ by gridDim.x (16 at Np = 2048), which keeps them on one XCD's L2.
+// cfg5, 256 chains (524 MB moved): 138.7 us for the round-5 kernel (64-feature tiles, byte LDS
+// reads), 92-94 us for this one at TR_P = 128 (5.6 TB/s; tools/ab_transpose.sh,
+// profiles/r06_transpose_ab.txt).
+#ifndef SBZ_TR_P
+#define SBZ_TR_P 128  // positions per tile (tools/ab_transpose.sh: 128 over 256 and 64)
+#endif
+constexpr int TR_P = SBZ_TR_P, TR_F = 128, TR_W = TR_F / 4, TR_S = TR_W + 1, TR_R = TR_P / 32;
+__global__ __launch_bounds__(256) void source_to_pm_kernel(int N, int F, int Np, const int *perm,
+                                                           const uint8_t *src, uint8_t *dst) {
+    __shared__ uint32_t tile[TR_P * TR_S];
+    const int tid = threadIdx.x;
+    const int p0 = blockIdx.x * TR_P, f0 = blockIdx.y * TR_F;
+    const size_t b = blockIdx.z;
+    const int c = tid & 7, rl = tid >> 3;  // 16-B chunk c of the rows of positions rl + 32 i
+    int rows[TR_R];
+#pragma unroll
+    for (int i = 0; i < TR_R; i++) {
+        const int p = p0 + rl + 32 * i;
+        rows[i] = p < N ? perm[p] : -1;
+    }
+    // (16-B loads of dword-aligned chunks: global loads need only dword alignment on gfx950)
+    typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+    uint32_t w[TR_R][4];
+#pragma unroll
+    for (int i = 0; i < TR_R; i++) {
+        const int fc = f0 + 16 * c;
+        const uint8_t *rp = src + (b * N + (size_t)max(rows[i], 0)) * F + min(fc, F - 16);
+        u32x4a v = {0u, 0u, 0u, 0u};
+        if (rows[i] >= 0 && fc < F) v = *reinterpret_cast<const u32x4a *>(rp);
+        // a chunk past the row's end (F - fc < 16 bytes, F a multiple of 4) was read from F - 16:
+        // shift its words down and zero the rest
+        const int sh = fc + 16 > F ? (fc + 16 - F) / 4 : 0;
+        const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; k++) w[i][k] = (k + sh < 4 && fc + 4 * k < F) ? vv[min(k + sh, 3)] : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < TR_R; i++)
+#pragma unroll
+        for (int k = 0; k < 4; k++) tile[(rl + 32 * i) * TR_S + 4 * c + k] = w[i][k];
+    __syncthreads();
+    // writes: TR_P / 4 lanes per feature word; 256 / (TR_P / 4) words at a time
+    constexpr int LPW = TR_P / 4, WPR = 256 / LPW;
+    const int ql = tid % LPW, fw0 = tid / LPW;
+    if (p0 + 4 * ql >= Np) return;  // (no barrier follows)
+    for (int fw = fw0; fw < TR_W; fw += WPR) {
+        const int fb = f0 + 4 * fw;
+        if (fb >= F) break;  // uniform
+        uint32_t q[4];  // positions 4 ql + j, bytes = features fb .. fb + 3
+#pragma unroll
+        for (int j = 0; j < 4; j++) q[j] = tile[(4 * ql + j) * TR_S + fw];
+        // o_i: feature fb + i, bytes = positions 4 lane .. + 3
+        const uint32_t a_lo = __builtin_amdgcn_perm(q[1], q[0], 0x05010400u);  // q0.0 q1.0 q0.1 q1.1
+        const uint32_t a_hi = __builtin_amdgcn_perm(q[1], q[0], 0x07030602u);  // q0.2 q1.2 q0.3 q1.3
+        const uint32_t b_lo = __builtin_amdgcn_perm(q[3], q[2], 0x05010400u);
+        const uint32_t b_hi = __builtin_amdgcn_perm(q[3], q[2], 0x07030602u);
+        const uint32_t o[4] = {__builtin_amdgcn_perm(b_lo, a_lo, 0x05040100u),
+                               __builtin_amdgcn_perm(b_lo, a_lo, 0x07060302u),
+                               __builtin_amdgcn_perm(b_hi, a_hi, 0x05040100u),
+                               __builtin_amdgcn_perm(b_hi, a_hi, 0x07060302u)};
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            *reinterpret_cast<uint32_t *>(dst + (b * F + fb + i) * Np + p0 + 4 * ql) = o[i];
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // Host side: kernel choice and launch
 // ------------------------------------------------------------------------------------------
@@ -1334,6 +1411,13 @@ int lik_configure(sbz_ctx *ctx) {
 
 int launch_source_transpose(sbz_ctx *ctx, int B, const uint8_t *src, uint8_t *dst, bool to_pm) {
     if (B <= 0) return SBZ_OK;
+    if (to_pm && ctx->d.n_features % 4 == 0 && ctx->d.n_features >= 16) {  // whole-line tiles
+        const dim3 g((ctx->Np + TR_P - 1) / TR_P, (ctx->d.n_features + TR_F - 1) / TR_F, B);
+        source_to_pm_kernel<<<g, 256, 0, ctx->stream>>>(ctx->d.n_sites, ctx->d.n_features, ctx->Np, ctx->d_perm,
+                                                         src, dst);
+        hipError_t e = hipGetLastError();
+        return e == hipSuccess ? SBZ_OK : hip_fail(ctx, e, "source_to_pm_kernel launch");
+    }
     const dim3 grid((ctx->Np + RP_T - 1) / RP_T, (ctx->d.n_features + RP_F - 1) / RP_F, B);
     if (to_pm)
         source_transpose_kernel<true><<<grid, 256, 0, ctx->stream>>>(ctx->d.n_sites, ctx->d.n_features, ctx->Np,
@@ -1403,7 +1487,8 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
             lds = source_rc_lds_bytes(d, ctx->C);
             const int W = tasks_per_chain(ctx, fn, lds, B);
             a.fpw = (F + W - 1) / W;
-            names = source_pm ? "lik_source_rc_kernel" : "source_transpose_kernel lik_source_rc_kernel";
+            names = source_pm ? "lik_source_rc_kernel"
+                    : (F % 4 == 0 && F >= 16 ? "source_to_pm_kernel lik_source_rc_kernel" : "source_transpose_kernel lik_source_rc_kernel");
         } else {
             fn = ctx->C == 3 ? reinterpret_cast<const void *>(&lik_source_generic_kernel<3>)
                              : reinterpret_cast<const void *>(&lik_source_generic_kernel<2>);
