@@ -297,7 +297,7 @@ int sbz_set_option(sbz_ctx *ctx, int32_t option, int64_t value) {
             ctx->mh_la = (int)value;
             return SBZ_OK;
         case SBZ_OPT_MH_GROUP:
-            if (value < 1 || value > 4) return fail(ctx, SBZ_EINVAL, "sampler move groups must be in 1..4");
+            if (value < 1 || value > 8) return fail(ctx, SBZ_EINVAL, "sampler move groups must be in 1..8");
             ctx->mh_group = (int)value;
             return SBZ_OK;
         default: return fail(ctx, SBZ_EINVAL, "unknown option " + std::to_string(option));

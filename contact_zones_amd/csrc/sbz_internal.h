@@ -78,7 +78,7 @@ struct sbz_ctx {
     int n_cu = 256;        // compute units of the device
     int src_waves = 0;     // SBZ_OPT_SRC_WAVES: waves per chain of the source-mode sampler (0: 8)
     int mh_la = 24;        // SBZ_OPT_MH_LOOKAHEAD: sampler proposals planned ahead per batch (1..24)
-    int mh_group = 4;      // SBZ_OPT_MH_GROUP: grouped planned parameter moves (1..4)
+    int mh_group = 8;      // SBZ_OPT_MH_GROUP: grouped planned parameter moves (1..8; at most the waves)
     int src_hbm = 0;       // SBZ_OPT_SRC_HBM 1: source-mode sampler keeps sources in HBM even when they fit LDS
     int src_pass_tables = 1;  // SBZ_OPT_SRC_PASS_TABLES 0: HBM-source sampler passes per cell, no count tables
     std::string last_kernels;  // sbz_last_kernels

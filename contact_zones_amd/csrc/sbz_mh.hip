@@ -962,9 +962,11 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
     // diagnostic builds (tools/build_mh_variant.sh NAME -DSBZ_MH_STAMP=K): the trace's ll column
     // holds shader-clock cycles per step instead (K = 1: the whole step, make_plans included;
     // 2: the grouped path's delta phase; 3: make_plans; a group's cycles are split evenly over its
-    // members; 4 / 5 / 6: wave 0's delta_param table build / gathers / log + sum, not split);
+    // members; 4 / 5 / 6: wave 0's delta_param table build / gathers / log + sum, not split; 7 / 8 /
+    // 9: a step of the sequential path (zone moves, unplanned moves): its move draw / proposal and
+    // delta / MH test and apply);
     // tools/mh_optime.py --stamps reads them
-    long long stamp_t0 = 0, stamp_plan = 0, stamp_d0 = 0, stamp_d1 = 0;
+    long long stamp_t0 = 0, stamp_plan = 0, stamp_d0 = 0, stamp_d1 = 0, stamp_p1 = 0, stamp_p3 = 0;
     double stamp_val = 0.0;
 #endif
     auto trace_step = [&](int st, int op_, bool acc) {
@@ -1340,6 +1342,9 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             poff = off;
         }
 
+#ifdef SBZ_MH_STAMP
+        stamp_p1 = clock64();
+#endif
         // ---- 2. Dirichlet proposal of the pair (zone_sampling.py:421-438, :537-569)
         fence_params();  // (planned parameter moves took the grouped path above)
         double nv0 = 0.0, nv1 = 0.0;
@@ -1406,6 +1411,9 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             dprior = uni(dprior + (geo_new - geo_cur));
         }
 
+#ifdef SBZ_MH_STAMP
+        stamp_p3 = clock64();
+#endif
         // ---- 4. metropolis_hastings_ratio (mcmc_generative.py:331-351, uniform priors)
         bool accept = false;
         if (log_q_back == -INFINITY) {
@@ -1469,7 +1477,14 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             bsync();
         }
 #ifdef SBZ_MH_STAMP
-        stamp_val = SBZ_MH_STAMP == 1 ? (double)(clock64() - stamp_t0) : SBZ_MH_STAMP == 3 ? (double)stamp_plan : 0.0;
+        {
+            const long long now = clock64();
+            stamp_val = SBZ_MH_STAMP == 1 ? (double)(now - stamp_t0)
+                      : SBZ_MH_STAMP == 3 ? (double)stamp_plan
+                      : SBZ_MH_STAMP == 7 ? (double)(stamp_p1 - stamp_t0)
+                      : SBZ_MH_STAMP == 8 ? (double)(stamp_p3 - stamp_p1)
+                      : SBZ_MH_STAMP == 9 ? (double)(now - stamp_p3) : 0.0;
+        }
 #endif
         trace_step(step, op, accept);
     }
@@ -1500,8 +1515,12 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
     }
 }
 
+// Waves per chain (one workgroup per chain): 8 since round 6, two per SIMD at <= 256 registers
+// per lane (2 spilled); with move groups of 8 the cfg5 default mix runs 2.99 us per step against
+// 3.23 for 4 waves with groups of 4 (tools/ab_mh_waves_r06.sh, profiles/r06_mh_ab.txt).  A/B builds:
+// tools/build_mh_variant.sh NAME -DSBZ_MH_WAVES=4.
 #ifndef SBZ_MH_WAVES
-#define SBZ_MH_WAVES 4  // A/B builds only (tools/build_mh_variant.sh NAME -DSBZ_MH_WAVES=8)
+#define SBZ_MH_WAVES 8
 #endif
 constexpr int MH_WAVES = SBZ_MH_WAVES;  // waves per chain (one workgroup per chain)
 

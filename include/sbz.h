@@ -120,8 +120,8 @@ int sbz_synchronize(sbz_ctx *ctx);
  *                             columns <= 192, and the LDS holds them); 0: per-cell passes
  *   SBZ_OPT_MH_GROUP          mixture sampler with Philox draws: planned parameter moves on pairwise
  *                             different features whose deltas are computed at once, one per wave,
- *                             1..4 (default 4; fewer when the per-wave cell tables do not fit the
- *                             LDS; trajectories do not depend on it)
+ *                             1..8 (default 8; at most the sampler's waves per chain, fewer when the
+ *                             per-wave cell tables do not fit the LDS; trajectories do not depend on it)
  * SBZ_EINVAL for an unknown option or a value out of range. */
 enum sbz_option {
     SBZ_OPT_LIK_TASKS_PER_CU = 1,

@@ -503,13 +503,13 @@ def test_options(gpu_available):
     assert {k: eng.get_option(k) for k in ("lik_tasks_per_cu", "lik_banked", "src_table", "src_waves",
                                            "src_hbm", "src_stage", "mh_lookahead", "mh_group")} == \
         {"lik_tasks_per_cu": 0, "lik_banked": 1, "src_table": 1, "src_waves": 0, "src_hbm": 0,
-         "src_stage": 1, "mh_lookahead": 24, "mh_group": 4}
+         "src_stage": 1, "mh_lookahead": 24, "mh_group": 8}
     ref = eng.loglik(zos, w, pg, pz, pf)
     for tpc in (1, 2, 4, 12):
         eng.set_option("lik_tasks_per_cu", tpc)
         _assert_close(eng.loglik(zos, w, pg, pz, pf), ref, tol=1e-14)
     for name, bad in (("lik_tasks_per_cu", -1), ("lik_banked", 2), ("src_waves", 3), ("mh_lookahead", 0),
-                      ("mh_lookahead", 25), ("mh_group", 0), ("mh_group", 5)):
+                      ("mh_lookahead", 25), ("mh_group", 0), ("mh_group", 9)):
         with pytest.raises(SbzError):
             eng.set_option(name, bad)
     with pytest.raises(ValueError):
