@@ -130,6 +130,35 @@ def test_bench_cpu_sampler_baseline_processes():
     assert r["value"] > 0 and len(r["steps_per_process"]) == 2 and min(r["steps_per_process"]) > 0
 
 
+def test_bench_cpu_source_sampler_baseline_processes():
+    """The SAMPLE_SOURCE = true sampler's CPU baseline: the restated step loop
+    with source resampling and the Gibbs operators drawing from their beta / Dirichlet
+    distributions (oracle/mh_numpy, DrawTape) in one child process per core, all reaped when it
+    returns: steps/s per core and all-core, the ESS of the traces, the container ratio to the
+    reference."""
+    import argparse
+    import bench
+    args = argparse.Namespace(sites=60, features=12, states=4, zones=2, families=2, zone_size=10,
+                              seed=3, cpu_procs=2)
+    r = bench.cpu_baseline_src_sampler(args, 0.5)
+    assert r["cores"] == 2 and r["kind"] == "port" and r["unit"] == "MH steps/s"
+    assert r["value"] > 0 and len(r["steps_per_process"]) == 2 and min(r["steps_per_process"]) > 0
+    assert r["restatement_over_reference"] > 0
+
+
+def test_bench_reaps_children():
+    """bench.reap_children ends and reports any process the bench left behind:
+    a sleeping child is found, terminated and reaped; a second call finds nothing."""
+    import subprocess
+    import sys
+    import bench
+    p = subprocess.Popen([sys.executable, "-c", "import time; time.sleep(60)"])
+    found = bench.reap_children()
+    assert [d["pid"] for d in found] == [p.pid]
+    assert p.poll() is not None
+    assert bench.reap_children() == []
+
+
 def test_bench_source_sampler_pmc_needs_the_same_kernel_sources(tmp_path, monkeypatch):
     """The source-mode leg reports PMC counters per chain-step only from a committed profile measured
     on the current kernel sources (its _meta.source_hash); an older build's profile is named, not
