@@ -963,7 +963,8 @@ def source_lik_leg(args, eng, gen, dev, stream, rank, world):
     P, D, per_launch = algorithmic_bytes(a, B, True)
     launch_s = secs / K
     # the by-site entry (the reference's Sample.source order, [B][N][F]): the same launches with
-    # the sources by site, transposed to positions on the device by the entry (source_to_pm_kernel)
+    # the sources by site, reordered by position on the device by the entry (source_to_pk_kernel:
+    # 2-bit planes, the default; with src_pack = 0 one byte per cell, source_to_pm_kernel)
     c0 = pool[0]
     src_site = torch.empty(B, args.sites, args.features, dtype=torch.uint8, device=dev)
     eng.source_layout_device(B, c0["src_pm"].data_ptr(), src_site.data_ptr(), False)
@@ -979,24 +980,37 @@ def source_lik_leg(args, eng, gen, dev, stream, rank, world):
     torch.cuda.synchronize()
     if not torch.equal(out[0], ref):
         raise SystemExit("source branch: by-site and by-position launches disagree")
-    ev0.record(stream)
-    for i in range(K):
-        step_site()
-    ev1.record(stream)
+
+    def time_site():
+        ev0.record(stream)
+        for i in range(K):
+            step_site()
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        t = torch.tensor([ev0.elapsed_time(ev1) / 1e3], dtype=torch.float64, device=dev)
+        if world > 1:
+            _all_reduce(t, dist.ReduceOp.MAX)
+        return float(t[0]) / K, eng.last_kernels()
+    site_launch_s, site_kernels = time_site()
+    eng.set_option("src_pack", 0)
+    step_site()
     torch.cuda.synchronize()
-    t = torch.tensor([ev0.elapsed_time(ev1) / 1e3], dtype=torch.float64, device=dev)
-    if world > 1:
-        _all_reduce(t, dist.ReduceOp.MAX)
-    site_launch_s = float(t[0]) / K
-    site_kernels = eng.last_kernels()
+    if not torch.equal(out[1], ref):
+        raise SystemExit("source branch: by-site launches with byte and 2-bit reorders disagree")
+    byte_launch_s, byte_kernels = time_site()
+    eng.set_option("src_pack", 1)
     del pool, src_site
     traffic, traffic_src = pmc_kernel_traffic(args, B, "lik_source_rc_kernel")
     return {"evals_per_sec": B * K * world / secs, "launch_us": launch_s * 1e6,
             "by_site": {"launch_us": site_launch_s * 1e6, "kernels": site_kernels,
-                        "transpose_us_est": (site_launch_s - launch_s) * 1e6,
+                        "reorder_us_est": (site_launch_s - launch_s) * 1e6,
+                        "byte_reorder": {"launch_us": byte_launch_s * 1e6, "kernels": byte_kernels,
+                                         "reorder_us_est": (byte_launch_s - launch_s) * 1e6},
                         "how": "the same launches with the sources by site ([B][N][F], the reference's "
-                               "order): sbz_loglik_batch_device transposes them to positions first; "
-                               "transpose_us_est = by-site launch - by-position launch"},
+                               "order): sbz_loglik_batch_device reorders them by position first, into "
+                               "2-bit planes (default) or bytes (src_pack = 0, 'byte_reorder'); "
+                               "reorder_us_est = by-site launch - by-position launch; all three "
+                               "launches give bit-identical values (checked)"},
             "bytes_per_eval": P + D / B, "bytes_per_launch": per_launch,
             "achieved_GBs": per_launch / launch_s / 1e9,
             "frac": per_launch / launch_s / 1e9 / HBM_PEAK_GBS, "steps": K,

@@ -16,7 +16,7 @@ SBZ_SOURCE_BY_SITE = 0
 SBZ_SOURCE_BY_POSITION = 1
 # sbz_option (include/sbz.h): name -> id
 OPTIONS = {"lik_tasks_per_cu": 1, "lik_banked": 2, "src_table": 3, "src_waves": 4, "src_hbm": 5,
-           "src_stage": 6, "mh_lookahead": 7, "src_pass_tables": 8, "mh_group": 9}
+           "src_stage": 6, "mh_lookahead": 7, "src_pass_tables": 8, "mh_group": 9, "src_pack": 10}
 ERRORS = {-1: "SBZ_EINVAL", -2: "SBZ_EHIP", -3: "SBZ_ENOMEM", -4: "SBZ_ESTATE"}
 
 

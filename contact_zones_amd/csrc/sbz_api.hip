@@ -300,6 +300,7 @@ int sbz_set_option(sbz_ctx *ctx, int32_t option, int64_t value) {
             if (value < 1 || value > 8) return fail(ctx, SBZ_EINVAL, "sampler move groups must be in 1..8");
             ctx->mh_group = (int)value;
             return SBZ_OK;
+        case SBZ_OPT_SRC_PACK: return flag(ctx->src_pack);
         default: return fail(ctx, SBZ_EINVAL, "unknown option " + std::to_string(option));
     }
 }
@@ -316,6 +317,7 @@ int sbz_get_option(const sbz_ctx *ctx, int32_t option, int64_t *value) {
         case SBZ_OPT_MH_LOOKAHEAD: *value = ctx->mh_la; return SBZ_OK;
         case SBZ_OPT_SRC_PASS_TABLES: *value = ctx->src_pass_tables; return SBZ_OK;
         case SBZ_OPT_MH_GROUP: *value = ctx->mh_group; return SBZ_OK;
+        case SBZ_OPT_SRC_PACK: *value = ctx->src_pack; return SBZ_OK;
         default: return SBZ_EINVAL;
     }
 }

@@ -35,6 +35,7 @@ struct LikArgs {
     const double *pf;       // [B][Fam][F][S] (C == 3 only)
     const uint8_t *src_pm;  // [B][F][Np] component per cell by position (position-major), or nullptr
     const uint8_t *src_rm;  // [B][N][F]  the caller's sources by site (lik_source_generic_kernel)
+    int pk_row;             // src_pm holds 2-bit planes (source_to_pk_kernel): bytes per feature row
     double *partial;        // [B][W]     task partial sums
     unsigned *ticket;       // [B]        finished tasks per chain (0 between launches)
     unsigned *zflag;        // [B]        source branch: a task saw a zero selected weight (0
@@ -79,6 +80,7 @@ struct sbz_ctx {
     int src_waves = 0;     // SBZ_OPT_SRC_WAVES: waves per chain of the source-mode sampler (0: 8)
     int mh_la = 24;        // SBZ_OPT_MH_LOOKAHEAD: sampler proposals planned ahead per batch (1..24)
     int mh_group = 8;      // SBZ_OPT_MH_GROUP: grouped planned parameter moves (1..8; at most the waves)
+    int src_pack = 1;      // SBZ_OPT_SRC_PACK 0: by-site likelihood sources reordered into bytes, not bit planes
     int src_hbm = 0;       // SBZ_OPT_SRC_HBM 1: source-mode sampler keeps sources in HBM even when they fit LDS
     int src_pass_tables = 1;  // SBZ_OPT_SRC_PASS_TABLES 0: HBM-source sampler passes per cell, no count tables
     std::string last_kernels;  // sbz_last_kernels

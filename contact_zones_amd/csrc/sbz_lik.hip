@@ -748,10 +748,18 @@ constexpr int SRC_NWC = 32;  // features per normalised-weight batch
 #ifndef SBZ_SRC_RC_WAVES
 #define SBZ_SRC_RC_WAVES 2  // launch bound: waves per SIMD (3 spills: 262 vs 246 us per launch)
 #endif
-template <int C, int SPL, bool XS8>
+// PK: the sources come as 2-bit planes (source_to_pk_kernel, the by-site entry): per feature row
+// and lane, one dword pair (lo, hi) per 8 position groups, bit 8 j + kk of lo / hi = bit 0 / 1 of
+// the component at position 4 lane + 256 (8 kb + kk) + j of the chunk; pair (chunk, kb, lane) at
+// byte ((chunk * NOB + kb) * 64 + lane) * 8 of the row (a.pk_row bytes).  A quarter of the bytes
+// the by-position layout streams, and the same two selector words per group.
+template <int C, int SPL, bool XS8, bool PK = false>
 __global__ __launch_bounds__(WAVE, SBZ_SRC_RC_WAVES) void lik_source_rc_kernel(LikArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     constexpr int NO = SPL / 4;
+    constexpr int KP = NO < 8 ? NO : 8;  // PK: position groups per dword pair
+    constexpr int NOB = NO / KP;         // PK: dword pairs per lane, feature and chunk
+    static_assert(!PK || NO >= 4, "2-bit planes need 16 sites per lane or more");
     const int lane = threadIdx.x;
     const int b = blockIdx.y;
     const int fa = blockIdx.x * a.fpw;
@@ -788,8 +796,9 @@ __global__ __launch_bounds__(WAVE, SBZ_SRC_RC_WAVES) void lik_source_rc_kernel(L
                                                                         (int)((uint32_t)max(Fam, 1) * zfs * 8u), 0x00020000);
     const __amdgpu_buffer_rsrc_t robs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(a.obs_fm), (short)0,
                                                                           a.F * a.Np, 0x00020000);
+    const int src_row = PK ? a.pk_row : a.Np;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t *>(a.src_pm + (size_t)b * a.F * a.Np), (short)0, a.F * a.Np, 0x00020000);
+        const_cast<uint8_t *>(a.src_pm + (size_t)b * a.F * src_row), (short)0, a.F * src_row, 0x00020000);
     // lane offsets (bytes) of its parameter rows; rows past Z / Fam read a valid row (unused)
     const uint32_t vg = na ? OOB : lxc * 8u;
     uint32_t vz[2], vf[2];
@@ -813,6 +822,22 @@ __global__ __launch_bounds__(WAVE, SBZ_SRC_RC_WAVES) void lik_source_rc_kernel(L
     auto load_words = [&](const __amdgpu_buffer_rsrc_t &rs, int f, int c0, uint32_t (&o)[NO]) {
 #pragma unroll
         for (int k = 0; k < NO; k++) o[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, lane * 4, f * a.Np + c0 + 256 * k, 0);
+    };
+    // the sources of feature f in the chunk at c0: NO words (by position) or NOB (lo, hi) pairs
+    auto load_src = [&](int f, int c0, uint32_t (&o)[NO]) {
+        if constexpr (PK) {
+            const int cb = c0 / (SPL * WAVE);
+#pragma unroll
+            for (int kb = 0; kb < NOB; kb++) {
+                const unsigned long long v = __builtin_bit_cast(
+                    unsigned long long,
+                    __builtin_amdgcn_raw_buffer_load_b64(rsrc, lane * 8, f * a.pk_row + (cb * NOB + kb) * WAVE * 8, 0));
+                o[2 * kb] = (uint32_t)v;
+                o[2 * kb + 1] = (uint32_t)(v >> 32);
+            }
+        } else {
+            load_words(rsrc, f, c0, o);
+        }
     };
 
     for (int x = lane; x < S1; x += WAVE) tab[rn * S1 + x] = 1.0;  // padding positions
@@ -917,10 +942,18 @@ __global__ __launch_bounds__(WAVE, SBZ_SRC_RC_WAVES) void lik_source_rc_kernel(L
             if (q < NO) renorm(m[q], e);
     };
     // the 4 table rows of position group k from its 4 component bytes
-    auto rows_of = [&](int k, uint32_t cw) -> uint32_t {
-        const uint32_t r01 = __builtin_amdgcn_perm(M1[k], M0[k], ((cw & 0x01010101u) << 2) + 0x03020100u);
+    auto rows_of = [&](int k, const uint32_t (&sb)[NO]) -> uint32_t {
+        uint32_t s0, s1;  // bit 0 / bit 1 of the 4 components, each moved to bit 2 of its byte
+        if constexpr (PK) {
+            s0 = ((sb[2 * (k / KP)] >> (k % KP)) & 0x01010101u) << 2;
+            s1 = ((sb[2 * (k / KP) + 1] >> (k % KP)) & 0x01010101u) << 2;
+        } else {
+            s0 = (sb[k] & 0x01010101u) << 2;
+            s1 = (sb[k] & 0x02020202u) << 1;
+        }
+        const uint32_t r01 = __builtin_amdgcn_perm(M1[k], M0[k], s0 + 0x03020100u);
         if (C == 2) return r01;
-        return __builtin_amdgcn_perm(M2[k], r01, ((cw & 0x02020202u) << 1) + 0x03020100u);
+        return __builtin_amdgcn_perm(M2[k], r01, s1 + 0x03020100u);
     };
     auto feature = [&](int f, int c0, bool live, const SrcParams &cur, const uint32_t (&ob)[NO],
                        const uint32_t (&sb)[NO], SrcParams &fill, uint32_t (&ofill)[NO], uint32_t (&sfill)[NO]) {
@@ -931,11 +964,11 @@ __global__ __launch_bounds__(WAVE, SBZ_SRC_RC_WAVES) void lik_source_rc_kernel(L
         const int fn = min(f + 1, fb - 1);
         load(fn, fill);
         load_words(robs, fn, c0, ofill);
-        load_words(rsrc, fn, c0, sfill);
+        load_src(fn, c0, sfill);
         if (!live) return;
         uint32_t rw[NO];
 #pragma unroll
-        for (int k = 0; k < NO; k++) rw[k] = rows_of(k, sb[k]);
+        for (int k = 0; k < NO; k++) rw[k] = rows_of(k, sb);
         auto addr = [&](int k, int j) {
             const uint32_t xb = (ob[k] >> (8 * j)) & 0xffu;
             const uint32_t rr = (rw[k] >> (8 * j)) & 0xffu;
@@ -1014,7 +1047,7 @@ __global__ __launch_bounds__(WAVE, SBZ_SRC_RC_WAVES) void lik_source_rc_kernel(L
             }
             load(fa, P[0]);
             load_words(robs, fa, c0, O[0]);
-            load_words(rsrc, fa, c0, R[0]);
+            load_src(fa, c0, R[0]);
 #pragma unroll
             for (int k = 0; k < NO; k++) {
                 uint32_t m0 = 0, m1 = 0, m2 = 0;
@@ -1245,6 +1278,93 @@ __global__ __launch_bounds__(256) void source_to_pm_kernel(int N, int F, int Np,
     }
 }
 
+// By-site sources [B][N][F] -> 2-bit planes by position (F a multiple of 4, SPL >= 16), the layout
+// lik_source_rc_kernel<.., PK = true> reads: per feature row, dword pair q = (chunk * NOB + kb) * 64
+// + lane holds, at bit 8 j + kk of its lo / hi word, bit 0 / 1 of the component at position
+// chunk * 64 SPL + 4 lane + 256 (KP kb + kk) + j (KP = min(SPL / 4, 8) groups per pair).  The row
+// is SPL / 2 ... 4 bytes per 16 positions: a quarter of the by-position layout's bytes at SPL = 32.
+// One workgroup covers 64 / KP consecutive pairs (lanes) of one (chunk, kb) and 128 features: its
+// 256 positions (KP runs of 256 / KP) are read as whole 128-B row segments into LDS as in
+// source_to_pm_kernel; then thread (feature word fw, pair l) reads the KP x 4 words of its
+// positions, transposes each 4 x 4 byte block (v_perm_b32) and slides bits 0 / 1 of each
+// feature's bytes into its planes; 8 consecutive lanes store 8 consecutive pairs of one row.
+// Padding positions (p >= N) hold 0 (the kernel maps them to the neutral row whatever they hold).
+#ifndef SBZ_PK_P
+#define SBZ_PK_P 256  // positions per tile
+#endif
+#ifndef SBZ_PK_F
+#define SBZ_PK_F 128  // features per tile (64 or 128)
+#endif
+constexpr int PK_P = SBZ_PK_P, PK_F = SBZ_PK_F, PK_W = PK_F / 4, PK_S = PK_W + 1;
+template <int KP>
+__global__ __launch_bounds__(256) void source_to_pk_kernel(int N, int F, int Np, int spl, int pk_row,
+                                                           const int *perm, const uint8_t *src, uint8_t *dst) {
+    constexpr int LT = PK_P / (4 * KP);           // pairs (lanes) per tile
+    constexpr int LPR = PK_F / 16, RPP = 256 / LPR, NPASS = PK_P / RPP;  // row loads: 16 B per lane
+    __shared__ uint32_t tile[PK_P * PK_S];
+    const int tid = threadIdx.x;
+    const int q0 = blockIdx.x * LT;  // first pair of the tile: (chunk * NOB + kb) * 64 + l0
+    const int nob = spl / 4 / KP;
+    const int cb = q0 / 64, l0 = q0 % 64;
+    const int chunk = cb / nob, kb = cb % nob;
+    const int pbase = chunk * 64 * spl + 4 * l0 + 256 * KP * kb;
+    const int f0 = blockIdx.y * PK_F;
+    const size_t b = blockIdx.z;
+    // tile row r: run kk = r / (4 LT), u = r % (4 LT) -> position pbase + 256 kk + u
+    auto pos_of = [&](int r) { return pbase + 256 * (r / (4 * LT)) + r % (4 * LT); };
+    const int c = tid % LPR, rl = tid / LPR;
+    const int fc = f0 + 16 * c;
+    typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+    uint32_t w[NPASS][4];
+#pragma unroll
+    for (int i = 0; i < NPASS; i++) {
+        const int p = pos_of(rl + RPP * i);
+        const int row = p < N ? perm[p] : -1;
+        u32x4a v = {0u, 0u, 0u, 0u};
+        if (row >= 0 && fc < F) v = *reinterpret_cast<const u32x4a *>(src + (b * N + (size_t)row) * F + min(fc, F - 16));
+        const int sh = fc + 16 > F ? (fc + 16 - F) / 4 : 0;  // a chunk past the row's end: see source_to_pm_kernel
+        const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; k++) w[i][k] = (k + sh < 4 && fc + 4 * k < F) ? vv[min(k + sh, 3)] : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < NPASS; i++)
+#pragma unroll
+        for (int k = 0; k < 4; k++) tile[(rl + RPP * i) * PK_S + 4 * c + k] = w[i][k];
+    __syncthreads();
+    for (int t = tid; t < PK_W * LT; t += 256) {
+        const int l = t % LT, fw = t / LT;
+        const int fb = f0 + 4 * fw;
+        if (fb >= F) break;  // t grows with fw
+        uint32_t lo[4] = {0u, 0u, 0u, 0u}, hi[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int kk = 0; kk < KP; kk++) {
+            uint32_t q[4];  // positions 4 l + j of run kk; bytes = features fb .. fb + 3
+#pragma unroll
+            for (int j = 0; j < 4; j++) q[j] = tile[(kk * 4 * LT + 4 * l + j) * PK_S + fw];
+            const uint32_t a_lo = __builtin_amdgcn_perm(q[1], q[0], 0x05010400u);
+            const uint32_t a_hi = __builtin_amdgcn_perm(q[1], q[0], 0x07030602u);
+            const uint32_t b_lo = __builtin_amdgcn_perm(q[3], q[2], 0x05010400u);
+            const uint32_t b_hi = __builtin_amdgcn_perm(q[3], q[2], 0x07030602u);
+            const uint32_t o[4] = {__builtin_amdgcn_perm(b_lo, a_lo, 0x05040100u),
+                                   __builtin_amdgcn_perm(b_lo, a_lo, 0x07060302u),
+                                   __builtin_amdgcn_perm(b_hi, a_hi, 0x05040100u),
+                                   __builtin_amdgcn_perm(b_hi, a_hi, 0x07060302u)};
+#pragma unroll
+            for (int i = 0; i < 4; i++) {  // o[i]: feature fb + i, byte j = position 4 l + j
+                lo[i] |= (o[i] & 0x01010101u) << kk;
+                hi[i] |= ((o[i] >> 1) & 0x01010101u) << kk;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            if (fb + i >= F) break;
+            const unsigned long long v = (unsigned long long)lo[i] | ((unsigned long long)hi[i] << 32);
+            *reinterpret_cast<unsigned long long *>(dst + (b * F + fb + i) * (size_t)pk_row + (size_t)(q0 + l) * 8) = v;
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // Host side: kernel choice and launch
 // ------------------------------------------------------------------------------------------
@@ -1301,7 +1421,13 @@ size_t source_rc_lds_bytes(const sbz_dims &d, int C) {
     return ((((rows * S1) + 1) & ~(size_t)1) + (size_t)SRC_NWC * 8 + WAVE) * 8 + ((rows + 7) & ~(size_t)7);
 }
 template <int C>
-const void *source_rc_kernel(int spl, bool xs8) {
+const void *source_rc_kernel(int spl, bool xs8, bool pk = false) {
+    if (pk) {  // 2-bit planes (sites per lane 16 or 32)
+        if (spl == 16) return xs8 ? reinterpret_cast<const void *>(&lik_source_rc_kernel<C, 16, true, true>)
+                                  : reinterpret_cast<const void *>(&lik_source_rc_kernel<C, 16, false, true>);
+        return xs8 ? reinterpret_cast<const void *>(&lik_source_rc_kernel<C, 32, true, true>)
+                   : reinterpret_cast<const void *>(&lik_source_rc_kernel<C, 32, false, true>);
+    }
     if (xs8) {
         switch (spl) {
             case 4: return reinterpret_cast<const void *>(&lik_source_rc_kernel<C, 4, true>);
@@ -1323,7 +1449,21 @@ void configure_source(std::vector<const void *> &v) {
     for (int spl = 4; spl <= 32; spl *= 2) {
         v.push_back(source_rc_kernel<C>(spl, true));
         v.push_back(source_rc_kernel<C>(spl, false));
+        if (spl >= 16) {
+            v.push_back(source_rc_kernel<C>(spl, true, true));
+            v.push_back(source_rc_kernel<C>(spl, false, true));
+        }
     }
+}
+
+// the by-site entry reorders its sources into 2-bit planes (source_to_pk_kernel)
+bool source_pk_applies(const sbz_ctx *ctx) {
+    return ctx->src_pack && ctx->spl >= 16 && ctx->d.n_features % 4 == 0 && ctx->d.n_features >= 16;
+}
+// bytes per feature row of the 2-bit planes: 8 per lane and pair, NOB pairs per chunk
+int source_pk_row(const sbz_ctx *ctx) {
+    const int no = ctx->spl / 4, kp = no < 8 ? no : 8;
+    return ctx->Np / (64 * ctx->spl) * (no / kp) * 64 * 8;
 }
 
 // How the mixture branch runs for these dims: table path with FR family registers (banked or
@@ -1409,6 +1549,20 @@ int lik_configure(sbz_ctx *ctx) {
     return SBZ_OK;
 }
 
+int launch_source_pack(sbz_ctx *ctx, int B, const uint8_t *src, uint8_t *dst) {
+    const int no = ctx->spl / 4, kp = no < 8 ? no : 8;
+    const int pairs = source_pk_row(ctx) / 8;
+    const dim3 g(pairs / (PK_P / (4 * kp)), (ctx->d.n_features + PK_F - 1) / PK_F, B);
+    if (kp == 8)
+        source_to_pk_kernel<8><<<g, 256, 0, ctx->stream>>>(ctx->d.n_sites, ctx->d.n_features, ctx->Np, ctx->spl,
+                                                            source_pk_row(ctx), ctx->d_perm, src, dst);
+    else
+        source_to_pk_kernel<4><<<g, 256, 0, ctx->stream>>>(ctx->d.n_sites, ctx->d.n_features, ctx->Np, ctx->spl,
+                                                            source_pk_row(ctx), ctx->d_perm, src, dst);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? SBZ_OK : hip_fail(ctx, e, "source_to_pk_kernel launch");
+}
+
 int launch_source_transpose(sbz_ctx *ctx, int B, const uint8_t *src, uint8_t *dst, bool to_pm) {
     if (B <= 0) return SBZ_OK;
     if (to_pm && ctx->d.n_features % 4 == 0 && ctx->d.n_features >= 16) {  // whole-line tiles
@@ -1463,7 +1617,7 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
     const void *fn = nullptr;
     size_t lds = 0;
     const char *names = nullptr;
-    bool src_rc = false;
+    bool src_rc = false, pk = false;
     int rc;
     if (!src_mode) {
         const MixPlan plan = plan_mixture(d, ctx->C);
@@ -1482,12 +1636,14 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
     } else {
         src_rc = ctx->src_rc && source_rc_applies(d, ctx->C) && source_rc_lds_bytes(d, ctx->C) <= 64 * 1024;
         if (src_rc) {
-            fn = ctx->C == 3 ? source_rc_kernel<3>(ctx->spl, ctx->xs8 != 0)
-                             : source_rc_kernel<2>(ctx->spl, ctx->xs8 != 0);
+            pk = !source_pm && source_pk_applies(ctx);
+            fn = ctx->C == 3 ? source_rc_kernel<3>(ctx->spl, ctx->xs8 != 0, pk)
+                             : source_rc_kernel<2>(ctx->spl, ctx->xs8 != 0, pk);
             lds = source_rc_lds_bytes(d, ctx->C);
             const int W = tasks_per_chain(ctx, fn, lds, B);
             a.fpw = (F + W - 1) / W;
             names = source_pm ? "lik_source_rc_kernel"
+                    : pk ? "source_to_pk_kernel lik_source_rc_kernel<planes>"
                     : (F % 4 == 0 && F >= 16 ? "source_to_pm_kernel lik_source_rc_kernel" : "source_transpose_kernel lik_source_rc_kernel");
         } else {
             fn = ctx->C == 3 ? reinterpret_cast<const void *>(&lik_source_generic_kernel<3>)
@@ -1530,6 +1686,13 @@ int launch_loglik(sbz_ctx *ctx, int B, const uint8_t *zone, const double *w, con
     if (src_rc) {
         if (source_pm) {
             a.src_pm = source;
+        } else if (pk) {  // the reference layout: reordered into 2-bit planes by position first
+            a.pk_row = source_pk_row(ctx);
+            rc = ensure(ctx, ctx->src_t, (size_t)B * F * a.pk_row);
+            if (rc) return rc;
+            rc = launch_source_pack(ctx, B, source, static_cast<uint8_t *>(ctx->src_t.ptr));
+            if (rc) return rc;
+            a.src_pm = static_cast<const uint8_t *>(ctx->src_t.ptr);
         } else {  // the reference layout: transposed to the position-major one first
             rc = ensure(ctx, ctx->src_t, (size_t)B * F * ctx->Np);
             if (rc) return rc;

@@ -122,6 +122,11 @@ int sbz_synchronize(sbz_ctx *ctx);
  *                             different features whose deltas are computed at once, one per wave,
  *                             1..8 (default 8; at most the sampler's waves per chain, fewer when the
  *                             per-wave cell tables do not fit the LDS; trajectories do not depend on it)
+ *   SBZ_OPT_SRC_PACK          1 (default): sbz_loglik_batch / sbz_loglik_batch_device with by-site
+ *                             sources on the table kernel, N > 512 and F a multiple of 4 (F >= 16),
+ *                             reorder the sources into 2-bit component planes by position before the
+ *                             launch; 0: into one byte per cell (the by-position layout).  Results do
+ *                             not depend on it.
  * SBZ_EINVAL for an unknown option or a value out of range. */
 enum sbz_option {
     SBZ_OPT_LIK_TASKS_PER_CU = 1,
@@ -133,6 +138,7 @@ enum sbz_option {
     SBZ_OPT_MH_LOOKAHEAD = 7,
     SBZ_OPT_SRC_PASS_TABLES = 8,
     SBZ_OPT_MH_GROUP = 9,
+    SBZ_OPT_SRC_PACK = 10,
 };
 int sbz_set_option(sbz_ctx *ctx, int32_t option, int64_t value);
 int sbz_get_option(const sbz_ctx *ctx, int32_t option, int64_t *value);
@@ -266,7 +272,9 @@ typedef struct sbz_chains {
                                          when every prior term is 0 */
     uint8_t *source;                  /* in/out (sample_source): component of each observation,
                                          0 global, 1 zone, 2 family (Sample.source), in the layout
-                                         source_layout names */
+                                         source_layout names.  By position, the padding columns
+                                         (p >= N) may be rewritten with 0 (the HBM-sources kernel
+                                         with pass tables copies whole rows back); never read. */
     /* sample_source only: the reference's Gibbs operators on p_global / p_zones / p_families
      * change the chain's Sample in place (zone_sampling.py:333-400), so the parameter arrays of a
      * logged sample (mcmc_generative.py:353-367 keeps references) go on changing until an

@@ -501,16 +501,63 @@ def test_options(gpu_available):
     obs, fam, zos, w, pg, pz, pf, _ = _random_batch(rng, 200, 100, 5, 2, 2, 64, True, 25)
     eng = LikelihoodEngine(obs, fam, 5, 2, 2, True)
     assert {k: eng.get_option(k) for k in ("lik_tasks_per_cu", "lik_banked", "src_table", "src_waves",
-                                           "src_hbm", "src_stage", "mh_lookahead", "mh_group")} == \
+                                           "src_hbm", "src_stage", "mh_lookahead", "mh_group", "src_pack")} == \
         {"lik_tasks_per_cu": 0, "lik_banked": 1, "src_table": 1, "src_waves": 0, "src_hbm": 0,
-         "src_stage": 1, "mh_lookahead": 24, "mh_group": 8}
+         "src_stage": 1, "mh_lookahead": 24, "mh_group": 8, "src_pack": 1}
     ref = eng.loglik(zos, w, pg, pz, pf)
     for tpc in (1, 2, 4, 12):
         eng.set_option("lik_tasks_per_cu", tpc)
         _assert_close(eng.loglik(zos, w, pg, pz, pf), ref, tol=1e-14)
     for name, bad in (("lik_tasks_per_cu", -1), ("lik_banked", 2), ("src_waves", 3), ("mh_lookahead", 0),
-                      ("mh_lookahead", 25), ("mh_group", 0), ("mh_group", 9)):
+                      ("mh_lookahead", 25), ("mh_group", 0), ("mh_group", 9), ("src_pack", 2)):
         with pytest.raises(SbzError):
             eng.set_option(name, bad)
     with pytest.raises(ValueError):
         eng.set_option("no_such_option", 1)
+
+
+@pytest.mark.parametrize("shape", [
+    (700, 92, 5, 3, 2, 6, True, 40),        # 16 sites per lane (planes of 4 groups)
+    (1100, 64, 10, 8, 4, 6, True, 30),      # 32 sites per lane, one 2048-position chunk
+    (3000, 20, 4, 2, 0, 5, False, 200),     # two chunks, no families, C = 2
+    (2000, 500, 10, 8, 4, 3, True, 50),     # cfg5
+    (600, 16, 3, 1, 1, 4, True, 100),       # F = 16: one feature tile, 128-B loads past the row end
+])
+def test_source_by_site_planes(gpu_available, shape):
+    """The by-site source entry (sbz_loglik_batch, the reference's Sample.source order) where it
+    reorders the sources into 2-bit planes (source_to_pk_kernel, option src_pack = 1, the default
+    for N > 512 and F a multiple of 4): bit-identical to the byte reorder (src_pack = 0; the same
+    table rows in the same order), within 1e-12 of the C oracle, through the host and the device
+    entries, with a zero selected weight (-inf) and tiny parameters (task re-run) in the batch."""
+    import torch
+    from contact_zones_amd.likelihood import LikelihoodEngine
+    from oracle import oracle_c
+    N, F, S, Z, Fam, B, inh, zs = shape
+    rng = np.random.default_rng(N + 7 * F)
+    obs, fam, zos, w, pg, pz, pf, src = _random_batch(rng, N, F, S, Z, Fam, B, inh, zs)
+    if not inh:
+        src = np.minimum(src, 1).astype(np.uint8)
+    s1 = int(np.flatnonzero(zos[1] != 255)[0])
+    w[1, F - 1, 1] = 0.0                # chain 1: a zoned site selects a zone weight of 0 -> -inf
+    src[1, s1, F - 1] = 1
+    pg[2, :, 1] = 1e-200                # chain 2: tiny parameters, products underflow
+    eng = LikelihoodEngine(obs, fam, S, Z, Fam, inh)
+    planes = eng.loglik(zos, w, pg, pz, pf, src)
+    assert eng.last_kernels() == "source_to_pk_kernel lik_source_rc_kernel<planes>"
+    eng.set_option("src_pack", 0)
+    byte = eng.loglik(zos, w, pg, pz, pf, src)
+    assert eng.last_kernels() == "source_to_pm_kernel lik_source_rc_kernel"
+    np.testing.assert_array_equal(planes, byte)
+    ref = oracle_c.loglik_batch(obs, fam, zos, w, pg, pz, pf, source=src, inheritance=inh)
+    assert ref[1] == -np.inf
+    _assert_close(planes, ref, tol=1e-12)
+    eng.set_option("src_pack", 1)
+    dev = torch.device("cuda:0")
+    t = [torch.from_numpy(np.ascontiguousarray(v)).to(dev) if v is not None else None
+         for v in (zos, w, pg, pz, pf, src)]
+    out = torch.empty(B, dtype=torch.float64, device=dev)
+    eng.set_stream(torch.cuda.current_stream().cuda_stream)
+    eng.loglik_device(B, *[x.data_ptr() if x is not None else 0 for x in t], out.data_ptr())
+    torch.cuda.synchronize()
+    assert eng.last_kernels() == "source_to_pk_kernel lik_source_rc_kernel<planes>"
+    np.testing.assert_array_equal(out.cpu().numpy(), planes)

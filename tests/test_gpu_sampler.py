@@ -255,7 +255,7 @@ def test_philox_planned_proposals_do_not_change_trajectories(gpu_available, case
     import torch
     fx = load_golden(case)
     runs = []
-    for la, grp in ((1, 4), (24, 4), (6, 4), (24, 1), (24, 2), (6, 3)):
+    for la, grp in ((1, 4), (24, 4), (6, 4), (24, 1), (24, 2), (6, 3), (24, 8), (6, 8), (24, 7), (12, 5)):
         eng, smp, st = _setup(fx, {"mh_lookahead": la, "mh_group": grp})
         outs = [smp.run(st, n, fx["max_size"], fx["p_grow_connected"], seed=4242, chain_id0=3, trace=True)
                 for n in (700, 5, 1301)]

@@ -148,13 +148,15 @@ def test_bench_cpu_source_sampler_baseline_processes():
 
 def test_bench_reaps_children():
     """bench.reap_children ends and reports any process the bench left behind:
-    a sleeping child is found, terminated and reaped; a second call finds nothing."""
+    a sleeping child is found, terminated and reaped; a second call finds nothing.  (Inside the whole
+    suite the test process may hold other children of earlier tests, e.g. a process pool's workers,
+    which the first call ends too.)"""
     import subprocess
     import sys
     import bench
     p = subprocess.Popen([sys.executable, "-c", "import time; time.sleep(60)"])
     found = bench.reap_children()
-    assert [d["pid"] for d in found] == [p.pid]
+    assert p.pid in [d["pid"] for d in found]
     assert p.poll() is not None
     assert bench.reap_children() == []
 

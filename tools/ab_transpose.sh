@@ -8,5 +8,5 @@ for v in ${VARIANTS:-default}; do
   SBZ_LIB_PATH=$lib timeout -k 10 300 python bench.py $Q > gpurun_out/ab_tr_$v.json 2> gpurun_out/ab_tr_$v.err || { tail -5 gpurun_out/ab_tr_$v.err; exit 1; }
   python -c "
 import json; d=json.loads(open('gpurun_out/ab_tr_$v.json').read().strip().splitlines()[-1])['likelihood_source_branch']
-print('$v', 'by-position %.1f us' % d['launch_us'], 'by-site %.1f us' % d['by_site']['launch_us'], 'transpose est %.1f us' % d['by_site']['transpose_us_est'])"
+print('$v', 'by-position %.1f us' % d['launch_us'], 'by-site %.1f us' % d['by_site']['launch_us'], 'transpose est %.1f us' % d['by_site']['reorder_us_est'])"
 done
