@@ -1293,7 +1293,7 @@ __global__ __launch_bounds__(256) void source_to_pm_kernel(int N, int F, int Np,
 #define SBZ_PK_P 256  // positions per tile
 #endif
 #ifndef SBZ_PK_F
-#define SBZ_PK_F 128  // features per tile (64 or 128)
+#define SBZ_PK_F 64  // features per tile (32, 64 or 128; tools/ab_pack.sh: 64)
 #endif
 constexpr int PK_P = SBZ_PK_P, PK_F = SBZ_PK_F, PK_W = PK_F / 4, PK_S = PK_W + 1;
 template <int KP>

@@ -383,9 +383,10 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
         bsync();
         return nsel;
     };
-    // mark nb[t] = stamp for every site t adjacent to a member of zone z: the members are
-    // compacted into lst, then every thread marks one member's neighbours (the adjacency loads of
-    // all members in flight at once)
+    // mark nb[t] = stamp for every site t adjacent to a member of zone z: every thread marks the
+    // neighbours of the members among its own sites (a zone's members rarely share a thread's KT
+    // sites, so the adjacency loads of all members are in flight at once; marking is idempotent,
+    // so no compaction of the members and no barrier before the marks)
     auto mark = [&](int z) {
         stamp++;
         if (stamp == 0) {  // wrapped: clear
@@ -393,17 +394,20 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
             bsync();
             stamp = 1;
         }
-        const int nmem = compact_sel(SEL_ZONE, z);
-        for (int i = tid; i < nmem; i += NT) {
-            const int s = lst[i];
-            const int e0 = a.adj_ptr[s], e1 = a.adj_ptr[s + 1];
-            for (int e = e0; e < e1; e += 8) {
-                int t[8];
+        for (int c = 0; c < nsc; c++) {
+            uint32_t m = scan_mask(SEL_ZONE, z, c);
+            while (m) {
+                const int s = c * CH + tid * KT + (int)__builtin_ctz(m);
+                m &= m - 1;
+                const int e0 = a.adj_ptr[s], e1 = a.adj_ptr[s + 1];
+                for (int e = e0; e < e1; e += 8) {
+                    int t[8];
 #pragma unroll
-                for (int k = 0; k < 8; k++) t[k] = a.adj_idx[MH_IDX(min(e + k, e1 - 1), a.nnz, 1)];
+                    for (int k = 0; k < 8; k++) t[k] = a.adj_idx[MH_IDX(min(e + k, e1 - 1), a.nnz, 1)];
 #pragma unroll
-                for (int k = 0; k < 8; k++)
-                    if (e + k < e1) nb[MH_IDX(t[k], N, 2)] = stamp;
+                    for (int k = 0; k < 8; k++)
+                        if (e + k < e1) nb[MH_IDX(t[k], N, 2)] = stamp;
+                }
             }
         }
         bsync();
