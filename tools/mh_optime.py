@@ -86,6 +86,15 @@ def main():
         if a.stamps:
             cyc, op = out["ll"].cpu().numpy(), out["op"].cpu().numpy()
             res[name]["cycles_by_op"] = {int(o): round(float(cyc[op == o].mean())) for o in np.unique(op)}
+            # a group's members carry the same (split) stamp: runs of equal values = group sizes
+            sizes = []
+            for c in range(cyc.shape[0]):
+                v = cyc[c]
+                brk = np.flatnonzero(np.diff(v) != 0) + 1
+                sizes.extend(np.diff(np.concatenate([[0], brk, [len(v)]])).tolist())
+            h = np.bincount(np.minimum(sizes, 9))
+            res[name]["run_sizes"] = {int(i): int(n) for i, n in enumerate(h) if n}
+            res[name]["cycles_per_step_mean"] = round(float(cyc.mean()))
         print(name, res[name], flush=True)
     print(json.dumps(res))
 
