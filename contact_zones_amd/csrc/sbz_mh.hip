@@ -549,9 +549,9 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
     // changed entries are exactly the cells the reference recomputes: every cell for the weights
     // (the slot's dense table, rewritten whole), states ia / ib of the component's rows otherwise
     // (the slot's sparse table, 1.0 everywhere else: only the 2 x rows changed entries are written,
-    // and reset to 1.0 after the gathers).  A sparse move reads only the positions its entries can
-    // apply to (state ia / ib; the zone's rows for p_zones; the family's position range for
-    // p_families, families being contiguous in the position order); the others multiply 1.
+    // and reset to 1.0 after the gathers).  A p_families move reads only its family's position
+    // range (families are contiguous in the position order); every other position there, and of
+    // the other moves, reads its entry, 1.0 where the move changes nothing.
 #ifdef SBZ_MH_STAMP
     double stamp_dp = 0.0;  // phase cycles of the last delta_param (SBZ_MH_STAMP 4 / 5 / 6)
 #endif
@@ -567,15 +567,10 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
         const bool dense = comp == 3;
         double *tab = wtab + (size_t)wvu * 2 * nent + (dense ? 0 : nent);
         // positions the move's entries can apply to: [p_lo, p_hi) (a family's range for p_families)
-        // and class rows [c_lo, c_lo + c_span) (bytes; the zone's rows for p_zones)
         int p_lo = 0, p_hi = a.Np;
-        uint32_t c_lo = 0, c_span = (uint32_t)(ncls * row_bytes);
         if (comp == 2) {
             p_lo = uni(fpr[2 * (row + 1)]);
             p_hi = uni(fpr[2 * (row + 1) + 1]);
-        } else if (comp == 1) {
-            c_lo = (uint32_t)((row + 1) * FamC * row_bytes);
-            c_span = (uint32_t)(FamC * row_bytes);
         }
         const int k_lo = p_lo / 256, k_hi = p_hi > p_lo ? (p_hi + 255) / 256 : k_lo;  // chunks
         // the feature's observation words, all in flight during the table build
@@ -645,16 +640,16 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
         const long long dt_tb = clock64();
 #endif
         // gathers: position p = 256 k + 4 lane + j of chunk k, two chunks (8 positions per lane)
-        // at a time.  Dense: all 8 table reads issued together; sparse: a read only where the
-        // position's state is ia / ib and its class row / position is the move's (a branch per
-        // position, skipped when no lane needs it).  Safe factors (within 2^+-120): the 8 multiply
-        // as a tree, one renormalisation per pair of chunks; otherwise renormalise after every
-        // factor.
+        // at a time, all 8 table reads issued together.  A sparse move's table holds 1.0 wherever
+        // the move changes nothing, so every position of its chunk range reads its entry as a dense
+        // move does: the product is the same as reading only the changed entries (round 6: no
+        // branch per position, 2.97 -> 2.89 us per step of the cfg5 default mix,
+        // profiles/r06_mh_sparse_ab.txt).  Safe factors (within 2^+-120): the 8 multiply as a
+        // tree, one renormalisation per pair of chunks; otherwise renormalise after every factor.
         double m = 1.0;
         int e = 0;
         const unsigned char *tb = reinterpret_cast<const unsigned char *>(tab);
         const uint32_t xsh = a.xs8 ? 0u : 3u;
-        const uint32_t xa = (uint32_t)ia << (3 - xsh), xbv = (uint32_t)ib << (3 - xsh);  // obs byte of ia / ib
         for (int b0 = k_lo; b0 < k_hi; b0 += OBW) {
             if (b0 > k_lo) {
 #pragma unroll
@@ -670,22 +665,10 @@ __global__ __launch_bounds__(NWV * 64) void mh_kernel(MhArgs a) {
                 const uint32_t oa = o[j], ob = o[j + 1];
                 const uint32_t r8[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
                 double v[8];
-                if (dense) {
 #pragma unroll
-                    for (int q = 0; q < 8; q++) {
-                        const uint32_t xb = ((q < 4 ? oa : ob) >> (8 * (q & 3))) & 0xffu;
-                        v[q] = *reinterpret_cast<const double *>(tb + r8[q] + (xb << xsh));
-                    }
-                } else {
-#pragma unroll
-                    for (int q = 0; q < 8; q++) {
-                        const uint32_t xb = ((q < 4 ? oa : ob) >> (8 * (q & 3))) & 0xffu;
-                        const int pq = (q < 4 ? i0 : i0 + 1) * 256 + 4 * lane + (q & 3);
-                        const bool need = (xb == xa || xb == xbv) && (r8[q] - c_lo) < c_span &&
-                                          (uint32_t)(pq - p_lo) < (uint32_t)(p_hi - p_lo);
-                        v[q] = 1.0;
-                        if (need) v[q] = lds_rd(reinterpret_cast<const double *>(tb + r8[q] + (xb << xsh)));
-                    }
+                for (int q = 0; q < 8; q++) {
+                    const uint32_t xb = ((q < 4 ? oa : ob) >> (8 * (q & 3))) & 0xffu;
+                    v[q] = *reinterpret_cast<const double *>(tb + r8[q] + (xb << xsh));
                 }
                 if (!two) {
 #pragma unroll
