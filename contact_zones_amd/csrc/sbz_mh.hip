@@ -1,6 +1,6 @@
 // sbz_mh.hip — batched Metropolis-Hastings for the sBayes zone model on CDNA4 (gfx950).
 //
-// One workgroup of 4 waves (one per SIMD of a CU) runs one chain for n_steps without leaving the
+// One workgroup of 8 waves (two per SIMD of a CU) runs one chain for n_steps without leaving the
 // kernel:
 // MCMCGenerative.step (sbayes/sampling/mcmc_generative.py:282-351) with the operators of
 // ZoneMCMC / ZoneMCMCWarmup (sbayes/sampling/zone_sampling.py) for SAMPLE_SOURCE = false; priors
@@ -11,8 +11,8 @@
 //   dirichlet_proposal :537-569 (q = exp(scipy dirichlet._logpdf) then log)
 //   gibbsish_sample_zones :619-702 (warm-up :1323-1326; weight 0 in the reference's own table,
 //   mcmc_setup.py:77, so it runs only when a caller gives it a weight)
-// Every decision is uniform: all lanes of all 4 waves draw the same values and take the same
-// branches; the 256 threads share the per-site / per-feature work.
+// Every decision is uniform: all lanes of all the waves draw the same values and take the same
+// branches; the 512 threads share the per-site / per-feature work.
 //
 // State: the chain's zone assignment lives in LDS for the whole run (written back at the end);
 // parameters stay in HBM and are updated in place on acceptance.  The log-likelihood is updated
@@ -134,7 +134,7 @@ __device__ __forceinline__ void bsync() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-// One chain per workgroup of NWV waves (one per SIMD of the CU).  Every wave runs the same
+// One chain per workgroup of NWV waves (8: two per SIMD of the CU).  Every wave runs the same
 // control flow: all draws and decisions are computed redundantly and identically by every wave
 // (wave-uniform, from the same LDS / HBM state), and the per-site / per-feature work of a step is
 // split over all NWV * 64 threads, with block reductions in a fixed order (deterministic).

@@ -22,9 +22,10 @@
 //                                      operator table (mcmc_setup.py:77)
 // The Gibbs operators return Q_GIBBS (log q = -inf): always accepted.
 //
-// One wave runs one chain.  The chain's sources (N x F bytes, current and candidate), zone
-// assignment and counters live in LDS for the whole launch; every operator is a few
-// lane-parallel passes over the N*F observations (per observation: the normalised weights and
+// One workgroup of NW waves (8 by default) runs one chain.  The chain's sources (N x F bytes,
+// current and candidate), zone assignment and counters live in LDS for the whole launch where they
+// fit, in HBM by position with per-chain count tables otherwise (the table-pass kernel, cfg5);
+// every operator is a few lane-parallel passes over the N*F observations (per observation: the normalised weights and
 // component likelihoods in the reference's operation order, the posterior, the categorical draw,
 // the source-branch log-likelihood log(w_src * lh_src), model.py:177-184).  Draws come from the
 // replay tape (the reference's own decisions) or from Philox: uniform decisions from the wave's
